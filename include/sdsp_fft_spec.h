@@ -1,0 +1,78 @@
+/*
+ * sdsp_fft_spec.h — the arithmetic specification of every FFT on the analyze_audio path.
+ *
+ * The reference computes all FFTs with rustfft "6.2" (Cargo.toml:18; call sites
+ * src/features/chroma/extractor.rs:326-346, src/features/period/tempogram_fft.rs:149-151,
+ * src/features/period/autocorrelation.rs:240-251).  rustfft's planner picks an
+ * implementation-defined algorithm and SIMD path, so the reference does not pin the
+ * rounding of its FFT outputs ("parity unpinned").  sdsp pins it:
+ *
+ *   complex FFT, size M = 2^m, forward (e^{-2 pi i jk/M}), no scaling:
+ *     Stockham autosort, decimation in frequency, radix-4 stages while the current
+ *     sub-transform length n >= 4, then one radix-2 stage if n == 2.  One radix-4 stage
+ *     with stride s (s = 1, 4, 16, ...) and m = n/4, for p < m, q < s:
+ *        a = x[q + s(p)],  b = x[q + s(p+m)],  c = x[q + s(p+2m)],  d = x[q + s(p+3m)]
+ *        apc = a + c;  amc = a - c;  bpd = b + d;  bmd = b - d
+ *        jbmd = (bmd.im, -bmd.re)                     (-i * (b - d))
+ *        y[q + s(4p+0)] = apc + bpd
+ *        y[q + s(4p+1)] = W^{1p} * (amc + jbmd)
+ *        y[q + s(4p+2)] = W^{2p} * (apc - bpd)
+ *        y[q + s(4p+3)] = W^{3p} * (amc - jbmd)
+ *     with W^{kp} = tw[k*p*(M/n)] from the M-point table below, and the complex product
+ *        (w * z) = (w.re*z.re - w.im*z.im,  w.re*z.im + w.im*z.re)   (two roundings each,
+ *        no FMA).  Radix-2 stage (n == 2): y[q] = x[q] + x[q+s]; y[q+s] = x[q] - x[q+s].
+ *
+ *   real-input FFT of size N = 2M: z[j] = (x[2j], x[2j+1]); Z = FFT_M(z); for k = 0..M:
+ *        Zk = Z[k mod M]; Zc = conj(Z[(M-k) mod M])
+ *        E = ((Zk.re + Zc.re)*0.5, (Zk.im + Zc.im)*0.5)
+ *        D = Zk - Zc;  O = (D.im*0.5, -(D.re*0.5))
+ *        X[k] = E + rt[k] * O,  rt[k] = e^{-2 pi i k/N}
+ *     |X[k]| = sqrt(X.re*X.re + X.im*X.im);  power = X.re*X.re + X.im*X.im.
+ *
+ * Twiddles are cos/sin evaluated in double by sdsp_libm and rounded once to f32.  Both the
+ * CPU restatement (oracle/) and the HIP kernels implement exactly this operation order, so
+ * their spectra agree bit for bit; tests/test_oracle_fft.py checks the specification
+ * against numpy's float64 FFT (relative error <= 2e-6 of the frame's peak).
+ */
+#ifndef SDSP_FFT_SPEC_H
+#define SDSP_FFT_SPEC_H
+
+#include "sdsp_libm.h"
+
+#define SD_TWO_PI_D 6.28318530717958647692e+00
+#define SD_PIO2_D 1.57079632679489661923e+00
+
+/* tw[j] = e^{-2 pi i j / M}, j = 0..M-1, as interleaved (re, im) f32 pairs */
+static inline void sdsp_fft_twiddles(int M, float* tw_interleaved) {
+    for (int j = 0; j < M; j++) {
+        double th = SD_TWO_PI_D * (double)j / (double)M;
+        double c = sd_cos_d(th);
+        double s = sd_cos_d(th - SD_PIO2_D); /* sin(th) */
+        tw_interleaved[2 * j] = (float)c;
+        tw_interleaved[2 * j + 1] = (float)(-s);
+    }
+}
+
+/* rt[k] = e^{-2 pi i k / N}, k = 0..N/2, as interleaved (re, im) f32 pairs */
+static inline void sdsp_rfft_twiddles(int N, float* rt_interleaved) {
+    for (int k = 0; k <= N / 2; k++) {
+        double th = SD_TWO_PI_D * (double)k / (double)N;
+        double c = sd_cos_d(th);
+        double s = sd_cos_d(th - SD_PIO2_D);
+        rt_interleaved[2 * k] = (float)c;
+        rt_interleaved[2 * k + 1] = (float)(-s);
+    }
+}
+
+/*
+ * Symmetric Hann window exactly as extractor.rs:318-323 / tempogram_fft.rs:122-128:
+ *   x = 2.0 * PI * i as f32 / (n - 1) as f32;  w = 0.5 * (1.0 - x.cos())
+ * (all f32 operations, left to right).
+ */
+static inline float sdsp_hann_f32(int i, int n) {
+    const float PI_F = 3.14159265358979323846f;
+    float x = 2.0f * PI_F * (float)i / (float)(n - 1);
+    return 0.5f * (1.0f - sd_cosf(x));
+}
+
+#endif /* SDSP_FFT_SPEC_H */

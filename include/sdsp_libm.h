@@ -1,0 +1,289 @@
+/*
+ * sdsp_libm.h — the f32 transcendental contract shared by every sdsp compute path.
+ *
+ * Why this exists
+ * ---------------
+ * The reference (stratum-dsp, Rust) evaluates `f32::ln`, `exp`, `powf`, `cos`, `log10`,
+ * `log2`, `exp2` through whatever libm the Rust std links (glibc on Linux, the MSVC CRT
+ * on Windows, where its published numbers were taken).  Those results are therefore not
+ * pinned by the reference itself (SURVEY.md §8c "Third-party arithmetic").  glibc 2.35's
+ * f32 routines are also not correctly rounded: measured in this container, `logf`
+ * differs from the correctly rounded value on ~0.1% of inputs and `cosf` on ~1.3% of
+ * Hann-window arguments.
+ *
+ * sdsp pins them instead: every function below evaluates in IEEE double using only
+ * + - * / and exact bit manipulation (no libm, no FMA: build with -ffp-contract=off), and
+ * rounds once to f32.  The results are correctly rounded except within ~1e-7 of a
+ * rounding midpoint, and — more importantly — they are *bit-identical* on the x86 host
+ * and on gfx950, so the CPU restatement in oracle/ and the HIP kernels agree bit for bit
+ * wherever they perform the same arithmetic.
+ *
+ * `powf(x, 2)` is special-cased to `x*x`: glibc's powf(x, 2.0f) equalled x*x on every one
+ * of 3.0e8 sampled f32 inputs (tests/test_libm.py), and the harmonic mask
+ * (extractor.rs:1337-1347) evaluates it 2×63.5 M times per 3-min track.
+ */
+#ifndef SDSP_LIBM_H
+#define SDSP_LIBM_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#define SD_HD __host__ __device__ inline
+#else
+#define SD_HD static inline
+#endif
+
+SD_HD uint64_t sd_bits_d(double d) {
+    uint64_t u;
+    __builtin_memcpy(&u, &d, 8);
+    return u;
+}
+SD_HD double sd_from_bits_d(uint64_t u) {
+    double d;
+    __builtin_memcpy(&d, &u, 8);
+    return d;
+}
+SD_HD uint32_t sd_bits_f(float f) {
+    uint32_t u;
+    __builtin_memcpy(&u, &f, 4);
+    return u;
+}
+SD_HD float sd_from_bits_f(uint32_t u) {
+    float f;
+    __builtin_memcpy(&f, &u, 4);
+    return f;
+}
+
+SD_HD int sd_isnan_f(float x) { return x != x; }
+SD_HD int sd_isfinite_f(float x) { return (sd_bits_f(x) & 0x7f800000u) != 0x7f800000u; }
+
+#define SD_INF_F (sd_from_bits_f(0x7f800000u))
+#define SD_NAN_F (sd_from_bits_f(0x7fc00000u))
+#define SD_INF_D (sd_from_bits_d(0x7ff0000000000000ull))
+
+/* ln2 split so that k*LN2_HI is exact for |k| < 2^11 */
+#define SD_LN2_HI 6.93147180369123816490e-01 /* 0x3fe62e42fee00000 */
+#define SD_LN2_LO 1.90821492927058770002e-10 /* 0x3dea39ef35793c76 */
+#define SD_INV_LN2 1.44269504088896338700e+00
+#define SD_LN10 2.30258509299404590109e+00
+#define SD_SQRT2 1.41421356237309514547e+00
+
+/* natural log of a positive, finite, normal double (every f32 > 0 is one) */
+SD_HD double sd_log_d(double x) {
+    uint64_t u = sd_bits_d(x);
+    int e = (int)((u >> 52) & 0x7ff) - 1023;
+    double m = sd_from_bits_d((u & 0x000fffffffffffffull) | 0x3ff0000000000000ull);
+    if (m > SD_SQRT2) {
+        m = m * 0.5;
+        e = e + 1;
+    }
+    double f = m - 1.0;
+    double s = f / (2.0 + f);
+    double z = s * s;
+    /* log(m) = 2 atanh(s) = 2 (s + s^3/3 + s^5/5 + ...), |s| <= 0.1716 */
+    double p = 1.0 / 23.0;
+    p = 1.0 / 21.0 + z * p;
+    p = 1.0 / 19.0 + z * p;
+    p = 1.0 / 17.0 + z * p;
+    p = 1.0 / 15.0 + z * p;
+    p = 1.0 / 13.0 + z * p;
+    p = 1.0 / 11.0 + z * p;
+    p = 1.0 / 9.0 + z * p;
+    p = 1.0 / 7.0 + z * p;
+    p = 1.0 / 5.0 + z * p;
+    p = 1.0 / 3.0 + z * p;
+    double two_s = 2.0 * s;
+    double r = two_s + two_s * (z * p);
+    double ed = (double)e;
+    return ed * SD_LN2_HI + (ed * SD_LN2_LO + r);
+}
+
+/* e^x for finite double x */
+SD_HD double sd_exp_d(double x) {
+    if (x != x) return x;
+    if (x > 709.0) return SD_INF_D;
+    if (x < -745.0) return 0.0;
+    double t = x * SD_INV_LN2 + 0.5;
+    /* floor without libm: |t| < 1100 */
+    double kd = (double)(int64_t)t;
+    if (kd > t) kd = kd - 1.0;
+    double r = (x - kd * SD_LN2_HI) - kd * SD_LN2_LO; /* |r| <= ~0.347 */
+    double p = 1.0 / 6227020800.0;                      /* 1/13! */
+    p = 1.0 / 479001600.0 + r * p;                      /* 1/12! */
+    p = 1.0 / 39916800.0 + r * p;                       /* 1/11! */
+    p = 1.0 / 3628800.0 + r * p;
+    p = 1.0 / 362880.0 + r * p;
+    p = 1.0 / 40320.0 + r * p;
+    p = 1.0 / 5040.0 + r * p;
+    p = 1.0 / 720.0 + r * p;
+    p = 1.0 / 120.0 + r * p;
+    p = 1.0 / 24.0 + r * p;
+    p = 1.0 / 6.0 + r * p;
+    p = 0.5 + r * p;
+    p = 1.0 + r * p;
+    p = 1.0 + r * p;
+    int k = (int)kd;
+    if (k < -1000) {
+        /* scale in two steps to stay in the normal range of the intermediate */
+        p = p * sd_from_bits_d((uint64_t)(1023 - 600) << 52);
+        k = k + 600;
+    }
+    if (k > 1023) return SD_INF_D;
+    return p * sd_from_bits_d((uint64_t)(k + 1023) << 52);
+}
+
+/* cos of a finite double with |x| < 2^20, via Cody-Waite reduction by pi/2 */
+SD_HD double sd_cos_d(double x) {
+    const double PIO2_HI = 1.57079632673412561417e+00; /* 0x3ff921fb54400000 */
+    const double PIO2_LO = 6.07710050650619224932e-11; /* 0x3dd0b4611a626331 */
+    const double TWO_OVER_PI = 6.36619772367581382433e-01;
+    double t = x * TWO_OVER_PI;
+    double kd = (double)(int64_t)(t >= 0.0 ? t + 0.5 : t - 0.5);
+    double r = (x - kd * PIO2_HI) - kd * PIO2_LO; /* |r| <= ~pi/4 */
+    double z = r * r;
+    /* cos(r) = 1 - z(1/2! - z(1/4! - z(1/6! - ...))) */
+    double c = 1.0 / 6402373705728000.0; /* 1/18! */
+    c = 1.0 / 20922789888000.0 - z * c;  /* 1/16! */
+    c = 1.0 / 87178291200.0 - z * c;     /* 1/14! */
+    c = 1.0 / 479001600.0 - z * c;       /* 1/12! */
+    c = 1.0 / 3628800.0 - z * c;         /* 1/10! */
+    c = 1.0 / 40320.0 - z * c;           /* 1/8!  */
+    c = 1.0 / 720.0 - z * c;
+    c = 1.0 / 24.0 - z * c;
+    c = 0.5 - z * c;
+    double cosr = 1.0 - z * c;
+    /* sin(r) = r - r z(1/3! - z(1/5! - z(1/7! - ...))) */
+    double s = 1.0 / 121645100408832000.0; /* 1/19! */
+    s = 1.0 / 355687428096000.0 - z * s;   /* 1/17! */
+    s = 1.0 / 1307674368000.0 - z * s;     /* 1/15! */
+    s = 1.0 / 6227020800.0 - z * s;        /* 1/13! */
+    s = 1.0 / 39916800.0 - z * s;          /* 1/11! */
+    s = 1.0 / 362880.0 - z * s;            /* 1/9!  */
+    s = 1.0 / 5040.0 - z * s;
+    s = 1.0 / 120.0 - z * s;
+    s = 1.0 / 6.0 - z * s;
+    double sinr = r - r * (z * s);
+    int q = (int)((int64_t)kd & 3);
+    if (q == 0) return cosr;
+    if (q == 1) return -sinr;
+    if (q == 2) return -cosr;
+    return sinr;
+}
+
+/* ---- f32 entry points (the Rust f32 method each one stands in for) ---- */
+
+/* f32::ln */
+SD_HD float sd_logf(float x) {
+    if (x != x) return x;
+    if (x < 0.0f) return SD_NAN_F;
+    if (x == 0.0f) return -SD_INF_F;
+    if (!sd_isfinite_f(x)) return x;
+    return (float)sd_log_d((double)x);
+}
+
+/* f32::log10 */
+SD_HD float sd_log10f(float x) {
+    if (x != x) return x;
+    if (x < 0.0f) return SD_NAN_F;
+    if (x == 0.0f) return -SD_INF_F;
+    if (!sd_isfinite_f(x)) return x;
+    return (float)(sd_log_d((double)x) / SD_LN10);
+}
+
+/* f32::log2 */
+SD_HD float sd_log2f(float x) {
+    if (x != x) return x;
+    if (x < 0.0f) return SD_NAN_F;
+    if (x == 0.0f) return -SD_INF_F;
+    if (!sd_isfinite_f(x)) return x;
+    return (float)(sd_log_d((double)x) * SD_INV_LN2);
+}
+
+/* f32::exp */
+SD_HD float sd_expf(float x) {
+    if (x != x) return x;
+    return (float)sd_exp_d((double)x);
+}
+
+/* f32::exp2 */
+SD_HD float sd_exp2f(float x) {
+    if (x != x) return x;
+    return (float)sd_exp_d((double)x * SD_LN2_HI + (double)x * SD_LN2_LO);
+}
+
+/* f32::cos, valid for |x| < 2^20 (window and tempogram arguments are in [0, 2*pi]) */
+SD_HD float sd_cosf(float x) {
+    if (x != x) return x;
+    return (float)sd_cos_d((double)x);
+}
+
+/* f32::powf (IEEE special cases for the operand ranges the pipeline produces) */
+SD_HD float sd_powf(float x, float y) {
+    if (y == 2.0f) return x * x; /* == glibc powf(x, 2) on 3.0e8 sampled inputs */
+    if (y == 1.0f) return x;
+    if (y == 0.0f) return 1.0f;
+    if (x != x || y != y) return SD_NAN_F;
+    if (x == 1.0f) return 1.0f;
+    if (x == 0.0f) return y > 0.0f ? 0.0f : SD_INF_F;
+    if (x < 0.0f) {
+        /* integral y keeps the sign pattern; otherwise NaN (matches powf) */
+        float yi = (float)(int64_t)y;
+        if (yi != y) return SD_NAN_F;
+        float r = (float)sd_exp_d((double)y * sd_log_d(-(double)x));
+        int64_t yl = (int64_t)y;
+        return (yl & 1) ? -r : r;
+    }
+    if (!sd_isfinite_f(x)) return y > 0.0f ? SD_INF_F : 0.0f;
+    return (float)sd_exp_d((double)y * sd_log_d((double)x));
+}
+
+/* f32::rem_euclid */
+SD_HD float sd_rem_euclid_f(float x, float m) {
+    float r = __builtin_fmodf(x, m);
+    if (r < 0.0f) r = r + (m < 0.0f ? -m : m);
+    return r;
+}
+
+/* f32::max / f32::min: NaN operands are ignored (Rust semantics) */
+SD_HD float sd_maxf(float a, float b) {
+    if (a != a) return b;
+    if (b != b) return a;
+    return a > b ? a : b;
+}
+SD_HD float sd_minf(float a, float b) {
+    if (a != a) return b;
+    if (b != b) return a;
+    return a < b ? a : b;
+}
+SD_HD float sd_clampf(float x, float lo, float hi) {
+    /* f32::clamp: NaN stays NaN */
+    if (x < lo) x = lo;
+    if (x > hi) x = hi;
+    return x;
+}
+SD_HD float sd_absf(float x) { return sd_from_bits_f(sd_bits_f(x) & 0x7fffffffu); }
+
+/* `f32 as usize` / `as i32`: saturating, NaN -> 0 */
+SD_HD uint64_t sd_f2u64(float x) {
+    if (!(x > 0.0f)) return 0;
+    if (x >= 18446744073709551616.0f) return ~0ull;
+    return (uint64_t)x;
+}
+SD_HD int32_t sd_f2i32(float x) {
+    if (x != x) return 0;
+    if (x >= 2147483648.0f) return 2147483647;
+    if (x <= -2147483648.0f) return (-2147483647 - 1);
+    return (int32_t)x;
+}
+SD_HD int64_t sd_f2i64(float x) {
+    if (x != x) return 0;
+    if (x >= 9223372036854775808.0f) return 9223372036854775807ll;
+    if (x <= -9223372036854775808.0f) return (-9223372036854775807ll - 1);
+    return (int64_t)x;
+}
+
+/* f32::round: half away from zero (exact) */
+SD_HD float sd_roundf(float x) { return __builtin_roundf(x); }
+
+#endif /* SDSP_LIBM_H */

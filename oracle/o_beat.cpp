@@ -1,0 +1,320 @@
+// o_beat.cpp — beat grid (TEST INFRASTRUCTURE, see oracle_internal.hpp).
+//
+// Follows src/features/beat_tracking/{mod.rs:108-485, hmm.rs:121-441, tempo_variation.rs:95-227,
+// bayesian.rs:77-272, time_signature.rs:90-199}.
+#include <algorithm>
+#include <array>
+
+#include "oracle_internal.hpp"
+
+namespace orc {
+
+struct BeatPos {
+    float t, conf;
+};
+
+// hmm.rs:121-441.  The Viterbi pass is run faithfully, but note that the
+// emission is state-independent, so the extracted beats never depend on the path.
+static bool hmm_track(float bpm, const std::vector<float>& on, std::vector<BeatPos>* out) {
+    if (bpm <= EPS || bpm > 300.0f) return false;  // InvalidInput
+    if (on.empty()) return false;
+    const float start = on[0], end = on.back();
+    const float interval = 60.0f / bpm;
+    const size_t nf = (size_t)sd_f2u64(__builtin_ceilf((end - start) / interval)) + 1;
+    const float sigma = 0.05f / 2.0f;
+    const float sigma_sq = sigma * sigma;
+    std::vector<float> emis(nf);
+    for (size_t t = 0; t < nf; t++) {
+        const float ft = start + ((float)t * interval);
+        float md = SD_INF_F;
+        for (float o : on) {
+            const float d = sd_absf(o - ft);
+            if (d < md) md = d;
+        }
+        const float dsq = md * md;
+        emis[t] = sd_expf(-dsq / (2.0f * sigma_sq));  // identical for all 5 states
+    }
+    // transition matrix (hmm.rs:184-219), rows normalized
+    float T[5][5];
+    for (int i = 0; i < 5; i++) {
+        float sum = 0.0f;
+        for (int j = 0; j < 5; j++) {
+            const int d = i > j ? i - j : j - i;
+            T[i][j] = d == 0 ? 0.7f : d == 1 ? 0.15f : 0.0f;
+            sum += T[i][j];
+        }
+        if (sum > EPS)
+            for (int j = 0; j < 5; j++) T[i][j] /= sum;
+    }
+    // Viterbi (hmm.rs:308-375)
+    std::vector<float> v(5), nv(5);
+    std::vector<std::array<int, 5>> bp(nf);
+    for (int s = 0; s < 5; s++) v[s] = (1.0f / 5.0f) * emis[0];
+    for (size_t t = 1; t < nf; t++) {
+        for (int s = 0; s < 5; s++) {
+            float best = 0.0f;
+            int bs = 0;
+            for (int ps = 0; ps < 5; ps++) {
+                const float p = v[ps] * T[ps][s];
+                if (p > best) {
+                    best = p;
+                    bs = ps;
+                }
+            }
+            nv[s] = best * emis[t];
+            bp[t][s] = bs;
+        }
+        v.swap(nv);
+    }
+    // (path irrelevant to the output; extract beats, hmm.rs:383-441)
+    out->clear();
+    for (size_t t = 0; t < nf; t++) {
+        const float e = emis[t];
+        if (e > 0.1f) {
+            const float bt = start + ((float)t * interval);
+            float md = SD_INF_F;
+            for (float o : on) {
+                const float d = sd_absf(o - bt);
+                if (d < md) md = d;
+            }
+            const float align = md < 0.05f ? 1.0f - (md / 0.05f) : 0.0f;
+            out->push_back({bt, sd_minf(e * 0.7f + align * 0.3f, 1.0f)});
+        }
+    }
+    std::stable_sort(out->begin(), out->end(), [](auto& a, auto& b) { return a.t < b.t; });
+    return true;
+}
+
+struct Seg {
+    float start, end, bpm, conf;
+    bool variable;
+};
+
+// tempo_variation.rs:95-227
+static std::vector<Seg> tempo_variations(const std::vector<float>& b, float nominal) {
+    if (b.size() < 4) return {{b.empty() ? 0.0f : b[0], b.empty() ? 0.0f : b.back(), nominal, 0.5f, false}};
+    if (nominal <= EPS) fail(SDSP_ERR_INVALID_INPUT, "Invalid nominal BPM");
+    const float total = b.back() - b[0];
+    if (total < 2.0f) return {{b[0], b.back(), nominal, 0.8f, false}};
+    const float seg_dur = sd_clampf(total / 4.0f, 4.0f, 8.0f);
+    const float overlap = seg_dur * 0.5f;
+    std::vector<Seg> segs;
+    float cur = b[0];
+    while (cur < b.back()) {
+        const float se = sd_minf(cur + seg_dur, b.back());
+        std::vector<float> sb;
+        for (float x : b)
+            if (x >= cur && x <= se) sb.push_back(x);
+        if (sb.size() >= 3) {
+            std::vector<float> iv;
+            for (size_t i = 1; i < sb.size(); i++) {
+                const float d = sb[i] - sb[i - 1];
+                if (d > 0.0f) iv.push_back(d);
+            }
+            if (!iv.empty()) {
+                float sum = 0.0f;
+                for (float x : iv) sum += x;
+                const float mean = sum / (float)iv.size();
+                float vs = 0.0f;
+                for (float x : iv) {
+                    const float d = x - mean;
+                    vs += d * d;
+                }
+                const float var = vs / (float)iv.size();
+                const float sd = __builtin_sqrtf(var);
+                const float cv = mean > EPS ? sd / mean : 0.0f;
+                const float sbpm = mean > EPS ? 60.0f / mean : nominal;
+                const float conf = sd_maxf(1.0f - sd_minf(cv / 0.3f, 1.0f), 0.0f);
+                segs.push_back({cur, se, sbpm, conf, cv > 0.15f});
+            }
+        }
+        cur += seg_dur - overlap;
+    }
+    if (segs.empty()) segs.push_back({b[0], b.back(), nominal, 0.8f, false});
+    return segs;
+}
+
+// bayesian.rs:104-272 (tracker state carried across segments)
+struct Bayes {
+    float bpm, conf;
+};
+static void bayes_update(Bayes& st, const std::vector<float>& on, float* out_bpm) {
+    if (on.empty()) fail(SDSP_ERR_INVALID_INPUT, "Cannot update: no onsets provided");
+    if (st.bpm <= EPS || st.bpm > 300.0f) fail(SDSP_ERR_INVALID_INPUT, "Invalid current BPM");
+    std::vector<float> cands;
+    const float lo = sd_maxf(st.bpm - 5.0f, 60.0f), hi = sd_minf(st.bpm + 5.0f, 180.0f);
+    for (float b = lo; b <= hi; b += 0.5f) cands.push_back(b);
+    float best_bpm = st.bpm, best_l = 0.0f;
+    for (float cb : cands) {
+        if (cb <= EPS) fail(SDSP_ERR_INVALID_INPUT, "Invalid BPM for likelihood");
+        const float bi = 60.0f / cb;
+        const float st0 = on[0];
+        float ll = 0.0f;
+        int32_t valid = 0;
+        const float sig_sq = 0.05f * 0.05f;
+        for (float o : on) {
+            const int32_t idx = sd_f2i32(sd_roundf((o - st0) / bi));
+            const float exp_t = st0 + ((float)idx * bi);
+            const float d = sd_absf(o - exp_t);
+            const float dsq = d * d;
+            ll += -dsq / (2.0f * sig_sq);
+            valid++;
+        }
+        const float lik = valid == 0 ? 0.0f : sd_expf(ll / (float)valid);
+        if (lik > best_l) {
+            best_l = lik;
+            best_bpm = cb;
+        }
+    }
+    const float old = st.bpm;
+    st.bpm = best_bpm;
+    const float ch = sd_absf(best_bpm - old);
+    const float pen = ch < 1.0f ? 1.0f : ch < 3.0f ? 0.8f : 0.5f;
+    st.conf = sd_minf(best_l * pen, 1.0f);
+    *out_bpm = st.bpm;
+}
+
+// time_signature.rs:161-199
+static float score_ts(const std::vector<float>& iv, uint32_t bpb, float mean) {
+    if (iv.size() < bpb) return 0.0f;
+    const size_t lag = bpb;
+    float acc = 0.0f;
+    int32_t cnt = 0;
+    for (size_t i = 0; i + lag < iv.size(); i++) {
+        const float d = sd_absf(iv[i] - iv[i + lag]);
+        acc += 1.0f / (1.0f + d / mean);
+        cnt++;
+    }
+    if (cnt == 0) return 0.0f;
+    const float ac = acc / (float)cnt;
+    float vs = 0.0f;
+    for (float x : iv) {
+        const float d = x - mean;
+        vs += d * d;
+    }
+    const float var = vs / (float)iv.size();
+    const float cv = mean > EPS ? __builtin_sqrtf(var) / mean : 1.0f;
+    const float cons = 1.0f / (1.0f + cv);
+    return sd_minf(ac * 0.7f + cons * 0.3f, 1.0f);
+}
+
+// time_signature.rs:90-149 -> beats per bar
+static uint32_t time_signature(const std::vector<float>& b, float bpm) {
+    if (b.size() < 8) return 4;
+    if (bpm <= EPS) fail(SDSP_ERR_INVALID_INPUT, "Invalid BPM for time signature detection");
+    std::vector<float> iv;
+    for (size_t i = 1; i < b.size(); i++) {
+        const float d = b[i] - b[i - 1];
+        if (d > 0.0f) iv.push_back(d);
+    }
+    if (iv.empty()) return 4;
+    float sum = 0.0f;
+    for (float x : iv) sum += x;
+    const float mean = sum / (float)iv.size();
+    const float s44 = score_ts(iv, 4, mean), s34 = score_ts(iv, 3, mean), s68 = score_ts(iv, 6, mean);
+    // max_by with partial_cmp: the LAST maximum wins
+    uint32_t best = 4;
+    float bs = s44;
+    if (!(s34 < bs)) {
+        best = 3;
+        bs = s34;
+    }
+    if (!(s68 < bs)) {
+        best = 6;
+        bs = s68;
+    }
+    return best;
+}
+
+// beat_tracking/mod.rs:108-247 (+ downbeats :363-404, stability :425-485)
+bool generate_beat_grid(float bpm, float conf, const std::vector<float>& onsets_s, uint32_t sr,
+                        std::vector<float>* beats_out, std::vector<float>* down_out, float* stab_out) {
+    (void)sr;
+    try {
+        if (bpm <= 0.0f || bpm > 300.0f) return false;
+        if (onsets_s.empty()) return false;
+        std::vector<float> on(onsets_s);
+        std::stable_sort(on.begin(), on.end(), [](float a, float b) { return a < b; });
+        std::vector<BeatPos> pos;
+        if (!hmm_track(bpm, on, &pos)) return false;
+        if (pos.empty()) return false;  // ProcessingError
+        std::vector<float> bt;
+        for (auto& p : pos) bt.push_back(p.t);
+        auto segs = tempo_variations(bt, bpm);
+        bool var = false;
+        for (auto& s : segs) var |= s.variable;
+        if (var) {
+            std::vector<BeatPos> refined;
+            Bayes st{bpm, sd_clampf(conf, 0.0f, 1.0f)};
+            for (auto& s : segs) {
+                if (s.variable) {
+                    std::vector<float> so;
+                    for (float o : on)
+                        if (o >= s.start && o <= s.end) so.push_back(o);
+                    if (!so.empty()) {
+                        float ub;
+                        bayes_update(st, so, &ub);
+                        std::vector<BeatPos> sb;
+                        if (hmm_track(ub, so, &sb)) refined.insert(refined.end(), sb.begin(), sb.end());
+                    }
+                } else {
+                    for (auto& p : pos)
+                        if (p.t >= s.start && p.t <= s.end) refined.push_back(p);
+                }
+            }
+            if (!refined.empty()) {
+                std::stable_sort(refined.begin(), refined.end(), [](auto& a, auto& b) { return a.t < b.t; });
+                pos.swap(refined);
+            }
+        }
+        bt.clear();
+        for (auto& p : pos) bt.push_back(p.t);
+        const uint32_t bpb = time_signature(bt, bpm);
+        // generate_beat_grid_from_positions_with_time_sig (:290-320)
+        std::vector<float> beats(bt);
+        std::stable_sort(beats.begin(), beats.end(), [](float a, float b) { return a < b; });
+        std::vector<float> down;
+        if (!beats.empty()) {
+            const float bi = 60.0f / bpm;
+            const float bar = bi * (float)bpb;
+            const float tol = bar * 0.1f;
+            down.push_back(beats[0]);
+            for (size_t i = 1; i < beats.size(); i++) {
+                const float exp_t = down.back() + bar;
+                if (sd_absf(beats[i] - exp_t) <= tol) down.push_back(beats[i]);
+            }
+        }
+        // calculate_grid_stability
+        float stab = 0.0f;
+        if (pos.size() >= 2) {
+            std::vector<float> iv;
+            for (size_t i = 1; i < pos.size(); i++) {
+                const float d = pos[i].t - pos[i - 1].t;
+                if (d > 0.0f) iv.push_back(d);
+            }
+            if (!iv.empty()) {
+                float sum = 0.0f;
+                for (float x : iv) sum += x;
+                const float mean = sum / (float)iv.size();
+                if (mean > 1e-10f) {
+                    float vs = 0.0f;
+                    for (float x : iv) {
+                        const float d = x - mean;
+                        vs += d * d;
+                    }
+                    const float var = vs / (float)iv.size();
+                    const float cv = __builtin_sqrtf(var) / mean;
+                    stab = 1.0f / (1.0f + cv);
+                }
+            }
+        }
+        *beats_out = beats;
+        *down_out = down;
+        *stab_out = stab;
+        return true;
+    } catch (const AErr&) {
+        return false;  // src/lib.rs:932-943: any error -> empty grid, stability 0
+    }
+}
+
+}  // namespace orc

@@ -1,0 +1,257 @@
+// o_onset.cpp — preprocessing and onset detectors (TEST INFRASTRUCTURE, see oracle_internal.hpp).
+#include <algorithm>
+
+#include "oracle_internal.hpp"
+
+namespace orc {
+
+// src/preprocessing/normalization.rs:262-322 (normalize_peak; the RMS it computes is metadata only)
+void normalize_peak(std::vector<float>& x, float headroom_db) {
+    if (x.empty()) fail(SDSP_ERR_INVALID_INPUT, "Empty audio samples");
+    float peak = 0.0f;
+    for (float v : x) peak = sd_maxf(peak, sd_absf(v));  // fold(0.0, f32::max)
+    if (peak <= EPS) return;                               // :276-284
+    const float target = sd_powf(10.0f, (0.0f - headroom_db) / 20.0f);
+    float gain = target / peak;
+    gain = sd_minf(gain, 1.0f / peak);  // :296
+    for (float& v : x) v *= gain;
+}
+
+// src/preprocessing/silence.rs:102-279
+void detect_and_trim(const std::vector<float>& x, uint32_t sr, float threshold_db, uint32_t min_ms,
+                     size_t frame_size, size_t* trim_start, size_t* trim_end) {
+    const size_t n = x.size();
+    if (n == 0) {
+        *trim_start = *trim_end = 0;
+        return;
+    }
+    if (sr == 0) fail(SDSP_ERR_INVALID_INPUT, "Sample rate must be > 0");
+    if (frame_size == 0) fail(SDSP_ERR_INVALID_INPUT, "Frame size must be > 0");
+    const float thr = sd_powf(10.0f, threshold_db / 20.0f);
+    const size_t hop = frame_size / 2;
+    const size_t num_frames = n >= frame_size ? (n - frame_size) / hop + 1 : 1;
+    std::vector<char> silent(num_frames);
+    std::vector<size_t> starts(num_frames);
+    for (size_t i = 0; i < num_frames; i++) {
+        const size_t s = i * hop, e = std::min(s + frame_size, n);
+        float sum = 0.0f;
+        for (size_t k = s; k < e; k++) sum += x[k] * x[k];
+        const float rms = e > s ? __builtin_sqrtf(sum / (float)(e - s)) : 0.0f;
+        silent[i] = rms <= thr;
+        starts[i] = s;
+    }
+    const size_t min_samples = (size_t)sd_f2u64((float)min_ms / 1000.0f * (float)sr);
+    const size_t min_frames = (min_samples + hop - 1) / hop;  // div_ceil
+    struct R {
+        size_t s, e;
+    };
+    std::vector<R> regions;
+    bool in_sil = false;
+    size_t sil_start = 0;
+    for (size_t f = 0; f < num_frames; f++) {
+        if (silent[f] && !in_sil) {
+            in_sil = true;
+            sil_start = f;
+        } else if (!silent[f] && in_sil) {
+            in_sil = false;
+            const size_t end_f = f;
+            if (end_f - sil_start >= min_frames || sil_start == 0 || end_f == num_frames) {
+                const size_t ss = starts[sil_start];
+                const size_t es = end_f < starts.size() ? starts[end_f] : n;
+                regions.push_back({ss, es});
+            }
+        }
+    }
+    if (in_sil) {
+        if (num_frames - sil_start >= min_frames || sil_start == 0) regions.push_back({starts[sil_start], n});
+    }
+    size_t ts = 0, te = n;
+    if (!regions.empty() && regions.front().s == 0) ts = regions.front().e;
+    if (!regions.empty() && regions.back().e == n) te = regions.back().s;
+    ts = std::min(ts, te);
+    te = std::max(te, ts);
+    if (!(ts < te && te <= n)) ts = te = 0;
+    *trim_start = ts;
+    *trim_end = te;
+}
+
+// src/features/onset/energy_flux.rs:60-243
+std::vector<size_t> energy_flux_onsets(const float* s, size_t n, size_t frame, size_t hop, float thr_db) {
+    std::vector<size_t> on;
+    if (n == 0) return on;
+    if (frame == 0) fail(SDSP_ERR_INVALID_INPUT, "Frame size must be > 0");
+    if (hop == 0) fail(SDSP_ERR_INVALID_INPUT, "Hop size must be > 0");
+    if (frame > n) return on;
+    const size_t nf = (n - frame) / hop + 1;
+    if (nf < 2) return on;
+    std::vector<float> e(nf);
+    for (size_t i = 0; i < nf; i++) {
+        const size_t st = i * hop, en = std::min(st + frame, n);
+        float sum = 0.0f;
+        for (size_t k = st; k < en; k++) sum += s[k] * s[k];
+        e[i] = __builtin_sqrtf(sum / (float)(en - st));
+    }
+    std::vector<float> flux(nf - 1);
+    for (size_t i = 1; i < nf; i++) flux[i - 1] = sd_maxf(e[i] - e[i - 1], 0.0f);
+    float mx = 0.0f;
+    for (float v : flux) mx = sd_maxf(mx, v);
+    if (mx <= EPS) return on;
+    const float thr = mx * sd_powf(10.0f, thr_db / 20.0f);
+    const size_t L = flux.size();
+    for (size_t i = 1; i + 1 < L; i++) {
+        const float f = flux[i];
+        if (f > thr && f > flux[i - 1] && f >= flux[i + 1]) {
+            const size_t o = (i + 1) * hop;
+            if (o < n) on.push_back(o);
+        }
+    }
+    if (L > 1 && flux[0] > thr && flux[0] >= flux[1]) {
+        if (hop < n) on.push_back(hop);
+    }
+    const size_t li = L - 1;
+    if (L > 1 && flux[li] > thr && flux[li] > flux[li - 1]) {
+        const size_t o = (li + 1) * hop;
+        if (o < n) on.push_back(o);
+    }
+    std::sort(on.begin(), on.end());
+    if (!on.empty()) {
+        std::vector<size_t> d{on[0]};
+        for (size_t k = 1; k < on.size(); k++)
+            if (on[k] >= d.back() + hop / 2) d.push_back(on[k]);
+        on.swap(d);
+    }
+    return on;
+}
+
+// Shared tail of spectral_flux.rs:165-215 and hfc.rs:162-208: percentile threshold + peaks.
+static std::vector<size_t> peaks_over_percentile(const std::vector<float>& flux, float pct) {
+    std::vector<size_t> on;
+    if (flux.empty()) return on;
+    std::vector<float> sorted(flux);
+    std::stable_sort(sorted.begin(), sorted.end(), [](float a, float b) { return a < b; });
+    size_t ti = (size_t)sd_f2u64((float)sorted.size() * pct);
+    ti = std::min(ti, sorted.size() - 1);
+    const float thr = sorted[ti];
+    const size_t L = flux.size();
+    for (size_t i = 1; i + 1 < L; i++) {
+        const float f = flux[i];
+        if (f > thr && f > flux[i - 1] && f >= flux[i + 1]) on.push_back(i + 1);
+    }
+    if (L > 1 && flux[0] > thr && flux[0] >= flux[1]) on.push_back(1);
+    const size_t li = L - 1;
+    if (L > 1 && flux[li] > thr && flux[li] > flux[li - 1]) on.push_back(L);
+    std::sort(on.begin(), on.end());
+    on.erase(std::unique(on.begin(), on.end()), on.end());
+    return on;
+}
+
+// src/features/onset/spectral_flux.rs:60-221
+std::vector<size_t> spectral_flux_onsets(const Spec& m, float pct) {
+    if (m.empty()) return {};
+    if (!(pct >= 0.0f && pct <= 1.0f)) fail(SDSP_ERR_INVALID_INPUT, "Threshold percentile must be in [0, 1]");
+    if (m.bins == 0) fail(SDSP_ERR_INVALID_INPUT, "Empty magnitude frames");
+    if (m.frames < 2) return {};
+    const size_t B = m.bins;
+    std::vector<float> mx(m.frames);
+    for (size_t t = 0; t < m.frames; t++) {
+        float v = 0.0f;
+        const float* r = m.row(t);
+        for (size_t b = 0; b < B; b++) v = sd_maxf(v, r[b]);
+        mx[t] = v;
+    }
+    std::vector<float> flux(m.frames - 1);
+    for (size_t t = 1; t < m.frames; t++) {
+        const float* p = m.row(t - 1);
+        const float* c = m.row(t);
+        const bool pn = mx[t - 1] > EPS, cn = mx[t] > EPS;
+        float sum = 0.0f;
+        for (size_t b = 0; b < B; b++) {
+            const float pv = pn ? p[b] / mx[t - 1] : 0.0f;
+            const float cv = cn ? c[b] / mx[t] : 0.0f;
+            const float d = sd_maxf(cv - pv, 0.0f);
+            sum += d * d;
+        }
+        flux[t - 1] = __builtin_sqrtf(sum);
+    }
+    return peaks_over_percentile(flux, pct);
+}
+
+// src/features/onset/hfc.rs:70-214
+std::vector<size_t> hfc_onsets(const Spec& m, uint32_t sr, float pct) {
+    if (m.empty()) return {};
+    if (sr == 0) fail(SDSP_ERR_INVALID_INPUT, "Sample rate must be > 0");
+    if (!(pct >= 0.0f && pct <= 1.0f)) fail(SDSP_ERR_INVALID_INPUT, "Threshold percentile must be in [0, 1]");
+    if (m.bins == 0) fail(SDSP_ERR_INVALID_INPUT, "Empty magnitude frames");
+    if (m.frames < 2) return {};
+    std::vector<float> h(m.frames);
+    for (size_t t = 0; t < m.frames; t++) {
+        const float* r = m.row(t);
+        float acc = 0.0f;
+        for (size_t b = 0; b < m.bins; b++) acc += (float)b * r[b] * r[b];
+        h[t] = acc;
+    }
+    std::vector<float> flux(m.frames - 1);
+    for (size_t t = 1; t < m.frames; t++) flux[t - 1] = sd_maxf(h[t] - h[t - 1], 0.0f);
+    return peaks_over_percentile(flux, pct);
+}
+
+// src/features/onset/consensus.rs:111-287
+std::vector<OnsetCand> vote_onsets(const std::vector<size_t> lists[4], const float w[4], uint32_t tol_ms,
+                                   uint32_t sr) {
+    if (sr == 0) fail(SDSP_ERR_INVALID_INPUT, "Sample rate must be > 0");
+    if (tol_ms == 0) fail(SDSP_ERR_INVALID_INPUT, "Tolerance must be > 0");
+    for (int i = 0; i < 4; i++)
+        if (w[i] < 0.0f) fail(SDSP_ERR_INVALID_INPUT, "Weights must be non-negative");
+    const size_t tol = (size_t)sd_f2u64((float)tol_ms / 1000.0f * (float)sr);
+    struct O {
+        size_t sample;
+        int method;
+        float weight;
+    };
+    std::vector<O> all;
+    for (int mth = 0; mth < 4; mth++)
+        for (size_t s : lists[mth]) all.push_back({s, mth, w[mth]});
+    if (all.empty()) return {};
+    std::stable_sort(all.begin(), all.end(), [](const O& a, const O& b) { return a.sample < b.sample; });
+    // Greedy clustering: join the FIRST cluster (creation order) holding ANY member within tol.
+    std::vector<std::vector<const O*>> clusters;
+    for (const O& o : all) {
+        bool added = false;
+        for (auto& cl : clusters) {
+            for (const O* ex : cl) {
+                const int64_t dd = (int64_t)(int32_t)o.sample - (int64_t)(int32_t)ex->sample;
+                const uint64_t ad = (uint64_t)(dd < 0 ? -dd : dd);
+                if ((size_t)ad <= tol) {
+                    cl.push_back(&o);
+                    added = true;
+                    break;
+                }
+            }
+            if (added) break;
+        }
+        if (!added) clusters.push_back({&o});
+    }
+    std::vector<OnsetCand> cands;
+    float max_w = 0.0f;
+    for (int i = 0; i < 4; i++) max_w += w[i];
+    for (auto& cl : clusters) {
+        size_t sum = 0;
+        for (const O* o : cl) sum += o->sample;
+        const size_t center = sum / cl.size();
+        float tw = 0.0f;
+        bool voted[4] = {false, false, false, false};
+        for (const O* o : cl) {
+            tw += o->weight;
+            voted[o->method] = true;
+        }
+        uint32_t vb = 0;
+        for (int i = 0; i < 4; i++) vb += voted[i];
+        const float conf = max_w > 0.0f ? sd_clampf(tw / max_w, 0.0f, 1.0f) : 0.0f;
+        cands.push_back({center, (float)center / (float)sr, conf, vb});
+    }
+    std::stable_sort(cands.begin(), cands.end(),
+                     [](const OnsetCand& a, const OnsetCand& b) { return b.confidence < a.confidence; });
+    return cands;
+}
+
+}  // namespace orc

@@ -1,0 +1,149 @@
+"""ctypes wrapper of the CPU restatement (oracle/build/libsdsp_oracle.so).
+
+TEST INFRASTRUCTURE: imported only by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, as the checker — never by the product path (stratum-dsp_amd/).
+"""
+import ctypes as C
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(ROOT, "stratum-dsp_amd", "python"))
+from sdsp_abi import SdspConfig, SdspResult, result_to_dict  # noqa: E402
+
+LIB_PATH = os.path.join(HERE, "build", "libsdsp_oracle.so")
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-j8", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        fp = C.POINTER(C.c_float)
+        L.sdsp_oracle_config_default.argtypes = [C.POINTER(SdspConfig)]
+        L.sdsp_oracle_analyze.argtypes = [fp, C.c_uint64, C.c_uint32, C.POINTER(SdspConfig), C.POINTER(SdspResult),
+                                          C.c_char_p, C.c_uint64]
+        L.sdsp_oracle_analyze.restype = C.c_int32
+        L.sdsp_oracle_result_free.argtypes = [C.POINTER(SdspResult)]
+        L.sdsp_oracle_last_trace_json.restype = C.c_char_p
+        L.sdsp_oracle_stft.argtypes = [fp, C.c_uint64, C.c_uint64, C.c_uint64, fp]
+        L.sdsp_oracle_stft.restype = C.c_int64
+        L.sdsp_oracle_rfft.argtypes = [fp, C.c_uint64, fp]
+        L.sdsp_oracle_fft.argtypes = [fp, C.c_uint64]
+        L.sdsp_oracle_novelty_full.argtypes = [fp, C.c_uint64, C.c_uint64, C.c_uint32, fp]
+        L.sdsp_oracle_novelty_full.restype = C.c_int64
+        u64p = C.POINTER(C.c_uint64)
+        L.sdsp_oracle_vote_onsets.argtypes = [u64p, C.c_uint64] * 4 + [fp, C.c_uint32, C.c_uint32, u64p,
+                                                                        C.POINTER(C.c_uint32), fp]
+        L.sdsp_oracle_vote_onsets.restype = C.c_int64
+        L.sdsp_oracle_key_clarity.argtypes = [fp, C.c_int32]
+        L.sdsp_oracle_key_clarity.restype = C.c_float
+        L.sdsp_oracle_key_templates.argtypes = [fp]
+        L.sdsp_oracle_libm.argtypes = [C.c_int32, fp, fp, fp, C.c_uint64]
+        _lib = L
+    return _lib
+
+
+def _fp(a):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def default_config():
+    c = SdspConfig()
+    lib().sdsp_oracle_config_default(C.byref(c))
+    return c
+
+
+def analyze(samples, sample_rate=44100, config=None, trace=False):
+    """Returns (status, result_dict_or_error_message[, trace_dict])."""
+    x = np.ascontiguousarray(samples, dtype=np.float32)
+    cfg = config if config is not None else default_config()
+    r = SdspResult()
+    err = C.create_string_buffer(512)
+    st = lib().sdsp_oracle_analyze(_fp(x), x.size, sample_rate, C.byref(cfg), C.byref(r), err, 512)
+    tr = json.loads(lib().sdsp_oracle_last_trace_json().decode()) if trace else None
+    if st != 0:
+        out = (st, err.value.decode())
+    else:
+        out = (0, result_to_dict(r))
+        lib().sdsp_oracle_result_free(C.byref(r))
+    return out + ((tr,) if trace else ())
+
+
+def stft(x, nfft, hop):
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    if x.size < nfft:
+        return np.zeros((0, nfft // 2 + 1), np.float32)
+    frames = (x.size - nfft) // hop + 1
+    out = np.empty((frames, nfft // 2 + 1), np.float32)
+    n = lib().sdsp_oracle_stft(_fp(x), x.size, nfft, hop, _fp(out))
+    assert n == frames
+    return out
+
+
+def rfft(x):
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    out = np.empty(x.size // 2 + 1, np.complex64)
+    lib().sdsp_oracle_rfft(_fp(x), x.size, out.ctypes.data_as(C.POINTER(C.c_float)))
+    return out
+
+
+def fft(z):
+    z = np.array(z, dtype=np.complex64)
+    lib().sdsp_oracle_fft(z.ctypes.data_as(C.POINTER(C.c_float)), z.size)
+    return z
+
+
+def novelty_full(mags, sample_rate=44100):
+    m = np.ascontiguousarray(mags, dtype=np.float32)
+    out = np.empty(max(m.shape[0], 1), np.float32)
+    n = lib().sdsp_oracle_novelty_full(_fp(m), m.shape[0], m.shape[1], sample_rate, _fp(out))
+    return out[:n]
+
+
+def vote_onsets(lists, weights, tol_ms, sample_rate):
+    arrs = [np.ascontiguousarray(l, dtype=np.uint64) for l in lists]
+    total = sum(a.size for a in arrs) + 1
+    t = np.zeros(total, np.uint64)
+    v = np.zeros(total, np.uint32)
+    cf = np.zeros(total, np.float32)
+    w = np.ascontiguousarray(weights, dtype=np.float32)
+    args = []
+    for a in arrs:
+        args += [a.ctypes.data_as(C.POINTER(C.c_uint64)), a.size]
+    n = lib().sdsp_oracle_vote_onsets(*args, _fp(w), tol_ms, sample_rate, t.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                      v.ctypes.data_as(C.POINTER(C.c_uint32)), _fp(cf))
+    if n < 0:
+        return int(n)
+    return [(int(t[i]), int(v[i]), float(cf[i])) for i in range(n)]
+
+
+def key_clarity(scores):
+    s = np.ascontiguousarray(scores, dtype=np.float32)
+    return float(lib().sdsp_oracle_key_clarity(_fp(s), s.size))
+
+
+def key_templates():
+    out = np.empty((24, 12), np.float32)
+    lib().sdsp_oracle_key_templates(_fp(out))
+    return out
+
+
+def libm(op, x, y=None):
+    ops = {"ln": 0, "exp": 1, "cos": 2, "log10": 3, "log2": 4, "pow": 5}
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    y = np.ascontiguousarray(y if y is not None else np.zeros_like(x), dtype=np.float32)
+    out = np.empty_like(x)
+    lib().sdsp_oracle_libm(ops[op], _fp(x), _fp(y), _fp(out), x.size)
+    return out
