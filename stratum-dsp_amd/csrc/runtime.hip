@@ -1,0 +1,234 @@
+// runtime.hip — device contexts, FFT tables, C ABI housekeeping (config defaults, result
+// ownership, version) and stage probes.  The analyze pipeline itself is in pipeline.hip.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+#include "../../include/sdsp_fft_spec.h"
+#include "sdsp_runtime.hpp"
+
+namespace sdsp {
+
+static std::mutex g_ctx_mu;
+static std::map<int, std::unique_ptr<DeviceCtx>> g_ctx;
+
+DeviceCtx& device_ctx(int device) {
+    std::lock_guard<std::mutex> lk(g_ctx_mu);
+    auto& c = g_ctx[device];
+    if (!c) {
+        c.reset(new DeviceCtx());
+        c->device = device;
+        SDSP_HIP_CHECK(hipSetDevice(device));
+        SDSP_HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    }
+    return *c;
+}
+
+FftTables& DeviceCtx::tables(int N, bool with_window) {
+    auto& t = fft[N];
+    if (!t) {
+        t.reset(new FftTables());
+        const int M = N / 2;
+        std::vector<float> tw(2 * (size_t)std::max(M, 1)), rt((size_t)N + 2);
+        sdsp_fft_twiddles(std::max(M, 1), tw.data());
+        sdsp_rfft_twiddles(N, rt.data());
+        t->tw.ensure(tw.size() * 4);
+        t->rt.ensure(rt.size() * 4);
+        SDSP_HIP_CHECK(hipMemcpy(t->tw.p, tw.data(), tw.size() * 4, hipMemcpyHostToDevice));
+        SDSP_HIP_CHECK(hipMemcpy(t->rt.p, rt.data(), rt.size() * 4, hipMemcpyHostToDevice));
+    }
+    if (with_window && !t->window.p) {
+        std::vector<float> w((size_t)N);
+        for (int i = 0; i < N; i++) w[(size_t)i] = sdsp_hann_f32(i, N);  // extractor.rs:318-323
+        t->window.ensure(w.size() * 4);
+        SDSP_HIP_CHECK(hipMemcpy(t->window.p, w.data(), w.size() * 4, hipMemcpyHostToDevice));
+    }
+    return *t;
+}
+
+}  // namespace sdsp
+
+using namespace sdsp;
+
+extern "C" {
+
+// AnalysisConfig::default(), reference src/config.rs:594-744
+void sdsp_config_default(sdsp_config* c) {
+    std::memset(c, 0, sizeof(*c));
+    c->min_amplitude_db = -40.0f;
+    c->normalization = SDSP_NORM_PEAK;
+    c->enable_normalization = 1;
+    c->enable_silence_trimming = 1;
+    c->enable_onset_consensus = 1;
+    c->onset_threshold_percentile = 0.80f;
+    c->onset_consensus_tolerance_ms = 50;
+    for (int i = 0; i < 4; i++) c->onset_consensus_weights[i] = 0.25f;
+    c->hpss_margin = 10;
+    c->enable_legacy_bpm_guardrails = 1;
+    c->enable_tempogram_multi_resolution = 1;
+    c->tempogram_multi_res_top_k = 25;
+    c->tempogram_multi_res_w512 = 0.45f;
+    c->tempogram_multi_res_w256 = 0.35f;
+    c->tempogram_multi_res_w1024 = 0.20f;
+    c->tempogram_multi_res_structural_discount = 0.85f;
+    c->tempogram_multi_res_double_time_512_factor = 0.92f;
+    c->tempogram_multi_res_margin_threshold = 0.08f;
+    c->enable_tempogram_band_fusion = 1;
+    c->tempogram_band_low_max_hz = 200.0f;
+    c->tempogram_band_mid_max_hz = 2000.0f;
+    c->tempogram_band_high_max_hz = 8000.0f;
+    c->tempogram_band_w_full = 0.40f;
+    c->tempogram_band_w_low = 0.25f;
+    c->tempogram_band_w_mid = 0.20f;
+    c->tempogram_band_w_high = 0.15f;
+    c->tempogram_band_seed_only = 1;
+    c->tempogram_band_support_threshold = 0.25f;
+    c->tempogram_band_consensus_bonus = 0.08f;
+    c->tempogram_novelty_w_spectral = 0.30f;
+    c->tempogram_novelty_w_energy = 0.35f;
+    c->tempogram_novelty_w_hfc = 0.35f;
+    c->tempogram_novelty_local_mean_window = 16;
+    c->tempogram_novelty_smooth_window = 5;
+    c->debug_top_n = 5;
+    c->enable_tempogram_mel_novelty = 1;
+    c->tempogram_mel_n_mels = 40;
+    c->tempogram_mel_fmin_hz = 30.0f;
+    c->tempogram_mel_fmax_hz = 8000.0f;
+    c->tempogram_mel_max_filter_bins = 2;
+    c->tempogram_mel_weight = 0.15f;
+    c->tempogram_superflux_max_filter_bins = 4;
+    c->tempogram_candidates_top_n = 10;
+    c->legacy_bpm_preferred_min = 72.0f;
+    c->legacy_bpm_preferred_max = 168.0f;
+    c->legacy_bpm_soft_min = 60.0f;
+    c->legacy_bpm_soft_max = 210.0f;
+    c->legacy_bpm_conf_mul_preferred = 1.30f;
+    c->legacy_bpm_conf_mul_soft = 0.70f;
+    c->legacy_bpm_conf_mul_extreme = 0.01f;
+    c->min_bpm = 40.0f;
+    c->max_bpm = 240.0f;
+    c->bpm_resolution = 1.0f;
+    c->frame_size = 2048;
+    c->hop_size = 512;
+    c->center_frequency = 440.0f;
+    c->soft_chroma_mapping = 1;
+    c->soft_mapping_sigma = 0.5f;
+    c->chroma_sharpening_power = 1.0f;
+    c->enable_key_spectrogram_time_smoothing = 1;
+    c->key_spectrogram_smooth_margin = 12;
+    c->enable_key_frame_weighting = 1;
+    c->key_min_tonalness = 0.0f;
+    c->key_tonalness_power = 2.0f;
+    c->key_energy_power = 0.50f;
+    c->enable_key_harmonic_mask = 1;
+    c->key_harmonic_mask_power = 2.0f;
+    c->key_hpss_frame_step = 4;
+    c->key_hpss_time_margin = 8;
+    c->key_hpss_freq_margin = 8;
+    c->key_hpss_mask_power = 2.0f;
+    c->enable_key_stft_override = 1;
+    c->key_stft_frame_size = 8192;
+    c->key_stft_hop_size = 512;
+    c->key_template_set = SDSP_TEMPLATES_KRUMHANSL_KESSLER;
+    c->key_ensemble_kk_weight = 0.5f;
+    c->key_ensemble_temperley_weight = 0.5f;
+    c->key_median_segment_length_frames = 480;
+    c->key_median_segment_hop_frames = 120;
+    c->key_median_min_segments = 3;
+    static const uint64_t kMultiScale[3] = {120, 360, 720};
+    c->key_multi_scale_lengths = kMultiScale;
+    c->key_multi_scale_lengths_len = 3;
+    c->key_multi_scale_hop = 60;
+    c->key_multi_scale_min_clarity = 0.20f;
+    c->key_tuning_max_abs_semitones = 0.08f;
+    c->key_tuning_frame_step = 20;
+    c->key_tuning_peak_rel_threshold = 0.35f;
+    c->key_edge_trim_fraction = 0.15f;
+    c->enable_key_segment_voting = 1;
+    c->key_segment_len_frames = 1024;
+    c->key_segment_hop_frames = 512;
+    c->key_segment_min_clarity = 0.20f;
+    c->key_mode_third_ratio_margin = 0.00f;
+    c->key_mode_flip_min_score_ratio = 0.60f;
+    c->enable_key_hpcp = 1;
+    c->key_hpcp_peaks_per_frame = 24;
+    c->key_hpcp_num_harmonics = 4;
+    c->key_hpcp_harmonic_decay = 0.60f;
+    c->key_hpcp_mag_power = 0.50f;
+    c->key_hpcp_whitening_smooth_bins = 31;
+    c->key_hpcp_bass_fmin_hz = 55.0f;
+    c->key_hpcp_bass_fmax_hz = 300.0f;
+    c->key_hpcp_bass_weight = 0.35f;
+    c->key_minor_leading_tone_bonus_weight = 0.2f;
+}
+
+const char* sdsp_version(void) { return "stratum-hip 1 gfx950"; }
+
+void sdsp_result_free(sdsp_result* r) {
+    if (!r) return;
+    std::free(r->beats);
+    std::free(r->downbeats);
+    std::free(r->bars);
+    for (uint64_t i = 0; i < r->n_warnings; i++) std::free(r->warnings[i]);
+    std::free(r->warnings);
+    std::free(r->tempogram_candidates);
+    r->beats = r->downbeats = r->bars = nullptr;
+    r->warnings = nullptr;
+    r->tempogram_candidates = nullptr;
+    r->n_beats = r->n_downbeats = r->n_bars = r->n_warnings = r->n_tempogram_candidates = 0;
+}
+
+int32_t sdsp_last_stage_times(int32_t device, sdsp_stage_times* out) {
+    try {
+        DeviceCtx& c = device_ctx(device);
+        std::lock_guard<std::mutex> lk(c.mu);
+        *out = c.last;
+        return SDSP_OK;
+    } catch (const std::exception&) {
+        return SDSP_ERR_PROCESSING;
+    }
+}
+
+// Stage probe: STFT magnitudes of one host buffer (x*gain framed at hop), frames x (nfft/2+1).
+int32_t sdsp_debug_stft(const float* host_x, uint64_t n, uint64_t nfft, uint64_t hop, float gain, float* host_out,
+                        float* host_frame_max, int32_t device) {
+    try {
+        if (!(nfft == 2048 || nfft == 8192) || n < nfft || hop == 0) return SDSP_ERR_INVALID_INPUT;
+        DeviceCtx& c = device_ctx(device);
+        std::lock_guard<std::mutex> lk(c.mu);
+        SDSP_HIP_CHECK(hipSetDevice(device));
+        const uint64_t frames = (n - nfft) / hop + 1;
+        const int bins = (int)nfft / 2 + 1;
+        const int stride = (bins + 3) & ~3;
+        FftTables& tb = c.tables((int)nfft, true);
+        DevBuf x, pfx, off, g, row0, mags, fmax;
+        x.ensure(n * 4);
+        mags.ensure(frames * stride * 4);
+        fmax.ensure(frames * 4);
+        pfx.ensure(16);
+        off.ensure(8);
+        g.ensure(4);
+        row0.ensure(8);
+        const uint64_t pf[2] = {0, frames}, o0 = 0, r0 = 0;
+        SDSP_HIP_CHECK(hipMemcpy(x.p, host_x, n * 4, hipMemcpyHostToDevice));
+        SDSP_HIP_CHECK(hipMemcpy(pfx.p, pf, 16, hipMemcpyHostToDevice));
+        SDSP_HIP_CHECK(hipMemcpy(off.p, &o0, 8, hipMemcpyHostToDevice));
+        SDSP_HIP_CHECK(hipMemcpy(g.p, &gain, 4, hipMemcpyHostToDevice));
+        SDSP_HIP_CHECK(hipMemcpy(row0.p, &r0, 8, hipMemcpyHostToDevice));
+        launch_stft((int)nfft, nfft == 2048, x.as<float>(), pfx.as<uint64_t>(), 1, frames, off.as<uint64_t>(),
+                    g.as<float>(), (int)hop, tb.window.as<float>(), tb.tw.as<cx>(), tb.rt.as<cx>(), mags.as<float>(),
+                    row0.as<uint64_t>(), stride, fmax.as<float>(), c.stream);
+        SDSP_HIP_CHECK(hipGetLastError());
+        SDSP_HIP_CHECK(hipStreamSynchronize(c.stream));
+        SDSP_HIP_CHECK(hipMemcpy2D(host_out, (size_t)bins * 4, mags.p, (size_t)stride * 4, (size_t)bins * 4,
+                                   frames, hipMemcpyDeviceToHost));
+        if (host_frame_max && nfft == 2048)
+            SDSP_HIP_CHECK(hipMemcpy(host_frame_max, fmax.p, frames * 4, hipMemcpyDeviceToHost));
+        return SDSP_OK;
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "sdsp_debug_stft: %s\n", e.what());
+        return SDSP_ERR_PROCESSING;
+    }
+}
+
+}  // extern "C"

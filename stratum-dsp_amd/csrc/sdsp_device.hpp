@@ -1,0 +1,49 @@
+// sdsp_device.hpp — shared device-side definitions for the gfx950 analyze_audio kernels.
+//
+// Numerics contract: every kernel performs the reference's f32 operations in the reference's
+// order (sequential folds are kept sequential; see DESIGN.md "exactness"), builds with
+// -ffp-contract=off, and evaluates transcendentals through include/sdsp_libm.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/sdsp_libm.h"
+
+namespace sdsp {
+
+constexpr float EPS = 1e-10f;
+constexpr int WAVE = 64;
+
+struct cx {
+    float re, im;
+};
+__device__ __forceinline__ cx cadd(cx a, cx b) { return {a.re + b.re, a.im + b.im}; }
+__device__ __forceinline__ cx csub(cx a, cx b) { return {a.re - b.re, a.im - b.im}; }
+__device__ __forceinline__ cx cmul(cx w, cx z) { return {w.re * z.re - w.im * z.im, w.re * z.im + w.im * z.re}; }
+
+// ---- wave / block reductions (order-free ops only: max, min, integer sums) ----
+__device__ __forceinline__ float wave_max(float v) {
+    for (int o = 32; o > 0; o >>= 1) v = sd_maxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ int wave_sum_i(int v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Largest index i in [0, n) with pfx[i] <= key (pfx ascending, pfx[0] == 0): maps a flat
+// work index onto its track for ragged batches.
+__device__ __forceinline__ int find_track(const uint64_t* pfx, int n, uint64_t key) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        int mid = (lo + hi + 1) >> 1;
+        if (pfx[mid] <= key)
+            lo = mid;
+        else
+            hi = mid - 1;
+    }
+    return lo;
+}
+
+}  // namespace sdsp

@@ -1,0 +1,83 @@
+// sdsp_runtime.hpp — host-side runtime internals (device contexts, buffers, launchers).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/stratum_hip.h"
+#include "sdsp_device.hpp"
+
+#define SDSP_HIP_CHECK(expr)                                                                              \
+    do {                                                                                                  \
+        hipError_t _e = (expr);                                                                           \
+        if (_e != hipSuccess)                                                                             \
+            throw sdsp::HipError(std::string(#expr) + " failed: " + hipGetErrorString(_e) + " at " __FILE__); \
+    } while (0)
+
+namespace sdsp {
+
+struct HipError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+// Grow-only device allocation.
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    void ensure(size_t n) {
+        if (n <= bytes) return;
+        if (p) SDSP_HIP_CHECK(hipFree(p));
+        p = nullptr;
+        bytes = 0;
+        const size_t want = n + n / 8 + 4096;
+        SDSP_HIP_CHECK(hipMalloc(&p, want));
+        bytes = want;
+    }
+    template <class T>
+    T* as() const {
+        return reinterpret_cast<T*>(p);
+    }
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+};
+
+// Per-size FFT tables (sdsp_fft_spec.h) + STFT windows, uploaded once per device.
+struct FftTables {
+    DevBuf tw;      // M-point complex twiddles (M = N/2)
+    DevBuf rt;      // N/2+1 real-FFT post twiddles
+    DevBuf window;  // N-point symmetric Hann (STFT sizes only)
+};
+
+struct StageTimer;
+
+struct DeviceCtx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    std::map<int, std::unique_ptr<FftTables>> fft;  // keyed by real FFT size N
+    std::map<std::string, std::unique_ptr<DevBuf>> bufs;
+    sdsp_stage_times last{};
+    DevBuf& buf(const std::string& name) {
+        auto& b = bufs[name];
+        if (!b) b.reset(new DevBuf());
+        return *b;
+    }
+    FftTables& tables(int N, bool with_window);
+};
+
+DeviceCtx& device_ctx(int device);
+
+// ---- kernel launchers (defined next to their kernels) ----
+void launch_stft(int nfft, bool frame_max, const float* samples, const uint64_t* frame_pfx, int n_tracks,
+                 uint64_t total_frames, const uint64_t* src_off, const float* gain, int hop, const float* window,
+                 const cx* tw, const cx* rt, float* mags, const uint64_t* mag_row0, int stride, float* fmax,
+                 hipStream_t st);
+
+}  // namespace sdsp

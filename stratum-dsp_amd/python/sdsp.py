@@ -1,0 +1,166 @@
+"""Python binding of libstratum_hip.so (the MI355X analyze_audio engine).
+
+This is the ctypes stub a Python caller of the reference's API would use: `analyze_audio`
+mirrors `stratum_dsp::analyze_audio(samples, sample_rate, AnalysisConfig)` (reference
+src/lib.rs:86) and raises `AnalysisError` with the reference's Display text on failure.
+
+There is no CPU fallback: if the HIP library is missing or no GPU is visible, every compute
+call raises.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from sdsp_abi import ERROR_NAMES, SdspConfig, SdspResult, SdspStageTimes, result_to_dict
+
+PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG, "lib", "libstratum_hip.so")
+_lib = None
+
+
+class AnalysisError(Exception):
+    """AnalysisError (reference src/error.rs:7-34); .kind is the variant name."""
+
+    def __init__(self, code, message):
+        super().__init__(message)
+        self.code = code
+        self.kind = ERROR_NAMES.get(code, "Unknown")
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-j8", "-C", PKG])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"libstratum_hip.so not built ({LIB_PATH}); run __graft_entry__.build()")
+        L = C.CDLL(LIB_PATH)
+        fp = C.POINTER(C.c_float)
+        u64p = C.POINTER(C.c_uint64)
+        L.sdsp_config_default.argtypes = [C.POINTER(SdspConfig)]
+        L.sdsp_version.restype = C.c_char_p
+        L.sdsp_analyze_audio.argtypes = [fp, C.c_uint64, C.c_uint32, C.POINTER(SdspConfig), C.POINTER(SdspResult),
+                                         C.c_char_p, C.c_uint64]
+        L.sdsp_analyze_audio.restype = C.c_int32
+        L.sdsp_analyze_batch.argtypes = [C.POINTER(fp), u64p, C.c_uint64, C.c_uint32, C.POINTER(SdspConfig), C.c_uint32,
+                                         C.POINTER(SdspResult)]
+        L.sdsp_analyze_batch.restype = C.c_int32
+        L.sdsp_analyze_batch_device.argtypes = [C.c_void_p, u64p, u64p, C.c_uint64, C.c_uint32, C.POINTER(SdspConfig),
+                                                C.c_int32, C.c_void_p, C.POINTER(SdspResult)]
+        L.sdsp_analyze_batch_device.restype = C.c_int32
+        L.sdsp_result_free.argtypes = [C.POINTER(SdspResult)]
+        L.sdsp_generate_synthetic.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64, C.c_int32,
+                                              C.c_int32, C.c_void_p, fp, C.POINTER(C.c_int32)]
+        L.sdsp_generate_synthetic.restype = C.c_int32
+        L.sdsp_last_stage_times.argtypes = [C.c_int32, C.POINTER(SdspStageTimes)]
+        L.sdsp_last_stage_times.restype = C.c_int32
+        L.sdsp_debug_stft.argtypes = [fp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_float, fp, fp, C.c_int32]
+        L.sdsp_debug_stft.restype = C.c_int32
+        _lib = L
+    return _lib
+
+
+def _fp(a):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def default_config():
+    """AnalysisConfig::default() (reference src/config.rs:594-744)."""
+    c = SdspConfig()
+    lib().sdsp_config_default(C.byref(c))
+    return c
+
+
+def version():
+    return lib().sdsp_version().decode()
+
+
+def analyze_audio(samples, sample_rate=44100, config=None):
+    """analyze_audio(samples, sample_rate, config) -> AnalysisResult dict; raises AnalysisError."""
+    x = np.ascontiguousarray(samples, dtype=np.float32)
+    cfg = config if config is not None else default_config()
+    r = SdspResult()
+    err = C.create_string_buffer(512)
+    st = lib().sdsp_analyze_audio(_fp(x), x.size, sample_rate, C.byref(cfg), C.byref(r), err, 512)
+    if st != 0:
+        raise AnalysisError(st, err.value.decode())
+    try:
+        return result_to_dict(r)
+    finally:
+        lib().sdsp_result_free(C.byref(r))
+
+
+def analyze_batch(tracks, sample_rate=44100, config=None, device_mask=0):
+    """Batch form: list of per-track results; failed tracks come back as AnalysisError objects."""
+    arrs = [np.ascontiguousarray(t, dtype=np.float32) for t in tracks]
+    n = len(arrs)
+    ptrs = (C.POINTER(C.c_float) * n)(*[_fp(a) for a in arrs])
+    lens = np.array([a.size for a in arrs], dtype=np.uint64)
+    outs = (SdspResult * n)()
+    cfg = config if config is not None else default_config()
+    st = lib().sdsp_analyze_batch(ptrs, lens.ctypes.data_as(C.POINTER(C.c_uint64)), n, sample_rate, C.byref(cfg),
+                                  device_mask, outs)
+    if st != 0:
+        raise AnalysisError(st, "batch failed")
+    res = []
+    for i in range(n):
+        if outs[i].status != 0:
+            res.append(AnalysisError(outs[i].status, outs[i].error_message.decode()))
+        else:
+            res.append(result_to_dict(outs[i]))
+        lib().sdsp_result_free(C.byref(outs[i]))
+    return res
+
+
+def analyze_batch_device(d_ptr, offsets, lens, sample_rate=44100, config=None, device=0, stream=None,
+                         keep_raw=False):
+    """Tracks already resident in HBM (d_ptr: device address).  Returns results (dicts)."""
+    offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+    ln = np.ascontiguousarray(lens, dtype=np.uint64)
+    n = ln.size
+    outs = (SdspResult * n)()
+    cfg = config if config is not None else default_config()
+    st = lib().sdsp_analyze_batch_device(C.c_void_p(d_ptr), offs.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                         ln.ctypes.data_as(C.POINTER(C.c_uint64)), n, sample_rate, C.byref(cfg),
+                                         device, C.c_void_p(stream or 0), outs)
+    if st != 0:
+        raise AnalysisError(st, "device batch failed")
+    res = []
+    for i in range(n):
+        if outs[i].status != 0:
+            res.append(AnalysisError(outs[i].status, outs[i].error_message.decode()))
+        else:
+            res.append(result_to_dict(outs[i]))
+        lib().sdsp_result_free(C.byref(outs[i]))
+    return res
+
+
+def generate_synthetic(d_ptr, n_tracks, length, sample_rate=44100, seed0=0, bpm_mode=0, device=0, stream=None):
+    bpm = np.zeros(n_tracks, np.float32)
+    key = np.zeros(n_tracks, np.int32)
+    st = lib().sdsp_generate_synthetic(C.c_void_p(d_ptr), n_tracks, length, sample_rate, seed0, bpm_mode, device,
+                                       C.c_void_p(stream or 0), _fp(bpm), key.ctypes.data_as(C.POINTER(C.c_int32)))
+    if st != 0:
+        raise AnalysisError(st, "synthetic generation failed")
+    return bpm, key
+
+
+def stage_times(device=0):
+    t = SdspStageTimes()
+    lib().sdsp_last_stage_times(device, C.byref(t))
+    return {k: getattr(t, k) for k, _ in SdspStageTimes._fields_}
+
+
+def debug_stft(x, nfft, hop, gain=1.0, device=0):
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    frames = (x.size - nfft) // hop + 1
+    out = np.empty((frames, nfft // 2 + 1), np.float32)
+    fmax = np.empty(frames, np.float32)
+    st = lib().sdsp_debug_stft(_fp(x), x.size, nfft, hop, gain, _fp(out), _fp(fmax), device)
+    if st != 0:
+        raise AnalysisError(st, "debug_stft failed")
+    return out, fmax

@@ -1,0 +1,22 @@
+"""GPU STFT kernel vs the CPU restatement: bit-exact (same specified FFT arithmetic)."""
+import numpy as np
+import pytest
+
+import oracle
+import sdsp
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("nfft,hop", [(2048, 512), (2048, 256), (2048, 1024), (8192, 512)])
+def test_stft_bit_exact(nfft, hop):
+    rng = np.random.default_rng(nfft + hop)
+    x = (rng.standard_normal(44100 * 3) * 0.3).astype(np.float32)
+    gain = np.float32(0.8912509)
+    got, fmax = sdsp.debug_stft(x, nfft, hop, gain)
+    ref = oracle.stft((x * gain).astype(np.float32), nfft, hop)
+    assert got.shape == ref.shape
+    mism = np.count_nonzero(got.view(np.uint32) != ref.view(np.uint32))
+    assert mism == 0, f"{mism} of {ref.size} magnitudes differ (max abs diff {np.max(np.abs(got - ref))})"
+    if nfft == 2048:
+        assert np.array_equal(fmax, ref.max(axis=1))
