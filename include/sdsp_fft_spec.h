@@ -69,7 +69,7 @@ static inline void sdsp_rfft_twiddles(int N, float* rt_interleaved) {
  *   x = 2.0 * PI * i as f32 / (n - 1) as f32;  w = 0.5 * (1.0 - x.cos())
  * (all f32 operations, left to right).
  */
-static inline float sdsp_hann_f32(int i, int n) {
+SD_HD float sdsp_hann_f32(int i, int n) {
     const float PI_F = 3.14159265358979323846f;
     float x = 2.0f * PI_F * (float)i / (float)(n - 1);
     return 0.5f * (1.0f - sd_cosf(x));

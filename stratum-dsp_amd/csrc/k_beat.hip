@@ -1,0 +1,444 @@
+// k_beat.hip — beat grid, one thread per track (reference src/features/beat_tracking/):
+//
+//   HmmBeatTracker::track_beats   hmm.rs:121-441
+//   detect_tempo_variations       tempo_variation.rs:95-227
+//   BayesianBeatTracker           bayesian.rs:104-272
+//   detect_time_signature         time_signature.rs:90-199
+//   generate_beat_grid, downbeats, stability   beat_tracking/mod.rs:108-485
+//
+// Work per track is a few thousand scalar steps; the reference's O(frames x onsets) nearest-
+// onset scans become binary searches over the sorted onsets.  |o - t| is monotone on each
+// side of t in f32, so the nearest neighbour's distance is exactly the reference's minimum.
+// The Viterbi pass is not run: the emission is identical for all five states (hmm.rs:264-294),
+// so the extracted beats cannot depend on the path and Viterbi cannot fail.
+#include "kernels.hpp"
+
+namespace sdsp {
+
+// first index with a[i] >= x (a ascending)
+__device__ inline int lower_bound_f(const float* a, int n, float x) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (a[mid] < x)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+// first index with a[i] > x
+__device__ inline int upper_bound_f(const float* a, int n, float x) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (!(x < a[mid]))
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+__device__ inline float nearest_dist(const float* on, int n, float t) {
+    const int i = lower_bound_f(on, n, t);
+    float md = SD_INF_F;
+    if (i < n) md = sd_minf(md, sd_absf(on[i] - t));
+    if (i > 0) md = sd_minf(md, sd_absf(on[i - 1] - t));
+    return md;
+}
+
+// hmm.rs:121-441; returns number of beats or -1 (Err)
+__device__ int hmm_track(float bpm, const float* on, int n, float* out, int cap, int* overflow) {
+    if (bpm <= EPS || bpm > 300.0f) return -1;
+    if (n <= 0) return -1;
+    const float start = on[0], end = on[n - 1];
+    const float interval = 60.0f / bpm;
+    const uint64_t nf = sd_f2u64(__builtin_ceilf((end - start) / interval)) + 1;
+    const float sigma = 0.05f / 2.0f;
+    const float sigma_sq = sigma * sigma;
+    int nb = 0;
+    for (uint64_t t = 0; t < nf; t++) {
+        const float ft = start + ((float)t * interval);
+        const float md = nearest_dist(on, n, ft);
+        const float dsq = md * md;
+        const float em = sd_expf(-dsq / (2.0f * sigma_sq));
+        if (em > 0.1f) {
+            if (nb >= cap) {
+                *overflow = 1;
+                return nb;
+            }
+            out[nb++] = ft;
+        }
+    }
+    return nb;
+}
+
+// stable bottom-up merge sort (partial_cmp semantics on NaN-free data)
+__device__ void merge_sort_f(float* a, float* tmp, int n) {
+    for (int w = 1; w < n; w <<= 1) {
+        for (int lo = 0; lo < n; lo += 2 * w) {
+            const int mid = lo + w < n ? lo + w : n;
+            const int hi = lo + 2 * w < n ? lo + 2 * w : n;
+            int i = lo, j = mid, k = lo;
+            while (i < mid && j < hi) tmp[k++] = (a[j] < a[i]) ? a[j++] : a[i++];
+            while (i < mid) tmp[k++] = a[i++];
+            while (j < hi) tmp[k++] = a[j++];
+        }
+        for (int k = 0; k < n; k++) a[k] = tmp[k];
+    }
+}
+
+struct SegGen {
+    const float* b;
+    int n;
+    float seg_dur, step, cur, last;
+    float nominal;
+    bool single;  // the single-segment fallback cases
+    int phase;    // 0 = running, 1 = emitted single, 2 = done
+};
+
+struct Seg {
+    float start, end, bpm;
+    bool variable;
+};
+
+// Replays detect_tempo_variations (tempo_variation.rs:95-227) one segment at a time.
+// Returns false when exhausted.  *err set when the reference returns Err.
+__device__ bool seg_next(SegGen& g, Seg* s, bool* any_emitted) {
+    const float* b = g.b;
+    const int n = g.n;
+    if (g.phase == 2) return false;
+    if (g.single) {
+        if (g.phase == 1) {
+            g.phase = 2;
+            return false;
+        }
+        g.phase = 1;
+        s->start = n == 0 ? 0.0f : b[0];
+        s->end = n == 0 ? 0.0f : b[n - 1];
+        s->bpm = g.nominal;
+        s->variable = false;
+        *any_emitted = true;
+        return true;
+    }
+    while (g.cur < g.last) {
+        const float cur = g.cur;
+        const float se = sd_minf(cur + g.seg_dur, g.last);
+        g.cur += g.step;
+        const int i0 = lower_bound_f(b, n, cur);
+        const int i1 = upper_bound_f(b, n, se);
+        if (i1 - i0 < 3) continue;
+        float sum = 0.0f;
+        int cnt = 0;
+        for (int k = i0 + 1; k < i1; k++) {
+            const float d = b[k] - b[k - 1];
+            if (d > 0.0f) {
+                sum += d;
+                cnt++;
+            }
+        }
+        if (cnt == 0) continue;
+        const float mean = sum / (float)cnt;
+        float vs = 0.0f;
+        for (int k = i0 + 1; k < i1; k++) {
+            const float d = b[k] - b[k - 1];
+            if (d > 0.0f) {
+                const float dd = d - mean;
+                vs += dd * dd;
+            }
+        }
+        const float var = vs / (float)cnt;
+        const float sd = __builtin_sqrtf(var);
+        const float cv = mean > EPS ? sd / mean : 0.0f;
+        s->start = cur;
+        s->end = se;
+        s->bpm = mean > EPS ? 60.0f / mean : g.nominal;
+        s->variable = cv > 0.15f;
+        *any_emitted = true;
+        return true;
+    }
+    // exhausted; if nothing was emitted the reference returns one nominal segment
+    if (!*any_emitted) {
+        g.single = true;
+        g.phase = 1;
+        s->start = b[0];
+        s->end = b[n - 1];
+        s->bpm = g.nominal;
+        s->variable = false;
+        *any_emitted = true;
+        return true;
+    }
+    g.phase = 2;
+    return false;
+}
+
+__device__ bool seg_init(SegGen& g, const float* b, int n, float nominal) {
+    g.b = b;
+    g.n = n;
+    g.nominal = nominal;
+    g.phase = 0;
+    g.single = false;
+    if (n < 4) {
+        g.single = true;
+        return true;
+    }
+    if (nominal <= EPS) return false;  // Err
+    const float total = b[n - 1] - b[0];
+    if (total < 2.0f) {
+        g.single = true;
+        return true;
+    }
+    g.seg_dur = sd_clampf(total / 4.0f, 4.0f, 8.0f);
+    const float overlap = g.seg_dur * 0.5f;
+    g.step = g.seg_dur - overlap;
+    g.cur = b[0];
+    g.last = b[n - 1];
+    return true;
+}
+
+// bayesian.rs:104-178; returns false on Err
+__device__ bool bayes_update(float* cur_bpm, const float* on, int n, float* out_bpm) {
+    if (n <= 0) return false;
+    if (*cur_bpm <= EPS || *cur_bpm > 300.0f) return false;
+    const float lo = sd_maxf(*cur_bpm - 5.0f, 60.0f), hi = sd_minf(*cur_bpm + 5.0f, 180.0f);
+    float best_bpm = *cur_bpm, best_l = 0.0f;
+    const float sig_sq = 0.05f * 0.05f;
+    for (float cb = lo; cb <= hi; cb += 0.5f) {
+        if (cb <= EPS) return false;
+        const float bi = 60.0f / cb;
+        const float st0 = on[0];
+        float ll = 0.0f;
+        int32_t valid = 0;
+        for (int k = 0; k < n; k++) {
+            const float o = on[k];
+            const int32_t idx = sd_f2i32(sd_roundf((o - st0) / bi));
+            const float et = st0 + ((float)idx * bi);
+            const float d = sd_absf(o - et);
+            ll += -(d * d) / (2.0f * sig_sq);
+            valid++;
+        }
+        const float lik = valid == 0 ? 0.0f : sd_expf(ll / (float)valid);
+        if (lik > best_l) {
+            best_l = lik;
+            best_bpm = cb;
+        }
+    }
+    *cur_bpm = best_bpm;
+    *out_bpm = best_bpm;
+    return true;
+}
+
+__device__ float score_ts(const float* b, int nb, int bpb, float mean, int n_iv) {
+    if (n_iv < bpb) return 0.0f;
+    // intervals with d > 0, visited in order; autocorrelation at lag bpb over that list
+    // (materialised implicitly: iv(k) = k-th positive difference)
+    float acc = 0.0f;
+    int32_t cnt = 0;
+    // walk two cursors over positive differences
+    int ka = 1, kb = 1, seen_b = 0;
+    // advance kb to the bpb-th positive interval
+    while (seen_b < bpb && kb < nb) {
+        if (b[kb] - b[kb - 1] > 0.0f) seen_b++;
+        kb++;
+    }
+    // now kb is one past the (bpb)-th positive interval; iv index of kb's next positive = bpb
+    for (int i = 0; i + bpb < n_iv; i++) {
+        while (!(b[ka] - b[ka - 1] > 0.0f)) ka++;
+        while (!(b[kb] - b[kb - 1] > 0.0f)) kb++;
+        const float d = sd_absf((b[ka] - b[ka - 1]) - (b[kb] - b[kb - 1]));
+        acc += 1.0f / (1.0f + d / mean);
+        cnt++;
+        ka++;
+        kb++;
+    }
+    if (cnt == 0) return 0.0f;
+    const float ac = acc / (float)cnt;
+    float vs = 0.0f;
+    for (int k = 1; k < nb; k++) {
+        const float d = b[k] - b[k - 1];
+        if (d > 0.0f) {
+            const float dd = d - mean;
+            vs += dd * dd;
+        }
+    }
+    const float var = vs / (float)n_iv;
+    const float cv = mean > EPS ? __builtin_sqrtf(var) / mean : 1.0f;
+    const float cons = 1.0f / (1.0f + cv);
+    return sd_minf(ac * 0.7f + cons * 0.3f, 1.0f);
+}
+
+__global__ void k_beat(const int* __restrict__ tracks, int n_items, const uint32_t* __restrict__ onsets,
+                       const uint64_t* __restrict__ on_off, const int* __restrict__ on_n, uint32_t sr,
+                       const float* __restrict__ bpm_in, const float* __restrict__ conf_in,
+                       float* __restrict__ scratch, const uint64_t* __restrict__ beat_off,
+                       const int* __restrict__ beat_cap, float* __restrict__ beats, float* __restrict__ downs,
+                       BeatOut* __restrict__ out) {
+    const int it = blockIdx.x * blockDim.x + threadIdx.x;
+    if (it >= n_items) return;
+    const int trk = tracks[it];
+    BeatOut r{0, 0, 0.0f, 0};
+    const float bpm = bpm_in[trk];
+    const int n = on_n[trk];
+    const int cap = beat_cap[trk];
+    // scratch layout per track: [onsets_s | hmm | refined | tmp], each `cap` floats (cap >= n)
+    float* ons = scratch + beat_off[trk] * 4;
+    float* hb = ons + cap;
+    float* rb = hb + cap;
+    float* tmp = rb + cap;
+    float* ob = beats + beat_off[trk];
+    float* od = downs + beat_off[trk];
+    int overflow = 0;
+    if (!(bpm > 0.0f && n >= 2)) {  // src/lib.rs:913, 944-957
+        out[trk] = r;
+        return;
+    }
+    if (bpm > 300.0f) {  // generate_beat_grid InvalidInput
+        out[trk] = r;
+        return;
+    }
+    const uint32_t* os = onsets + on_off[trk];
+    for (int k = 0; k < n; k++) ons[k] = (float)os[k] / (float)sr;
+    // (already ascending; the reference's sort_by(partial_cmp) is a no-op here)
+    int nh = hmm_track(bpm, ons, n, hb, cap, &overflow);
+    if (nh <= 0 || overflow) {
+        if (overflow) r.ok = -1;
+        out[trk] = r;
+        return;
+    }
+    const float* fin = hb;
+    int nfin = nh;
+    // tempo variations + Bayesian refinement (mod.rs:140-219)
+    SegGen g;
+    if (!seg_init(g, hb, nh, bpm)) {
+        out[trk] = r;
+        return;
+    }
+    bool any = false, has_var = false;
+    Seg s;
+    {
+        SegGen g2 = g;
+        bool any2 = false;
+        while (seg_next(g2, &s, &any2)) has_var |= s.variable;
+    }
+    if (has_var) {
+        float cur_bpm = bpm;
+        int nr = 0;
+        while (seg_next(g, &s, &any)) {
+            if (s.variable) {
+                const int i0 = lower_bound_f(ons, n, s.start);
+                const int i1 = upper_bound_f(ons, n, s.end);
+                if (i1 > i0) {
+                    float ub;
+                    if (!bayes_update(&cur_bpm, ons + i0, i1 - i0, &ub)) {
+                        out[trk] = r;  // Err propagates -> empty grid
+                        return;
+                    }
+                    const int got = hmm_track(ub, ons + i0, i1 - i0, rb + nr, cap - nr, &overflow);
+                    if (overflow) {
+                        r.ok = -1;
+                        out[trk] = r;
+                        return;
+                    }
+                    if (got > 0) nr += got;
+                }
+            } else {
+                const int j0 = lower_bound_f(hb, nh, s.start);
+                const int j1 = upper_bound_f(hb, nh, s.end);
+                if (nr + (j1 - j0) > cap) {
+                    r.ok = -1;
+                    out[trk] = r;
+                    return;
+                }
+                for (int k = j0; k < j1; k++) rb[nr++] = hb[k];
+            }
+        }
+        if (nr > 0) {
+            merge_sort_f(rb, tmp, nr);
+            fin = rb;
+            nfin = nr;
+        }
+    }
+    // time signature (time_signature.rs:90-149)
+    int bpb = 4;
+    if (nfin >= 8) {
+        float sum = 0.0f;
+        int niv = 0;
+        for (int k = 1; k < nfin; k++) {
+            const float d = fin[k] - fin[k - 1];
+            if (d > 0.0f) {
+                sum += d;
+                niv++;
+            }
+        }
+        if (niv > 0) {
+            const float mean = sum / (float)niv;
+            const float s44 = score_ts(fin, nfin, 4, mean, niv), s34 = score_ts(fin, nfin, 3, mean, niv),
+                        s68 = score_ts(fin, nfin, 6, mean, niv);
+            float bs = s44;
+            if (!(s34 < bs)) {
+                bpb = 3;
+                bs = s34;
+            }
+            if (!(s68 < bs)) {
+                bpb = 6;
+                bs = s68;
+            }
+        }
+    }
+    // beats + downbeats (mod.rs:290-404)
+    for (int k = 0; k < nfin; k++) ob[k] = fin[k];
+    const float bi = 60.0f / bpm;
+    const float bar = bi * (float)bpb;
+    const float tolb = bar * 0.1f;
+    int nd = 0;
+    od[nd++] = fin[0];
+    for (int k = 1; k < nfin; k++) {
+        const float et = od[nd - 1] + bar;
+        if (sd_absf(fin[k] - et) <= tolb) od[nd++] = fin[k];
+    }
+    // stability (mod.rs:425-485)
+    float stab = 0.0f;
+    if (nfin >= 2) {
+        float sum = 0.0f;
+        int niv = 0;
+        for (int k = 1; k < nfin; k++) {
+            const float d = fin[k] - fin[k - 1];
+            if (d > 0.0f) {
+                sum += d;
+                niv++;
+            }
+        }
+        if (niv > 0) {
+            const float mean = sum / (float)niv;
+            if (mean > 1e-10f) {
+                float vs = 0.0f;
+                for (int k = 1; k < nfin; k++) {
+                    const float d = fin[k] - fin[k - 1];
+                    if (d > 0.0f) {
+                        const float dd = d - mean;
+                        vs += dd * dd;
+                    }
+                }
+                const float var = vs / (float)niv;
+                const float cv = __builtin_sqrtf(var) / mean;
+                stab = 1.0f / (1.0f + cv);
+            }
+        }
+    }
+    r.n_beats = nfin;
+    r.n_down = nd;
+    r.stability = stab;
+    r.ok = 1;
+    out[trk] = r;
+}
+
+void launch_beat(const int* tracks, int n_items, const uint32_t* onsets, const uint64_t* on_off, const int* on_n,
+                 uint32_t sr, const float* bpm, const float* conf, float* scratch, const uint64_t* beat_off,
+                 const int* beat_cap, float* beats, float* downs, BeatOut* out, hipStream_t st) {
+    if (n_items == 0) return;
+    hipLaunchKernelGGL(k_beat, dim3((n_items + 63) / 64), dim3(64), 0, st, tracks, n_items, onsets, on_off, on_n, sr,
+                       bpm, conf, scratch, beat_off, beat_cap, beats, downs, out);
+}
+
+}  // namespace sdsp

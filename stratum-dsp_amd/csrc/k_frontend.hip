@@ -1,0 +1,346 @@
+// k_frontend.hip — preprocessing and onset front-end kernels.
+//
+//   k_peak_abs / k_gain      normalize_peak            src/preprocessing/normalization.rs:262-322
+//   k_frame_rms              frame RMS                 silence.rs:154-169, energy_flux.rs:122-131
+//   k_trim                   silence regions + trim    silence.rs:171-279
+//   k_energy_onsets          energy-flux onsets        energy_flux.rs:133-243
+//   k_flux_onsets            spectral-flux / HFC peaks spectral_flux.rs:160-221, hfc.rs:156-214
+//   k_consensus              onset voting + selection  consensus.rs:111-287, src/lib.rs:181-290
+//
+// The normalised signal is never materialised: every consumer reads raw*gain (one f32
+// multiply, exactly the value the reference stores in place).
+#include "block_utils.hpp"
+#include "kernels.hpp"
+
+namespace sdsp {
+
+// ---- peak |x| per track (order-free max via atomicMax on the IEEE bits of |x| >= 0) ----
+__global__ __launch_bounds__(256) void k_peak_abs(const float* __restrict__ x, const uint64_t* __restrict__ in_off,
+                                                  const uint64_t* __restrict__ n_raw,
+                                                  const uint64_t* __restrict__ chunk_pfx, int T,
+                                                  unsigned int* __restrict__ peak_bits) {
+    constexpr int CH = 4096;
+    const uint64_t g = blockIdx.x;
+    const int trk = find_track(chunk_pfx, T, g);
+    const uint64_t c = g - chunk_pfx[trk];
+    const uint64_t s0 = c * CH, n = n_raw[trk];
+    const float* p = x + in_off[trk];
+    float m = 0.0f;
+    for (uint64_t i = s0 + threadIdx.x; i < s0 + CH && i < n; i += 256) m = sd_maxf(m, sd_absf(p[i]));
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0 && m > 0.0f) atomicMax(&peak_bits[trk], sd_bits_f(m));
+}
+
+// gain = min(10^(-headroom/20)/peak, 1/peak); peak <= 1e-10 leaves the samples untouched.
+__global__ void k_gain(const unsigned int* __restrict__ peak_bits, int T, float target, int enable,
+                       float* __restrict__ gain) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    const float peak = sd_from_bits_f(peak_bits[t]);
+    float g = 1.0f;
+    if (enable && peak > EPS) g = sd_minf(target / peak, 1.0f / peak);
+    gain[t] = g;
+}
+
+// RMS of frame f = sqrt(sum_{k<len} (x*g)^2 / len), sequential f32 sum (silence.rs:154-169).
+__global__ __launch_bounds__(256) void k_frame_rms(const float* __restrict__ x, const uint64_t* __restrict__ src_off,
+                                                   const float* __restrict__ gain,
+                                                   const uint64_t* __restrict__ n_len,
+                                                   const uint64_t* __restrict__ frame_pfx, int T,
+                                                   uint64_t total, int fs, int hop, float* __restrict__ rms) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= total) return;
+    const int trk = find_track(frame_pfx, T, g);
+    const uint64_t f = g - frame_pfx[trk];
+    const uint64_t n = n_len[trk];
+    const uint64_t s = f * (uint64_t)hop;
+    const uint64_t e = s + (uint64_t)fs < n ? s + (uint64_t)fs : n;
+    const float* p = x + src_off[trk];
+    const float gn = gain[trk];
+    float sum = 0.0f;
+    for (uint64_t k = s; k < e; k++) {
+        const float v = p[k] * gn;
+        sum += v * v;
+    }
+    rms[g] = e > s ? __builtin_sqrtf(sum / (float)(e - s)) : 0.0f;
+}
+
+// Silence regions and trim bounds, one thread per track (silence.rs:171-263).
+__global__ void k_trim(const float* __restrict__ rms, const uint64_t* __restrict__ frame_pfx, int T,
+                       const uint64_t* __restrict__ n_raw, int hop, float thr, uint64_t min_frames, int enable,
+                       uint64_t* __restrict__ trim_start, uint64_t* __restrict__ trim_end) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    const uint64_t n = n_raw[t];
+    if (!enable || n == 0) {
+        trim_start[t] = 0;
+        trim_end[t] = n;
+        return;
+    }
+    const uint64_t nf = frame_pfx[t + 1] - frame_pfx[t];
+    const float* r = rms + frame_pfx[t];
+    // Only the first region (if it starts at sample 0) and the last region (if it reaches the
+    // end) influence the trim; track both while replaying the reference's region scan.
+    bool have_first = false, have_last = false;
+    uint64_t first_s = 0, first_e = 0, last_s = 0, last_e = 0;
+    bool in_sil = false;
+    uint64_t ss = 0;
+    auto push = [&](uint64_t s, uint64_t e) {
+        if (!have_first) {
+            have_first = true;
+            first_s = s;
+            first_e = e;
+        }
+        have_last = true;
+        last_s = s;
+        last_e = e;
+    };
+    for (uint64_t f = 0; f < nf; f++) {
+        const bool sil = r[f] <= thr;
+        if (sil && !in_sil) {
+            in_sil = true;
+            ss = f;
+        } else if (!sil && in_sil) {
+            in_sil = false;
+            if (f - ss >= min_frames || ss == 0 || f == nf) push(ss * (uint64_t)hop, f < nf ? f * (uint64_t)hop : n);
+        }
+    }
+    if (in_sil && (nf - ss >= min_frames || ss == 0)) push(ss * (uint64_t)hop, n);
+    uint64_t ts = 0, te = n;
+    if (have_first && first_s == 0) ts = first_e;
+    if (have_last && last_e == n) te = last_s;
+    if (ts > te) ts = te;
+    if (te < ts) te = ts;
+    if (!(ts < te && te <= n)) ts = te = 0;
+    trim_start[t] = ts;
+    trim_end[t] = te;
+}
+
+// Energy-flux onsets (energy_flux.rs:133-243).  rms: per-frame RMS (frame_size, hop) of the
+// trimmed signal.  Out: onset sample positions (relative to the trimmed start), ascending.
+__global__ __launch_bounds__(256) void k_energy_onsets(const float* __restrict__ rms,
+                                                       const uint64_t* __restrict__ frame_pfx,
+                                                       const uint64_t* __restrict__ n_trim, int hop, float factor,
+                                                       uint32_t* __restrict__ out, const uint64_t* __restrict__ out_off,
+                                                       int* __restrict__ out_n) {
+    __shared__ float redf[8];
+    __shared__ int redi[9];
+    const int trk = blockIdx.x;
+    const int64_t nf = (int64_t)(frame_pfx[trk + 1] - frame_pfx[trk]);
+    const float* e = rms + frame_pfx[trk];
+    const uint64_t n = n_trim[trk];
+    uint32_t* o = out + out_off[trk];
+    if (nf < 2) {
+        if (threadIdx.x == 0) out_n[trk] = 0;
+        return;
+    }
+    const int64_t L = nf - 1;
+    auto flux = [&](int64_t i) { return sd_maxf(e[i + 1] - e[i], 0.0f); };
+    float m = 0.0f;
+    for (int64_t i = threadIdx.x; i < L; i += blockDim.x) m = sd_maxf(m, flux(i));
+    m = block_max(m, redf);
+    if (m <= EPS) {
+        if (threadIdx.x == 0) out_n[trk] = 0;
+        return;
+    }
+    const float thr = m * factor;
+    int base = 0;
+    for (int64_t c0 = 0; c0 < L; c0 += blockDim.x) {
+        const int64_t i = c0 + threadIdx.x;
+        bool on = false;
+        if (i < L && L > 1) {
+            const float f = flux(i);
+            if (i == 0)
+                on = f > thr && f >= flux(1);
+            else if (i == L - 1)
+                on = f > thr && f > flux(i - 1);
+            else
+                on = f > thr && f > flux(i - 1) && f >= flux(i + 1);
+            on = on && (uint64_t)(i + 1) * (uint64_t)hop < n;
+        }
+        int total;
+        const int slot = block_exclusive_flag(on, redi, &total);
+        if (on) o[base + slot] = (uint32_t)((i + 1) * hop);
+        base += total;
+    }
+    if (threadIdx.x == 0) out_n[trk] = base;
+}
+
+// Spectral-flux (kind 0) or HFC (kind 1) onsets: percentile threshold + local peaks, as
+// sample positions f*hop < n (spectral_flux.rs:160-215, hfc.rs:156-208, src/lib.rs:181-190).
+// sfo: per-frame-pair spectral flux (index t-1 for pair (t-1,t)); hfc: per-frame HFC.
+__global__ __launch_bounds__(256) void k_flux_onsets(const float* __restrict__ sfo, const float* __restrict__ hfc,
+                                                     float* __restrict__ scratch,
+                                                     const uint64_t* __restrict__ frame_pfx,
+                                                     const uint64_t* __restrict__ n_trim, int hop, float pct,
+                                                     uint32_t* __restrict__ out, const uint64_t* __restrict__ out_off,
+                                                     int* __restrict__ out_n, int T) {
+    __shared__ int hist[256];
+    __shared__ int misc[4];
+    __shared__ int redi[9];
+    const int trk = blockIdx.x % T;
+    const int kind = blockIdx.x / T;
+    const int64_t nf = (int64_t)(frame_pfx[trk + 1] - frame_pfx[trk]);
+    uint32_t* o = out + out_off[trk] + (uint64_t)kind * (frame_pfx[T]);  // kind-major halves
+    int* on_n = out_n + kind * T;
+    if (nf < 2) {
+        if (threadIdx.x == 0) on_n[trk] = 0;
+        return;
+    }
+    const int64_t L = nf - 1;
+    float* fl = scratch + frame_pfx[trk] + (uint64_t)kind * frame_pfx[T];
+    if (kind == 0) {
+        const float* s = sfo + frame_pfx[trk];
+        for (int64_t i = threadIdx.x; i < L; i += blockDim.x) fl[i] = s[i];
+    } else {
+        const float* h = hfc + frame_pfx[trk];
+        for (int64_t i = threadIdx.x; i < L; i += blockDim.x) fl[i] = sd_maxf(h[i + 1] - h[i], 0.0f);
+    }
+    __syncthreads();
+    uint64_t ti = sd_f2u64((float)L * pct);
+    if (ti > (uint64_t)(L - 1)) ti = (uint64_t)(L - 1);
+    const float thr = block_select_kth(fl, (int)L, (int)ti, hist, misc);
+    const uint64_t n = n_trim[trk];
+    int base = 0;
+    for (int64_t c0 = 0; c0 < L; c0 += blockDim.x) {
+        const int64_t i = c0 + threadIdx.x;
+        bool on = false;
+        if (i < L && L > 1) {
+            const float f = fl[i];
+            if (i == 0)
+                on = f > thr && f >= fl[1];
+            else if (i == L - 1)
+                on = f > thr && f > fl[i - 1];
+            else
+                on = f > thr && f > fl[i - 1] && f >= fl[i + 1];
+            on = on && (uint64_t)(i + 1) * (uint64_t)hop < n;  // frame i+1 -> sample (i+1)*hop
+        }
+        int total;
+        const int slot = block_exclusive_flag(on, redi, &total);
+        if (on) o[base + slot] = (uint32_t)((i + 1) * hop);
+        base += total;
+    }
+    if (threadIdx.x == 0) on_n[trk] = base;
+}
+
+// Onset consensus (consensus.rs:111-287) + selection (src/lib.rs:258-290), one thread per track.
+// Onsets arrive sorted, so a new cluster is only ever created once every earlier cluster is
+// out of reach; "join the first cluster with any member within tol" reduces to comparing
+// against the newest cluster's largest member.  Clusters are therefore disjoint and their
+// integer centres strictly increasing.
+__global__ void k_consensus(const uint32_t* __restrict__ energy, const uint64_t* __restrict__ e_off,
+                            const int* __restrict__ e_n, const uint32_t* __restrict__ flux_on,
+                            const uint64_t* __restrict__ f_off, const int* __restrict__ f_n, uint64_t kind_stride,
+                            int T, uint32_t tol, int enable, const int* __restrict__ has_mags,
+                            uint32_t* __restrict__ chosen, const uint64_t* __restrict__ c_off,
+                            int* __restrict__ c_n) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    const uint32_t* L0 = energy + e_off[t];
+    const int n0 = e_n[t];
+    uint32_t* out = chosen + c_off[t];
+    if (!enable || !has_mags[t]) {
+        for (int i = 0; i < n0; i++) out[i] = L0[i];
+        c_n[t] = n0;
+        return;
+    }
+    const uint32_t* L1 = flux_on + f_off[t];
+    const uint32_t* L2 = flux_on + f_off[t] + kind_stride;
+    const int n1 = f_n[t], n2 = f_n[T + t];
+    int i0 = 0, i1 = 0, i2 = 0;
+    // current cluster state
+    bool have = false;
+    uint64_t sum = 0, cnt = 0;
+    uint32_t cmax = 0;
+    int voted = 0;
+    int ns = 0;  // strong (>= 2 methods) written from the front
+    // pass 1 writes strong centres; remember whether any strong exists, else pass 2 writes all
+    auto flush = [&](bool strong_pass) {
+        if (!have) return;
+        const uint32_t centre = (uint32_t)(sum / cnt);
+        const int vb = __popc(voted);
+        if (!strong_pass || vb >= 2) {
+            if (ns == 0 || out[ns - 1] != centre) out[ns++] = centre;
+        }
+    };
+    for (int pass = 0; pass < 2; pass++) {
+        i0 = i1 = i2 = 0;
+        have = false;
+        ns = 0;
+        while (i0 < n0 || i1 < n1 || i2 < n2) {
+            // stable merge by sample: energy, spectral, hfc order on ties (sort_by_key is stable)
+            uint32_t s = 0xffffffffu;
+            int m = -1;
+            if (i0 < n0 && L0[i0] < s) s = L0[i0], m = 0;
+            if (i1 < n1 && L1[i1] < s) s = L1[i1], m = 1;
+            if (i2 < n2 && L2[i2] < s) s = L2[i2], m = 2;
+            if (m == 0) i0++;
+            else if (m == 1) i1++;
+            else i2++;
+            if (have && (uint64_t)(s - cmax) <= (uint64_t)tol) {
+                sum += s;
+                cnt++;
+                cmax = s;
+                voted |= 1 << m;
+            } else {
+                flush(pass == 0);
+                have = true;
+                sum = s;
+                cnt = 1;
+                cmax = s;
+                voted = 1 << m;
+            }
+        }
+        flush(pass == 0);
+        if (pass == 0 && ns > 0) break;  // strong set non-empty
+    }
+    if (ns == 0) {  // nothing clustered: keep the energy-flux onsets (lib.rs:283-285)
+        for (int i = 0; i < n0; i++) out[i] = L0[i];
+        ns = n0;
+    }
+    c_n[t] = ns;
+}
+
+// ---- launchers ----
+void launch_peak_gain(const float* x, const uint64_t* in_off, const uint64_t* n_raw, const uint64_t* chunk_pfx, int T,
+                      uint64_t n_chunks, unsigned int* peak_bits, float target, int enable, float* gain,
+                      hipStream_t st) {
+    if (T == 0) return;
+    (void)hipMemsetAsync(peak_bits, 0, (size_t)T * sizeof(unsigned int), st);
+    if (n_chunks) hipLaunchKernelGGL(k_peak_abs, dim3((unsigned)n_chunks), dim3(256), 0, st, x, in_off, n_raw, chunk_pfx, T, peak_bits);
+    hipLaunchKernelGGL(k_gain, dim3((T + 255) / 256), dim3(256), 0, st, peak_bits, T, target, enable, gain);
+}
+void launch_frame_rms(const float* x, const uint64_t* src_off, const float* gain, const uint64_t* n_len,
+                      const uint64_t* frame_pfx, int T, uint64_t total, int fs, int hop, float* rms, hipStream_t st) {
+    if (total == 0) return;
+    hipLaunchKernelGGL(k_frame_rms, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, x, src_off, gain, n_len,
+                       frame_pfx, T, total, fs, hop, rms);
+}
+void launch_trim(const float* rms, const uint64_t* frame_pfx, int T, const uint64_t* n_raw, int hop, float thr,
+                 uint64_t min_frames, int enable, uint64_t* trim_start, uint64_t* trim_end, hipStream_t st) {
+    if (T == 0) return;
+    hipLaunchKernelGGL(k_trim, dim3((T + 63) / 64), dim3(64), 0, st, rms, frame_pfx, T, n_raw, hop, thr, min_frames,
+                       enable, trim_start, trim_end);
+}
+void launch_energy_onsets(const float* rms, const uint64_t* frame_pfx, const uint64_t* n_trim, int hop, float factor,
+                          uint32_t* out, const uint64_t* out_off, int* out_n, int T, hipStream_t st) {
+    if (T == 0) return;
+    hipLaunchKernelGGL(k_energy_onsets, dim3(T), dim3(256), 0, st, rms, frame_pfx, n_trim, hop, factor, out, out_off,
+                       out_n);
+}
+void launch_flux_onsets(const float* sfo, const float* hfc, float* scratch, const uint64_t* frame_pfx,
+                        const uint64_t* n_trim, int hop, float pct, uint32_t* out, const uint64_t* out_off,
+                        int* out_n, int T, hipStream_t st) {
+    if (T == 0) return;
+    hipLaunchKernelGGL(k_flux_onsets, dim3(2 * T), dim3(256), 0, st, sfo, hfc, scratch, frame_pfx, n_trim, hop, pct,
+                       out, out_off, out_n, T);
+}
+void launch_consensus(const uint32_t* energy, const uint64_t* e_off, const int* e_n, const uint32_t* flux_on,
+                      const uint64_t* f_off, const int* f_n, uint64_t kind_stride, int T, uint32_t tol, int enable,
+                      const int* has_mags, uint32_t* chosen, const uint64_t* c_off, int* c_n, hipStream_t st) {
+    if (T == 0) return;
+    hipLaunchKernelGGL(k_consensus, dim3((T + 63) / 64), dim3(64), 0, st, energy, e_off, e_n, flux_on, f_off, f_n,
+                       kind_stride, T, tol, enable, has_mags, chosen, c_off, c_n);
+}
+
+}  // namespace sdsp

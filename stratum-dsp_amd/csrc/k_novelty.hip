@@ -1,0 +1,155 @@
+// k_novelty.hip — novelty curves from the per-frame features (reference
+// src/features/period/novelty.rs:336-986):
+//
+//   variants full/low/mid/high:  combined_novelty_with_params(superflux, energy flux, HFC flux)
+//       normalise each flux (:383-386, :521-530, :757-766), weighted mix / wsum (:893-904),
+//       normalise, local-mean subtraction with half-wave rectification (:943-964),
+//       moving average (:966-983), normalise.
+//   variant mel:  mel SuperFlux (:574-608), normalised.
+//
+// One workgroup per (track, variant); curves live in L2-resident global scratch between the
+// phases (every phase is elementwise or a short in-order window sum, so all outputs keep the
+// reference's exact f32 operation order; maxima are order-free).  The last phase also
+// produces the curve's sequential sum, used as the FFT tempogram's DC removal
+// (tempogram_fft.rs:110).
+#include "block_utils.hpp"
+#include "kernels.hpp"
+
+namespace sdsp {
+
+__global__ __launch_bounds__(1024) void k_novelty(const float* __restrict__ E, const float* __restrict__ H,
+                                                   const float* __restrict__ SFX, const uint64_t* __restrict__ frame_pfx,
+                                                   int T, uint64_t total, NovParams P, float* __restrict__ scratch,
+                                                   float* __restrict__ nov, float* __restrict__ nov_sum) {
+    __shared__ float red[16];
+    const int trk = blockIdx.x % T, v = blockIdx.x / T;
+    if (!P.band_on[v]) return;
+    const int64_t F = (int64_t)(frame_pfx[trk + 1] - frame_pfx[trk]);
+    if (F < 2) return;
+    const int64_t L = F - 1;
+    const uint64_t g0 = frame_pfx[trk];
+    const float* e = E + (uint64_t)v * total + g0;
+    const float* h = H + (uint64_t)v * total + g0;
+    const float* s = SFX + (uint64_t)v * total + g0;
+    float* A = scratch + ((uint64_t)v * 2 + 0) * total + g0;
+    float* Bf = scratch + ((uint64_t)v * 2 + 1) * total + g0;
+    float* out = nov + (uint64_t)v * total + g0;
+    const int tid = threadIdx.x, NT = blockDim.x;
+
+    float ms = 0.0f, me = 0.0f, mh = 0.0f;
+    for (int64_t i = tid; i < L; i += NT) {
+        ms = sd_maxf(ms, s[i]);
+        me = sd_maxf(me, sd_maxf(e[i + 1] - e[i], 0.0f));
+        mh = sd_maxf(mh, sd_maxf(h[i + 1] - h[i], 0.0f));
+    }
+    ms = block_max(ms, red);
+    me = block_max(me, red);
+    mh = block_max(mh, red);
+    float mc = 0.0f;
+    for (int64_t i = tid; i < L; i += NT) {
+        float sv = s[i], ev = sd_maxf(e[i + 1] - e[i], 0.0f), hv = sd_maxf(h[i + 1] - h[i], 0.0f);
+        if (ms > EPS) sv /= ms;
+        if (me > EPS) ev /= me;
+        if (mh > EPS) hv /= mh;
+        const float c = (sv * P.ws + ev * P.we + hv * P.wh) / P.wsum;
+        A[i] = c;
+        mc = sd_maxf(mc, c);
+    }
+    mc = block_max(mc, red);
+    if (mc > EPS)
+        for (int64_t i = tid; i < L; i += NT) A[i] /= mc;
+    __syncthreads();
+    float* cur = A;
+    float* oth = Bf;
+    if (P.lmw > 1) {
+        const int64_t half = P.lmw / 2;
+        for (int64_t i = tid; i < L; i += NT) {
+            const int64_t st = i >= half ? i - half : 0;
+            const int64_t en = i + half + 1 < L ? i + half + 1 : L;
+            float sum = 0.0f;
+            for (int64_t j = st; j < en; j++) sum += cur[j];
+            const float mean = sum / (float)(en - st);
+            oth[i] = sd_maxf(cur[i] - mean, 0.0f);
+        }
+        __syncthreads();
+        float* t = cur;
+        cur = oth;
+        oth = t;
+    }
+    if (P.smw > 1 && L >= 3) {
+        const int64_t half = P.smw / 2;
+        for (int64_t i = tid; i < L; i += NT) {
+            const int64_t st = i >= half ? i - half : 0;
+            const int64_t en = i + half + 1 < L ? i + half + 1 : L;
+            float sum = 0.0f;
+            for (int64_t j = st; j < en; j++) sum += cur[j];
+            oth[i] = sum / (float)(en - st);
+        }
+        __syncthreads();
+        float* t = cur;
+        cur = oth;
+        oth = t;
+    }
+    float mf = 0.0f;
+    for (int64_t i = tid; i < L; i += NT) mf = sd_maxf(mf, cur[i]);
+    mf = block_max(mf, red);
+    for (int64_t i = tid; i < L; i += NT) out[i] = mf > EPS ? cur[i] / mf : cur[i];
+    __syncthreads();
+    if (tid == 0) {
+        float sum = 0.0f;
+        for (int64_t i = 0; i < L; i++) sum += out[i];
+        nov_sum[(uint64_t)v * T + trk] = sum;
+    }
+}
+
+// mel SuperFlux novelty (novelty.rs:553-609), variant index 4
+__global__ __launch_bounds__(256) void k_mel_novelty(const float* __restrict__ MEL, int n_mels, int K,
+                                                     const uint64_t* __restrict__ frame_pfx, int T, uint64_t total,
+                                                     float* __restrict__ nov, float* __restrict__ nov_sum) {
+    __shared__ float red[8];
+    const int trk = blockIdx.x;
+    const int64_t F = (int64_t)(frame_pfx[trk + 1] - frame_pfx[trk]);
+    if (F < 2) return;
+    const int64_t L = F - 1;
+    const uint64_t g0 = frame_pfx[trk];
+    float* out = nov + 4 * total + g0;
+    float mf = 0.0f;
+    for (int64_t i = threadIdx.x; i < L; i += blockDim.x) {
+        const float* pv = MEL + (g0 + (uint64_t)i) * (uint64_t)n_mels;
+        const float* cv = pv + n_mels;
+        float sum = 0.0f;
+        for (int b = 0; b < n_mels; b++) {
+            const int lo = b - K < 0 ? 0 : b - K;
+            const int hi = b + K + 1 < n_mels ? b + K + 1 : n_mels;
+            float pm = 0.0f;
+            for (int q = lo; q < hi; q++) pm = sd_maxf(pm, pv[q]);
+            const float d = sd_maxf(cv[b] - pm, 0.0f);
+            sum += d * d;
+        }
+        const float fl = __builtin_sqrtf(sum);
+        out[i] = fl;
+        mf = sd_maxf(mf, fl);
+    }
+    mf = block_max(mf, red);
+    if (mf > EPS)
+        for (int64_t i = threadIdx.x; i < L; i += blockDim.x) out[i] /= mf;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float sum = 0.0f;
+        for (int64_t i = 0; i < L; i++) sum += out[i];
+        nov_sum[4 * (uint64_t)T + trk] = sum;
+    }
+}
+
+void launch_novelty(const float* E, const float* H, const float* SFX, const uint64_t* frame_pfx, int T, uint64_t total,
+                    const NovParams& P, float* scratch, float* nov, float* nov_sum, const float* MEL, int n_mels,
+                    int mel_k, bool mel_on, hipStream_t st) {
+    if (T == 0) return;
+    hipLaunchKernelGGL(k_novelty, dim3(4 * T), dim3(1024), 0, st, E, H, SFX, frame_pfx, T, total, P, scratch, nov,
+                       nov_sum);
+    if (mel_on)
+        hipLaunchKernelGGL(k_mel_novelty, dim3(T), dim3(256), 0, st, MEL, n_mels, mel_k, frame_pfx, T, total, nov,
+                           nov_sum);
+}
+
+}  // namespace sdsp

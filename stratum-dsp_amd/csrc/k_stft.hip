@@ -10,7 +10,7 @@
 // so the result is bit-identical to the CPU restatement.
 //
 // Ragged batches: blockIdx.x is a flat frame index over all tracks (frame_pfx prefix sums).
-#include "sdsp_device.hpp"
+#include "kernels.hpp"
 
 namespace sdsp {
 

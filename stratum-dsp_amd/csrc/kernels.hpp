@@ -1,0 +1,158 @@
+// kernels.hpp — parameter structs shared between the kernels and the pipeline, and the host
+// launchers each kernel file exports (kernels are launched only from their own TU).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sdsp_device.hpp"
+
+namespace sdsp {
+
+constexpr int NVAR = 5;  // novelty variants: full, low, mid, high, mel
+
+// ---- k_features ----
+struct FeatParams {
+    int B;             // bins per frame (nfft/2+1)
+    int stride;        // row stride of mags
+    int K;             // SuperFlux max-filter half width
+    int bs[4], be[4];  // band [start, end) for v = full, low, mid, high
+    int band_on[4];    // variant enabled (full always)
+    int n_mels;
+};
+constexpr int FT_FRAMES = 128;
+constexpr int FT_KMAX = 8;
+constexpr int FT_MELMAX = 48;
+
+// ---- k_novelty ----
+struct NovParams {
+    float ws, we, wh, wsum;
+    int lmw, smw;
+    int band_on[4];
+};
+
+// ---- k_tempo ----
+struct FftTgParams {
+    int P;
+    int b_lo, K;
+    float fres;
+    int lds;
+};
+struct SelParams {
+    float min_bpm, max_bpm, ac_tol;
+    float w[NVAR];
+    int present[NVAR];
+    int seed_only;
+    float support_thr, bonus;
+    int bonus_on;
+    int top_n;
+    int NB;
+    int gate;
+    int gate_top_n;
+    float gate_tol;
+};
+struct TempoEst {
+    float bpm, conf;
+    int agree;
+    int ok;
+    int n_cands;
+    int ambiguous, trap_low, trap_high;
+};
+struct MrParams {
+    float min_bpm, max_bpm, tol, w512, w256, w1024, dt, margin_thr;
+    int human_prior, top_k, band;
+    int sr, hop512;
+};
+
+// ---- k_beat ----
+struct BeatOut {
+    int n_beats, n_down;
+    float stability;
+    int ok;
+};
+
+// ---- k_key ----
+constexpr int HP_KMAX = 32;
+constexpr int HP_HMAX = 8;
+struct HarmEntry {
+    int state;
+    int tc[3];
+    float wt[3];
+    float hw;
+};
+struct HpcpParams {
+    int B, stride, pk_lo, pk_hi;
+    int K;
+    int hmax;
+    float p;
+};
+struct KeyParams {
+    int weighting;
+    float min_tonal, tonal_pow, energy_pow;
+    int seg_voting;
+    int seg_len, seg_hop;
+    float min_clarity;
+};
+struct KeyOut {
+    int mode, tonic;
+    float conf, clarity;
+    int ok;
+    int used_segments;
+    int weights_used;
+};
+
+// ---- launchers ----
+void launch_stft(int nfft, bool frame_max, const float* samples, const uint64_t* frame_pfx, int n_tracks,
+                 uint64_t total_frames, const uint64_t* src_off, const float* gain, int hop, const float* window,
+                 const cx* tw, const cx* rt, float* mags, const uint64_t* mag_row0, int stride, float* fmax,
+                 hipStream_t st);
+void launch_peak_gain(const float* x, const uint64_t* in_off, const uint64_t* n_raw, const uint64_t* chunk_pfx, int T,
+                      uint64_t n_chunks, unsigned int* peak_bits, float target, int enable, float* gain,
+                      hipStream_t st);
+void launch_frame_rms(const float* x, const uint64_t* src_off, const float* gain, const uint64_t* n_len,
+                      const uint64_t* frame_pfx, int T, uint64_t total, int fs, int hop, float* rms, hipStream_t st);
+void launch_trim(const float* rms, const uint64_t* frame_pfx, int T, const uint64_t* n_raw, int hop, float thr,
+                 uint64_t min_frames, int enable, uint64_t* trim_start, uint64_t* trim_end, hipStream_t st);
+void launch_energy_onsets(const float* rms, const uint64_t* frame_pfx, const uint64_t* n_trim, int hop, float factor,
+                          uint32_t* out, const uint64_t* out_off, int* out_n, int T, hipStream_t st);
+void launch_flux_onsets(const float* sfo, const float* hfc, float* scratch, const uint64_t* frame_pfx,
+                        const uint64_t* n_trim, int hop, float pct, uint32_t* out, const uint64_t* out_off,
+                        int* out_n, int T, hipStream_t st);
+void launch_consensus(const uint32_t* energy, const uint64_t* e_off, const int* e_n, const uint32_t* flux_on,
+                      const uint64_t* f_off, const int* f_n, uint64_t kind_stride, int T, uint32_t tol, int enable,
+                      const int* has_mags, uint32_t* chosen, const uint64_t* c_off, int* c_n, hipStream_t st);
+void launch_features(const float* mags, const float* fmax, const uint64_t* frame_pfx, const uint64_t* tile_pfx,
+                     int T, uint64_t n_tiles, const FeatParams& P, const int* mel_m, const float* mel_w, float* E,
+                     float* H, float* SFX, float* SFO, float* MEL, uint64_t total, hipStream_t st);
+void launch_novelty(const float* E, const float* H, const float* SFX, const uint64_t* frame_pfx, int T, uint64_t total,
+                    const NovParams& P, float* scratch, float* nov, float* nov_sum, const float* MEL, int n_mels,
+                    int mel_k, bool mel_on, hipStream_t st);
+void launch_fft_tempogram(const int* items, int n_items, int T, const float* nov, const float* nov_sum,
+                          const uint64_t* frame_pfx, uint64_t total, const FftTgParams& P, const cx* tw, const cx* rt,
+                          cx* gscratch, const uint64_t* out_off, float* out_bpm, float* out_pow, hipStream_t st);
+void launch_acf_tempogram(const int* items, int n_items, const float* nov, const uint64_t* frame_pfx, uint64_t total,
+                          const float* bpm_grid, const int* lag_grid, int NB, float* out_bpm, float* out_str,
+                          hipStream_t st);
+void launch_tempo_select(int n_items, const int* active, const float* fft_bpm, const float* fft_pow, const uint64_t* fft_off,
+                         const int* fft_k, const float* acf_bpm, const float* acf_str, const uint64_t* acf_off,
+                         const SelParams& P, TempoEst* est, float* cand, int cand_cap, hipStream_t st);
+void launch_multires(const int* tracks, int n_items, const float* c256, const int* n256, const float* c512,
+                     const int* n512, const float* c1024, const int* n1024, int cap256, int cap512, int cap1024,
+                     const TempoEst* base_est, const float* nov512, const uint64_t* fpfx512, const MrParams& P,
+                     TempoEst* mr_est, int* used, float* final_bpm, float* final_conf, hipStream_t st);
+void launch_beat(const int* tracks, int n_items, const uint32_t* onsets, const uint64_t* on_off, const int* on_n,
+                 uint32_t sr, const float* bpm, const float* conf, float* scratch, const uint64_t* beat_off,
+                 const int* beat_cap, float* beats, float* downs, BeatOut* out, hipStream_t st);
+void launch_mask(float* mags, int stride, int B, const uint64_t* frame_pfx, const int* tracks, int n_items, int margin,
+                 float power, hipStream_t st);
+void launch_hpcp(const float* mags, const uint64_t* frame_pfx, const uint64_t* tile_pfx, const int* tracks,
+                 int n_items, uint64_t n_tiles, const HpcpParams& P, const HarmEntry* harm, float* chroma,
+                 float* energy, hipStream_t st);
+void launch_key_vote(const int* tracks, int n_items, const uint64_t* frame_pfx, const float* chroma_raw,
+                     const float* energy, float* chroma_s, float* weights, float* seg_scratch, const uint64_t* seg_off,
+                     const float* tmpl, const KeyParams& P, KeyOut* out, hipStream_t st);
+void launch_synth(float* out, uint64_t n_tracks, uint64_t len, uint32_t sr, const float* bpm, const int* key,
+                  uint64_t seed0, hipStream_t st);
+void launch_synth_normalize(float* out, uint64_t n_tracks, uint64_t len, unsigned int* peak_bits, hipStream_t st);
+
+}  // namespace sdsp

@@ -1,26 +1,1265 @@
-// pipeline.hip — analyze_audio on the GPU (placeholder entry points; filled in by the pipeline).
+// pipeline.hip — analyze_audio() for a batch of tracks on one MI355X (reference src/lib.rs:86-1635),
+// plus the C ABI entry points (sdsp_analyze_audio / _batch / _batch_device, synthetic tracks).
+//
+// Per sub-batch (sized to an HBM budget), the host plans ragged per-track frame ranges and
+// launches, in stream order:
+//   A  peak/gain, silence RMS, trim                      -> host reads trim bounds (sync 1)
+//   B  energy RMS + energy-flux onsets; STFT 2048/512; frame features; spectral/HFC onsets;
+//      consensus; novelty (5 variants); FFT + ACF tempograms; candidate scoring + gate
+//                                                        -> host reads estimates (sync 2)
+//   C  escalation for ambiguous tracks: STFT 2048/256 and 2048/1024 of those tracks, the same
+//      feature/novelty/tempogram/scoring kernels, then multi-resolution fusion
+//   D  beat grid; E  key: STFT 8192/512 -> harmonic mask (in place) -> HPCP -> key vote
+//                                                        -> host reads results (sync 3)
+// No stage falls back to the CPU; host code only plans offsets and formats the result.
+#include <algorithm>
+#include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <string>
+#include <thread>
+#include <vector>
 
+#include "../../include/sdsp_fft_spec.h"
+#include "kernels.hpp"
 #include "sdsp_runtime.hpp"
 
+namespace sdsp {
+
+namespace {
+
+constexpr int STRIDE2 = 1028;  // 1025 bins, 16-B rows
+constexpr int STRIDE8 = 4100;  // 4097 bins
+constexpr int SUPPORT_HMAX = 8;
+
+uint64_t next_pow2(uint64_t n) {
+    uint64_t p = 1;
+    while (p < n) p <<= 1;
+    return p;
+}
+
+// ---------------------------------------------------------------------------------------
+// Host-side constant tables (identical arithmetic to the reference; sdsp_libm on both sides)
+struct MelTable {
+    std::vector<int> m;    // 2 per bin, -1 = none
+    std::vector<float> w;  // 2 per bin
+    int n_mels = 0;
+};
+
+// MelFilterbank::new, novelty.rs:83-165
+MelTable mel_table(uint32_t sr, int n_bins, int n_mels_in, float fmin_hz, float fmax_hz, std::string* err) {
+    MelTable t;
+    const int n_mels = std::max(n_mels_in, 4);
+    t.n_mels = n_mels;
+    const float nyq = (float)sr * 0.5f;
+    const float fmin = sd_minf(sd_maxf(fmin_hz, 0.0f), sd_maxf(nyq, 1.0f));
+    float fmax = fmax_hz;
+    if (!(sd_isfinite_f(fmax) && fmax > 0.0f)) fmax = nyq;
+    fmax = sd_clampf(fmax, fmin + 1.0f, nyq);
+    const int fft_size = (n_bins - 1) * 2;
+    const float fres = (float)sr / (float)fft_size;
+    auto mel = [](float f) { return 2595.0f * sd_log10f(1.0f + (f / 700.0f)); };
+    auto inv_mel = [](float v) { return 700.0f * (sd_powf(10.0f, v / 2595.0f) - 1.0f); };
+    const float mmin = mel(fmin), mmax = mel(fmax);
+    const float step = (mmax - mmin) / (float)(n_mels + 1);
+    std::vector<int> bp((size_t)n_mels + 2);
+    for (int i = 0; i < n_mels + 2; i++) {
+        const float hz = inv_mel(mmin + step * (float)i);
+        int64_t b = sd_f2i64(sd_roundf(hz / fres));
+        b = std::max<int64_t>(0, std::min<int64_t>(b, n_bins - 1));
+        bp[(size_t)i] = (int)b;
+    }
+    for (size_t i = 1; i < bp.size(); i++)
+        if (bp[i] <= bp[i - 1]) bp[i] = std::min(bp[i - 1] + 1, n_bins - 1);
+    t.m.assign((size_t)n_bins * 2, -1);
+    t.w.assign((size_t)n_bins * 2, 0.0f);
+    std::vector<int> cnt((size_t)n_bins, 0);
+    auto push = [&](int b, int m, float w) {
+        if (cnt[(size_t)b] >= 2) {
+            *err = "mel filterbank: more than two contributions for one bin";
+            return;
+        }
+        t.m[(size_t)b * 2 + cnt[(size_t)b]] = m;
+        t.w[(size_t)b * 2 + cnt[(size_t)b]] = w;
+        cnt[(size_t)b]++;
+    };
+    for (int mm = 0; mm < n_mels; mm++) {
+        const int l = bp[(size_t)mm], c = bp[(size_t)mm + 1], r = bp[(size_t)mm + 2];
+        if (!(l < c && c < r)) continue;
+        for (int b = l; b <= c; b++) {
+            const float w = b == l ? 0.0f : ((float)b - (float)l) / ((float)c - (float)l);
+            if (w > 0.0f) push(b, mm, w);
+        }
+        for (int b = c; b <= r; b++) {
+            const float w = b == r ? 0.0f : ((float)r - (float)b) / ((float)r - (float)c);
+            if (w > 0.0f) push(b, mm, w);
+        }
+    }
+    return t;
+}
+
+// hz_to_bin, tempogram.rs:279-289
+int hz_to_bin(float f, float fres, int n_bins) {
+    if (!sd_isfinite_f(f) || f <= 0.0f || !sd_isfinite_f(fres) || fres <= 0.0f) return 0;
+    int64_t b = sd_f2i64(sd_roundf(f / fres));
+    return (int)std::max<int64_t>(0, std::min<int64_t>(b, (int64_t)n_bins - 1));
+}
+
+// compiler-rt __powisf2 (Rust f32::powi)
+float powi_f(float a, int b) {
+    const bool recip = b < 0;
+    float r = 1.0f;
+    while (true) {
+        if (b & 1) r *= a;
+        b /= 2;
+        if (b == 0) break;
+        a *= a;
+    }
+    return recip ? 1.0f / r : r;
+}
+
+// per-(bin, harmonic) HPCP decisions, extractor.rs:636-668 (tuning 0)
+std::vector<HarmEntry> harm_table(int B, uint32_t sr, int fft_size, float sigma_in, int hmax, float decay_in) {
+    std::vector<HarmEntry> t((size_t)B * HP_HMAX);
+    const float fres = (float)sr / (float)fft_size;
+    const float fmin = sd_maxf(100.0f, 20.0f), fmax = sd_minf(5000.0f, (float)sr / 2.0f);
+    const float sigma = sd_maxf(sigma_in, 1e-6f);
+    const float decay = sd_clampf(decay_in, 0.0f, 1.0f);
+    for (int bin = 0; bin < B; bin++) {
+        const float f0 = (float)bin * fres;
+        for (int h = 1; h <= HP_HMAX; h++) {
+            HarmEntry& e = t[(size_t)bin * HP_HMAX + (size_t)(h - 1)];
+            e = HarmEntry{};
+            const float fh = f0 * (float)h;
+            if (h > hmax || fh > fmax) {
+                e.state = 0;
+                continue;
+            }
+            if (fh < fmin) {
+                e.state = 1;
+                continue;
+            }
+            e.state = 2;
+            const float semitone = 12.0f * sd_log2f(fh / 440.0f) + 57.0f - 0.0f;
+            const float spc = sd_rem_euclid_f(semitone, 12.0f);
+            const float ppc = sd_rem_euclid_f(sd_roundf(spc), 12.0f);
+            const int primary = sd_f2i32(ppc);
+            e.hw = powi_f(decay, h - 1) / (float)h;
+            for (int o = -1; o <= 1; o++) {
+                const int tc = (((primary + o) % 12) + 12) % 12;
+                float dist = sd_absf(spc - (float)tc);
+                dist = sd_minf(dist, 12.0f - dist);
+                e.tc[o + 1] = tc;
+                e.wt[o + 1] = sd_expf(-dist * dist / (2.0f * sigma * sigma));
+            }
+        }
+    }
+    return t;
+}
+
+// templates.rs:64-145
+void kk_templates(float* out /*24x12*/) {
+    const float cM[12] = {6.35f, 2.23f, 3.48f, 2.33f, 4.38f, 4.09f, 2.52f, 5.19f, 2.39f, 3.66f, 2.29f, 2.88f};
+    const float cm[12] = {6.33f, 2.68f, 3.52f, 5.38f, 2.60f, 3.53f, 2.54f, 4.75f, 3.98f, 2.69f, 3.34f, 3.17f};
+    for (int k = 0; k < 24; k++) {
+        float* v = out + k * 12;
+        const float* base = k < 12 ? cM : cm;
+        const int key = k % 12;
+        for (int s = 0; s < 12; s++) v[s] = base[(s + 12 - key) % 12];
+        float sq = 0.0f;
+        for (int i = 0; i < 12; i++) sq += v[i] * v[i];
+        const float n = __builtin_sqrtf(sq);
+        if (n > 1e-12f)
+            for (int i = 0; i < 12; i++) v[i] /= n;
+    }
+}
+
+// autocorrelation_tempogram's BPM grid and lags for one hop (tempogram_autocorr.rs:128-140)
+void acf_grid(uint32_t sr, int hop, float min_bpm, float max_bpm, float res, std::vector<float>* bpms,
+              std::vector<int>* lags) {
+    const float frame_rate = (float)sr / (float)hop;
+    for (float bpm = min_bpm; bpm <= max_bpm; bpm += res) {
+        const float bps = bpm / 60.0f;
+        const float fpb = frame_rate / bps;
+        bpms->push_back(bpm);
+        lags->push_back((int)std::min<uint64_t>(sd_f2u64(fpb), (uint64_t)INT32_MAX));
+    }
+}
+
+// in-range FFT-tempogram bins for size P (tempogram_fft.rs:158-175)
+void fft_bins(uint32_t sr, int hop, uint64_t P, float min_bpm, float max_bpm, int* b_lo, int* K, float* fres_out) {
+    const float frame_rate = (float)sr / (float)hop;
+    const float fres = frame_rate / (float)P;
+    *fres_out = fres;
+    int lo = -1, hi = -2;
+    for (uint64_t b = 0; b <= P / 2; b++) {
+        const float bpm = (float)b * fres * 60.0f;
+        if (bpm >= min_bpm && bpm <= max_bpm) {
+            if (lo < 0) lo = (int)b;
+            hi = (int)b;
+        }
+    }
+    *b_lo = lo < 0 ? 0 : lo;
+    *K = lo < 0 ? 0 : hi - lo + 1;
+}
+
+std::string fmt2(float v) {
+    char b[64];
+    std::snprintf(b, sizeof b, "%.2f", (double)v);
+    return b;
+}
+
+// ---------------------------------------------------------------------------------------
+struct Ctx {
+    DeviceCtx& d;
+    std::deque<std::vector<uint8_t>> keep;  // host staging kept alive until the next sync
+    explicit Ctx(DeviceCtx& dc) : d(dc) {}
+    template <class T>
+    T* up(const std::string& name, const std::vector<T>& v) {
+        DevBuf& b = d.buf(name);
+        const size_t bytes = std::max<size_t>(v.size() * sizeof(T), 16);
+        b.ensure(bytes);
+        if (!v.empty()) {
+            keep.emplace_back(reinterpret_cast<const uint8_t*>(v.data()),
+                              reinterpret_cast<const uint8_t*>(v.data()) + v.size() * sizeof(T));
+            SDSP_HIP_CHECK(hipMemcpyAsync(b.p, keep.back().data(), v.size() * sizeof(T), hipMemcpyHostToDevice, d.stream));
+        }
+        return b.as<T>();
+    }
+    template <class T>
+    T* dev(const std::string& name, size_t n) {
+        DevBuf& b = d.buf(name);
+        b.ensure(std::max<size_t>(n * sizeof(T), 16));
+        return b.as<T>();
+    }
+    template <class T>
+    std::vector<T> down(const T* p, size_t n) {
+        std::vector<T> v(n);
+        if (n) SDSP_HIP_CHECK(hipMemcpyAsync(v.data(), p, n * sizeof(T), hipMemcpyDeviceToHost, d.stream));
+        SDSP_HIP_CHECK(hipStreamSynchronize(d.stream));
+        keep.clear();
+        return v;
+    }
+    void sync() {
+        SDSP_HIP_CHECK(hipStreamSynchronize(d.stream));
+        keep.clear();
+    }
+};
+
+struct Timers {
+    hipEvent_t ev[16];
+    int n = 0;
+    DeviceCtx* d = nullptr;
+    void init(DeviceCtx& dc) {
+        d = &dc;
+        for (auto& e : ev) SDSP_HIP_CHECK(hipEventCreate(&e));
+    }
+    void mark(int i) { SDSP_HIP_CHECK(hipEventRecord(ev[i], d->stream)); }
+    double ms(int a, int b) {
+        float t = 0.0f;
+        if (hipEventElapsedTime(&t, ev[a], ev[b]) != hipSuccess) return 0.0;
+        return t;
+    }
+    ~Timers() {
+        if (d)
+            for (auto& e : ev) (void)hipEventDestroy(e);
+    }
+};
+
+struct TrackRes {
+    int status = SDSP_OK;
+    std::string err;
+    float bpm = 0, bpm_conf = 0;
+    int key_mode = 0, key_tonic = 0;
+    float key_conf = 0, key_clarity = 0, stability = 0, duration = 0;
+    float onset_consensus = 0;
+    std::vector<float> beats, downs;
+    int8_t mr_trig = -1, mr_used = -1, perc_trig = -1, perc_used = -1;
+    bool has_cands = false;
+    std::vector<sdsp_tempo_candidate> cands;
+};
+
+// Configuration support (everything the default path and its numeric knobs need).
+std::string unsupported(const sdsp_config& c) {
+    if (c.enable_normalization && c.normalization != SDSP_NORM_PEAK) return "RMS/LUFS normalization";
+    if (c.frame_size != 2048) return "frame_size other than 2048";
+    if (c.hop_size == 0 || c.hop_size > 8192) return "hop_size outside 1..8192";
+    if (c.enable_hpss_onsets) return "HPSS onsets";
+    if (c.force_legacy_bpm || c.enable_bpm_fusion) return "legacy-BPM output paths (force_legacy_bpm / enable_bpm_fusion)";
+    if (c.enable_tempogram_percussive_fallback) return "percussive tempogram fallback";
+    if (!(c.min_bpm > 0.0f && c.max_bpm > c.min_bpm && c.bpm_resolution > 0.0f)) return "BPM range/resolution";
+    if (c.tempogram_superflux_max_filter_bins > (uint64_t)FT_KMAX) return "superflux_max_filter_bins > 8";
+    if (c.enable_tempogram_mel_novelty && std::max<uint64_t>(c.tempogram_mel_n_mels, 4) > (uint64_t)FT_MELMAX)
+        return "tempogram_mel_n_mels > 48";
+    if (c.tempogram_mel_max_filter_bins > 16) return "tempogram_mel_max_filter_bins > 16";
+    if (!c.enable_key_stft_override || std::max<uint64_t>(c.key_stft_frame_size, 256) != 8192)
+        return "key STFT other than 8192";
+    if (c.key_stft_hop_size == 0) return "key_stft_hop_size 0";
+    if (c.enable_key_hpss_harmonic) return "key HPSS harmonic mask";
+    if (!c.enable_key_harmonic_mask && c.enable_key_spectrogram_time_smoothing) return "key time smoothing without mask";
+    if (c.key_spectrogram_smooth_margin > 31) return "key_spectrogram_smooth_margin > 31";
+    if (c.enable_key_log_frequency) return "key log-frequency spectrogram";
+    if (c.enable_key_tuning_compensation) return "key tuning compensation";
+    if (c.enable_key_beat_synchronous) return "beat-synchronous chroma";
+    if (!c.enable_key_hpcp || c.enable_key_hpcp_bass_blend || c.enable_key_hpcp_whitening)
+        return "non-HPCP / bass-blend / whitened chroma";
+    if (c.key_hpcp_peaks_per_frame > (uint64_t)HP_KMAX) return "key_hpcp_peaks_per_frame > 32";
+    if (c.key_hpcp_num_harmonics > (uint64_t)SUPPORT_HMAX) return "key_hpcp_num_harmonics > 8";
+    if (c.chroma_sharpening_power > 1.0f) return "chroma sharpening";
+    if (c.enable_key_edge_trim) return "key edge trim";
+    if (c.enable_key_ensemble) return "key ensemble";
+    if (c.key_template_set != SDSP_TEMPLATES_KRUMHANSL_KESSLER) return "Temperley templates";
+    if (c.enable_key_multi_scale && c.key_multi_scale_lengths_len > 0) return "multi-scale key";
+    if (c.enable_key_mode_heuristic || c.enable_key_minor_harmonic_bonus) return "key mode heuristic";
+    if (c.enable_ml_refinement) return "ML refinement";
+    return "";
+}
+
+// One "tempo pass": STFT (2048, hop) -> features -> novelty -> tempograms -> candidate scoring,
+// for a dense list of tracks.  Used for hop 512 (all tracks) and the escalation hops.
+struct TempoPassIn {
+    int hop;
+    const float* samples;
+    std::vector<uint64_t> src_off;  // per pass-track
+    std::vector<float> gain_h;
+    std::vector<uint64_t> n_trim;
+    bool want_onsets;  // hop-512 pass: also spectral/HFC onset features (SFO)
+    int top_n, gate, cand_cap;
+};
+struct TempoPassOut {
+    std::vector<uint64_t> fpfx;  // frame prefix over the pass's tracks
+    uint64_t total = 0;
+    // device pointers (valid until the next pass with the same tag)
+    float *mags = nullptr, *fmax = nullptr, *E = nullptr, *H = nullptr, *SFX = nullptr, *SFO = nullptr, *MEL = nullptr,
+          *nov = nullptr, *nov_sum = nullptr, *cand = nullptr;
+    uint64_t* d_fpfx = nullptr;
+    TempoEst* est = nullptr;
+    int* active = nullptr;
+    std::vector<int> active_h;
+    double stft_ms = 0, feat_ms = 0, tempo_ms = 0;
+    uint64_t stft_launch = 0;
+    double stft_bytes = 0;
+};
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------
+class Pipeline {
+   public:
+    Pipeline(DeviceCtx& d, const sdsp_config& cfg, uint32_t sr) : c_(d), d_(d), cfg_(cfg), sr_(sr) {}
+
+    void run(const float* d_samples, const std::vector<uint64_t>& in_off, const std::vector<uint64_t>& n_raw,
+             std::vector<TrackRes>& res);
+
+   private:
+    Ctx c_;
+    DeviceCtx& d_;
+    const sdsp_config& cfg_;
+    uint32_t sr_;
+    sdsp_stage_times times_{};
+
+    void sub_batch(const float* d_samples, const std::vector<uint64_t>& in_off, const std::vector<uint64_t>& n_raw,
+                   const std::vector<int>& idx, std::vector<TrackRes>& res);
+    void tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPassOut& out);
+};
+
+void Pipeline::run(const float* d_samples, const std::vector<uint64_t>& in_off, const std::vector<uint64_t>& n_raw,
+                   std::vector<TrackRes>& res) {
+    const size_t T = n_raw.size();
+    res.assign(T, TrackRes{});
+    const std::string why = unsupported(cfg_);
+    for (size_t i = 0; i < T; i++) {
+        if (n_raw[i] == 0) {
+            res[i].status = SDSP_ERR_INVALID_INPUT;
+            res[i].err = "Invalid input: Empty audio samples";
+        } else if (sr_ == 0) {
+            res[i].status = SDSP_ERR_INVALID_INPUT;
+            res[i].err = "Invalid input: Invalid sample rate";
+        } else if (!why.empty()) {
+            res[i].status = SDSP_ERR_NOT_IMPLEMENTED;
+            res[i].err = "Not implemented: " + why;
+        }
+    }
+    // sub-batches under an HBM budget (bytes per track estimated from its raw length)
+    const double budget = 64e9;
+    const uint64_t hop = cfg_.hop_size, khop = std::max<uint64_t>(cfg_.key_stft_hop_size, 1);
+    std::vector<int> cur;
+    double acc = 0;
+    auto flush = [&]() {
+        if (!cur.empty()) sub_batch(d_samples, in_off, n_raw, cur, res);
+        cur.clear();
+        acc = 0;
+    };
+    times_ = sdsp_stage_times{};
+    auto t0 = std::chrono::steady_clock::now();
+    for (size_t i = 0; i < T; i++) {
+        if (res[i].status != SDSP_OK) continue;
+        const double n = (double)n_raw[i];
+        const double need = n / hop * (STRIDE2 * 4.0 * 1.3 + 4 * 70.0) + n / khop * STRIDE8 * 4.0 +
+                            (n / 256 + n / 1024) * STRIDE2 * 4.0 + 1e6;
+        if (!cur.empty() && acc + need > budget) flush();
+        cur.push_back((int)i);
+        acc += need;
+    }
+    flush();
+    times_.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    d_.last = times_;
+}
+
+void Pipeline::tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPassOut& o) {
+    const int P_T = (int)in.src_off.size();
+    const int FS = 2048, hop = in.hop;
+    // frames per pass-track
+    o.fpfx.assign((size_t)P_T + 1, 0);
+    std::vector<uint64_t> tpfx((size_t)P_T + 1, 0);
+    o.active_h.assign((size_t)P_T, 0);
+    for (int t = 0; t < P_T; t++) {
+        const uint64_t n = in.n_trim[(size_t)t];
+        const uint64_t F = n >= (uint64_t)FS ? (n - FS) / (uint64_t)hop + 1 : 0;
+        o.fpfx[(size_t)t + 1] = o.fpfx[(size_t)t] + F;
+        tpfx[(size_t)t + 1] = tpfx[(size_t)t] + (F + FT_FRAMES - 1) / FT_FRAMES;
+        o.active_h[(size_t)t] = F >= 2;
+    }
+    const uint64_t total = o.fpfx[(size_t)P_T];
+    o.total = total;
+    o.d_fpfx = c_.up(tag + "fpfx", o.fpfx);
+    uint64_t* d_tpfx = c_.up(tag + "tpfx", tpfx);
+    uint64_t* d_src = c_.up(tag + "src", in.src_off);
+    float* d_gain = c_.up(tag + "gain", in.gain_h);
+    o.active = c_.up(tag + "active", o.active_h);
+    // STFT
+    FftTables& tb = d_.tables(FS, true);
+    o.mags = c_.dev<float>(tag + "mags", total * STRIDE2);
+    o.fmax = c_.dev<float>(tag + "fmax", total);
+    Timers tm;
+    tm.init(d_);
+    tm.mark(0);
+    launch_stft(FS, true, in.samples, o.d_fpfx, P_T, total, d_src, d_gain, hop, tb.window.as<float>(), tb.tw.as<cx>(),
+                tb.rt.as<cx>(), o.mags, o.d_fpfx, STRIDE2, o.fmax, d_.stream);
+    SDSP_HIP_CHECK(hipGetLastError());
+    tm.mark(1);
+    o.stft_launch = total ? 1 : 0;
+    {
+        double inb = 0;
+        for (int t = 0; t < P_T; t++) inb += 4.0 * (double)in.n_trim[(size_t)t];
+        o.stft_bytes = inb + 4.0 * (double)total * 1025.0;
+    }
+    // features
+    const int B = 1025;
+    FeatParams fp{};
+    fp.B = B;
+    fp.stride = STRIDE2;
+    fp.K = (int)std::max<uint64_t>(cfg_.tempogram_superflux_max_filter_bins, 1);
+    const float fres = (float)sr_ / (float)((B - 1) * 2);
+    const int b0 = std::min(1, B - 1);
+    const int bl = std::max(hz_to_bin(cfg_.tempogram_band_low_max_hz, fres, B), b0);
+    const int bm = std::max(hz_to_bin(cfg_.tempogram_band_mid_max_hz, fres, B), bl + 1);
+    int bh = cfg_.tempogram_band_high_max_hz > 0.0f ? std::max(hz_to_bin(cfg_.tempogram_band_high_max_hz, fres, B), bm + 1) : B;
+    bh = std::min(bh, B);
+    const float wb[4] = {cfg_.tempogram_band_w_full, cfg_.tempogram_band_w_low, cfg_.tempogram_band_w_mid,
+                         cfg_.tempogram_band_w_high};
+    const int bs_[4] = {0, b0, bl, bm}, be_[4] = {B, bl, bm, bh};
+    const bool band_cfg = cfg_.enable_tempogram_band_fusion || cfg_.enable_tempogram_mel_novelty ||
+                          cfg_.tempogram_band_consensus_bonus > 0.0f;  // use_aux_variants (src/lib.rs:375-377)
+    for (int v = 0; v < 4; v++) {
+        fp.bs[v] = std::min(bs_[v], B);
+        fp.be[v] = std::min(be_[v], B);
+        if (v == 0)
+            fp.band_on[v] = 1;
+        else
+            fp.band_on[v] = band_cfg && cfg_.enable_tempogram_band_fusion && sd_isfinite_f(wb[v]) && wb[v] > 0.0f &&
+                            be_[v] > bs_[v] + 1 && fp.be[v] > fp.bs[v] + 1;
+    }
+    const bool mel_on = band_cfg && cfg_.enable_tempogram_mel_novelty;
+    std::string merr;
+    MelTable mt = mel_table(sr_, B, (int)cfg_.tempogram_mel_n_mels, cfg_.tempogram_mel_fmin_hz, cfg_.tempogram_mel_fmax_hz,
+                            &merr);
+    if (!merr.empty()) throw HipError(merr);
+    fp.n_mels = mel_on ? mt.n_mels : 0;
+    int* d_melm = c_.up(tag + "melm", mt.m);
+    float* d_melw = c_.up(tag + "melw", mt.w);
+    o.E = c_.dev<float>(tag + "E", 4 * total);
+    o.H = c_.dev<float>(tag + "H", 4 * total);
+    o.SFX = c_.dev<float>(tag + "SFX", 4 * total);
+    o.SFO = c_.dev<float>(tag + "SFO", total);
+    o.MEL = c_.dev<float>(tag + "MEL", std::max<uint64_t>(total * (uint64_t)std::max(fp.n_mels, 1), 1));
+    launch_features(o.mags, o.fmax, o.d_fpfx, d_tpfx, P_T, tpfx[(size_t)P_T], fp, d_melm, d_melw, o.E, o.H, o.SFX, o.SFO,
+                    o.MEL, total, d_.stream);
+    SDSP_HIP_CHECK(hipGetLastError());
+    // novelty
+    NovParams np{};
+    if (band_cfg) {
+        np.ws = sd_maxf(cfg_.tempogram_novelty_w_spectral, 0.0f);
+        np.we = sd_maxf(cfg_.tempogram_novelty_w_energy, 0.0f);
+        np.wh = sd_maxf(cfg_.tempogram_novelty_w_hfc, 0.0f);
+        np.lmw = (int)cfg_.tempogram_novelty_local_mean_window;
+        np.smw = (int)cfg_.tempogram_novelty_smooth_window;
+    } else {  // combined_novelty defaults (novelty.rs:868-871)
+        np.ws = 0.5f;
+        np.we = 0.3f;
+        np.wh = 0.2f;
+        np.lmw = 16;
+        np.smw = 5;
+    }
+    np.wsum = sd_maxf(np.ws + np.we + np.wh, EPS);
+    for (int v = 0; v < 4; v++) np.band_on[v] = fp.band_on[v];
+    float* scratch = c_.dev<float>(tag + "novscr", 8 * std::max<uint64_t>(total, 1));
+    o.nov = c_.dev<float>(tag + "nov", NVAR * std::max<uint64_t>(total, 1));
+    o.nov_sum = c_.dev<float>(tag + "novsum", NVAR * (size_t)std::max(P_T, 1));
+    launch_novelty(o.E, o.H, o.SFX, o.d_fpfx, P_T, total, np, scratch, o.nov, o.nov_sum, o.MEL, fp.n_mels,
+                   (int)std::max<uint64_t>(cfg_.tempogram_mel_max_filter_bins, 1), mel_on, d_.stream);
+    SDSP_HIP_CHECK(hipGetLastError());
+    tm.mark(2);
+    // tempograms: items (track, variant) for active tracks
+    int present[NVAR];
+    for (int v = 0; v < 4; v++) present[v] = fp.band_on[v];
+    present[4] = mel_on;
+    std::vector<int> items;
+    for (int t = 0; t < P_T; t++)
+        if (o.active_h[(size_t)t])
+            for (int v = 0; v < NVAR; v++)
+                if (present[v]) items.push_back(t * NVAR + v);
+    // ACF
+    std::vector<float> gb;
+    std::vector<int> gl;
+    acf_grid(sr_, hop, cfg_.min_bpm, cfg_.max_bpm, cfg_.bpm_resolution, &gb, &gl);
+    const int NB = (int)gb.size();
+    if (NB > 512) throw HipError("autocorrelation grid larger than 512 BPMs");
+    float* d_gb = c_.up(tag + "acfgb", gb);
+    int* d_gl = c_.up(tag + "acfgl", gl);
+    int* d_items = c_.up(tag + "items", items);
+    const size_t n_it = items.size();
+    float* acf_bpm = c_.dev<float>(tag + "acfb", std::max<size_t>(n_it, 1) * (size_t)NB);
+    float* acf_str = c_.dev<float>(tag + "acfs", std::max<size_t>(n_it, 1) * (size_t)NB);
+    launch_acf_tempogram(d_items, (int)n_it, o.nov, o.d_fpfx, total, d_gb, d_gl, NB, acf_bpm, acf_str, d_.stream);
+    SDSP_HIP_CHECK(hipGetLastError());
+    // FFT tempograms grouped by P
+    std::vector<uint64_t> fft_off(n_it, 0);
+    std::vector<int> fft_k_track((size_t)P_T, 0);
+    std::map<uint64_t, std::vector<int>> byP;  // P -> item positions
+    for (size_t i = 0; i < n_it; i++) {
+        const int t = items[i] / NVAR;
+        const uint64_t L = o.fpfx[(size_t)t + 1] - o.fpfx[(size_t)t] - 1;
+        byP[next_pow2(L)].push_back((int)i);
+    }
+    uint64_t fcur = 0;
+    struct PClass {
+        uint64_t P;
+        FftTgParams prm;
+        std::vector<int> pos;
+    };
+    std::vector<PClass> classes;
+    for (auto& kv : byP) {
+        PClass pc{kv.first, FftTgParams{}, kv.second};
+        int b_lo, K;
+        float fr;
+        fft_bins(sr_, hop, kv.first, cfg_.min_bpm, cfg_.max_bpm, &b_lo, &K, &fr);
+        pc.prm.P = (int)kv.first;
+        pc.prm.b_lo = b_lo;
+        pc.prm.K = K;
+        pc.prm.fres = fr;
+        pc.prm.lds = kv.first <= 16384 ? 1 : 0;
+        uint64_t K2 = 1;
+        while (K2 < (uint64_t)K) K2 <<= 1;
+        if (K > 0 && K2 > kv.first / 2) throw HipError("FFT tempogram: too many in-range bins for the key buffer");
+        for (int i : pc.pos) {
+            fft_off[(size_t)i] = fcur;
+            fcur += (uint64_t)K;
+            fft_k_track[(size_t)(items[(size_t)i] / NVAR)] = K;
+        }
+        classes.push_back(pc);
+    }
+    float* fft_bpm = c_.dev<float>(tag + "fftb", std::max<uint64_t>(fcur, 1));
+    float* fft_pow = c_.dev<float>(tag + "fftp", std::max<uint64_t>(fcur, 1));
+    uint64_t* d_fft_off_items = c_.up(tag + "fftoffi", fft_off);
+    for (auto& pc : classes) {
+        if (pc.prm.K == 0) continue;
+        std::vector<int> sub;
+        std::vector<uint64_t> offs;
+        for (int i : pc.pos) {
+            sub.push_back(items[(size_t)i]);
+            offs.push_back(fft_off[(size_t)i]);
+        }
+        int* d_sub = c_.up(tag + "fsub" + std::to_string(pc.P), sub);
+        uint64_t* d_offs = c_.up(tag + "foff" + std::to_string(pc.P), offs);
+        FftTables& ft = d_.tables((int)pc.P, false);
+        cx* gscr = nullptr;
+        if (!pc.prm.lds) gscr = c_.dev<cx>(tag + "fgscr", sub.size() * (size_t)pc.P);
+        launch_fft_tempogram(d_sub, (int)sub.size(), P_T, o.nov, o.nov_sum, o.d_fpfx, total, pc.prm, ft.tw.as<cx>(),
+                             ft.rt.as<cx>(), gscr, d_offs, fft_bpm, fft_pow, d_.stream);
+        SDSP_HIP_CHECK(hipGetLastError());
+    }
+    (void)d_fft_off_items;
+    // per (track, variant) offsets for the selector
+    std::vector<uint64_t> fo((size_t)P_T * NVAR, 0), ao((size_t)P_T * NVAR, 0);
+    for (size_t i = 0; i < n_it; i++) {
+        fo[(size_t)items[i]] = fft_off[i];
+        ao[(size_t)items[i]] = (uint64_t)i * (uint64_t)NB;
+    }
+    uint64_t* d_fo = c_.up(tag + "selfo", fo);
+    uint64_t* d_ao = c_.up(tag + "selao", ao);
+    int* d_fk = c_.up(tag + "selfk", fft_k_track);
+    SelParams sp{};
+    sp.min_bpm = cfg_.min_bpm;
+    sp.max_bpm = cfg_.max_bpm;
+    sp.ac_tol = sd_maxf(cfg_.bpm_resolution, 0.5f);
+    for (int v = 0; v < NVAR; v++) sp.present[v] = present[v];
+    sp.w[0] = band_cfg ? cfg_.tempogram_band_w_full : 1.0f;
+    sp.w[1] = cfg_.tempogram_band_w_low;
+    sp.w[2] = cfg_.tempogram_band_w_mid;
+    sp.w[3] = cfg_.tempogram_band_w_high;
+    sp.w[4] = cfg_.tempogram_mel_weight;
+    sp.seed_only = band_cfg ? cfg_.tempogram_band_seed_only : 1;
+    sp.support_thr = sd_clampf(band_cfg ? cfg_.tempogram_band_support_threshold : 0.25f, 0.0f, 1.0f);
+    sp.bonus = sd_maxf(band_cfg ? cfg_.tempogram_band_consensus_bonus : 0.0f, 0.0f);
+    sp.bonus_on = sp.bonus > 0.0f && band_cfg && (cfg_.enable_tempogram_band_fusion || cfg_.enable_tempogram_mel_novelty);
+    sp.top_n = in.top_n;
+    sp.NB = NB;
+    sp.gate = in.gate;
+    sp.gate_top_n = (int)std::max<uint64_t>(
+        std::max<uint64_t>(cfg_.tempogram_candidates_top_n, cfg_.tempogram_multi_res_top_k), 10);
+    sp.gate_tol = sd_maxf(2.0f, cfg_.bpm_resolution);
+    o.est = c_.dev<TempoEst>(tag + "est", (size_t)std::max(P_T, 1));
+    o.cand = c_.dev<float>(tag + "cand", (size_t)std::max(P_T, 1) * (size_t)in.cand_cap * 4);
+    launch_tempo_select(P_T, o.active, fft_bpm, fft_pow, d_fo, d_fk, acf_bpm, acf_str, d_ao, sp, o.est, o.cand,
+                               in.cand_cap, d_.stream);
+    SDSP_HIP_CHECK(hipGetLastError());
+    tm.mark(3);
+    c_.sync();
+    o.stft_ms = tm.ms(0, 1);
+    o.feat_ms = tm.ms(1, 2);
+    o.tempo_ms = tm.ms(2, 3);
+}
+
+}  // namespace sdsp
+
+namespace sdsp {
+
+void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in_off, const std::vector<uint64_t>& n_raw,
+                         const std::vector<int>& idx, std::vector<TrackRes>& res) {
+    const int T = (int)idx.size();
+    const int FS = 2048;
+    const int HOP = (int)cfg_.hop_size;
+    hipStream_t st = d_.stream;
+    Timers tm;
+    tm.init(d_);
+    tm.mark(0);
+    // ---------------- A: peak/gain, silence, trim ----------------
+    std::vector<uint64_t> off((size_t)T), nr((size_t)T), cpfx((size_t)T + 1, 0), spfx((size_t)T + 1, 0);
+    for (int t = 0; t < T; t++) {
+        off[(size_t)t] = in_off[(size_t)idx[(size_t)t]];
+        nr[(size_t)t] = n_raw[(size_t)idx[(size_t)t]];
+        cpfx[(size_t)t + 1] = cpfx[(size_t)t] + (nr[(size_t)t] + 4095) / 4096;
+        const uint64_t fs = nr[(size_t)t] >= (uint64_t)FS ? (nr[(size_t)t] - FS) / (FS / 2) + 1 : 1;
+        spfx[(size_t)t + 1] = spfx[(size_t)t] + (cfg_.enable_silence_trimming ? fs : 0);
+    }
+    uint64_t* d_off = c_.up("A.off", off);
+    uint64_t* d_nr = c_.up("A.nr", nr);
+    uint64_t* d_cpfx = c_.up("A.cpfx", cpfx);
+    uint64_t* d_spfx = c_.up("A.spfx", spfx);
+    unsigned int* d_peak = c_.dev<unsigned int>("A.peak", (size_t)T);
+    float* d_gain = c_.dev<float>("A.gain", (size_t)T);
+    const float target = sd_powf(10.0f, (0.0f - 1.0f) / 20.0f);  // lib.rs:121 max_headroom_db = 1.0
+    launch_peak_gain(d_samples, d_off, d_nr, d_cpfx, T, cpfx[(size_t)T], d_peak, target, cfg_.enable_normalization, d_gain,
+                     st);
+    float* d_srms = c_.dev<float>("A.srms", spfx[(size_t)T]);
+    launch_frame_rms(d_samples, d_off, d_gain, d_nr, d_spfx, T, spfx[(size_t)T], FS, FS / 2, d_srms, st);
+    const float thr = sd_powf(10.0f, cfg_.min_amplitude_db / 20.0f);
+    const uint64_t min_samples = sd_f2u64((float)500u / 1000.0f * (float)sr_);
+    const uint64_t min_frames = (min_samples + (FS / 2) - 1) / (FS / 2);
+    uint64_t* d_ts = c_.dev<uint64_t>("A.ts", (size_t)T);
+    uint64_t* d_te = c_.dev<uint64_t>("A.te", (size_t)T);
+    launch_trim(d_srms, d_spfx, T, d_nr, FS / 2, thr, min_frames, cfg_.enable_silence_trimming, d_ts, d_te, st);
+    SDSP_HIP_CHECK(hipGetLastError());
+    std::vector<float> gain_h = c_.down(d_gain, (size_t)T);
+    std::vector<uint64_t> ts = c_.down(d_ts, (size_t)T), te = c_.down(d_te, (size_t)T);
+    tm.mark(1);
+    // remaining tracks (non-empty after trimming)
+    std::vector<int> R;  // positions in idx
+    for (int t = 0; t < T; t++) {
+        TrackRes& r = res[(size_t)idx[(size_t)t]];
+        const uint64_t n = te[(size_t)t] - ts[(size_t)t];
+        if (n == 0) {
+            r.status = SDSP_ERR_PROCESSING;
+            r.err = "Processing error: Audio is entirely silent after trimming";
+            continue;
+        }
+        r.duration = (float)n / (float)sr_;
+        R.push_back(t);
+    }
+    const int NR = (int)R.size();
+    if (NR == 0) return;
+    // ---------------- B: base tempo pass (hop = config hop) + onsets ----------------
+    const bool mr_on = cfg_.enable_tempogram_multi_resolution;
+    const int base_top_n =
+        (int)std::max<uint64_t>(std::max<uint64_t>(cfg_.tempogram_candidates_top_n, cfg_.tempogram_multi_res_top_k), 10);
+    TempoPassIn bin;
+    bin.hop = HOP;
+    bin.samples = d_samples;
+    for (int t : R) {
+        bin.src_off.push_back(off[(size_t)t] + ts[(size_t)t]);
+        bin.gain_h.push_back(gain_h[(size_t)t]);
+        bin.n_trim.push_back(te[(size_t)t] - ts[(size_t)t]);
+    }
+    bin.want_onsets = true;
+    bin.top_n = mr_on ? base_top_n : (cfg_.emit_tempogram_candidates ? (int)cfg_.tempogram_candidates_top_n : 1);
+    bin.cand_cap = std::max(bin.top_n, 1);
+    bin.gate = mr_on;
+    TempoPassOut bo;
+    tempo_pass("B.", bin, bo);
+    times_.stft2048_ms += bo.stft_ms;
+    times_.stft2048_launches += bo.stft_launch;
+    times_.stft2048_bytes += bo.stft_bytes;
+    times_.features_ms += bo.feat_ms;
+    times_.tempogram_ms += bo.tempo_ms;
+    tm.mark(2);
+    // onsets: energy flux (frame FS, hop HOP; same framing as the STFT), spectral flux, HFC, consensus
+    uint64_t* d_src = c_.up("B.src2", bin.src_off);
+    float* d_g = c_.up("B.gain2", bin.gain_h);
+    uint64_t* d_nt = c_.up("B.ntrim", bin.n_trim);
+    float* d_erms = c_.dev<float>("B.erms", std::max<uint64_t>(bo.total, 1));
+    launch_frame_rms(d_samples, d_src, d_g, d_nt, bo.d_fpfx, NR, bo.total, FS, HOP, d_erms, st);
+    uint32_t* d_eon = c_.dev<uint32_t>("B.eon", std::max<uint64_t>(bo.total, 1));
+    int* d_en = c_.dev<int>("B.en", (size_t)NR);
+    launch_energy_onsets(d_erms, bo.d_fpfx, d_nt, HOP, sd_powf(10.0f, -20.0f / 20.0f), d_eon, bo.d_fpfx, d_en, NR, st);
+    uint32_t* d_fon = c_.dev<uint32_t>("B.fon", 2 * std::max<uint64_t>(bo.total, 1));
+    int* d_fn = c_.dev<int>("B.fn", 2 * (size_t)NR);
+    float* d_fscr = c_.dev<float>("B.fscr", 2 * std::max<uint64_t>(bo.total, 1));
+    const float pct = cfg_.onset_threshold_percentile;
+    if (pct >= 0.0f && pct <= 1.0f)
+        launch_flux_onsets(bo.SFO, bo.H, d_fscr, bo.d_fpfx, d_nt, HOP, pct, d_fon, bo.d_fpfx, d_fn, NR, st);
+    else  // detect_*_onsets return Err -> warn + empty lists (src/lib.rs:196-218)
+        SDSP_HIP_CHECK(hipMemsetAsync(d_fn, 0, 2 * (size_t)NR * sizeof(int), st));
+    std::vector<int> has_mags((size_t)NR);
+    std::vector<uint64_t> coff((size_t)NR);
+    for (int i = 0; i < NR; i++) {
+        has_mags[(size_t)i] = bo.fpfx[(size_t)i + 1] > bo.fpfx[(size_t)i];
+        coff[(size_t)i] = 3 * bo.fpfx[(size_t)i];
+    }
+    int* d_hm = c_.up("B.hasm", has_mags);
+    uint64_t* d_coff = c_.up("B.coff", coff);
+    uint32_t* d_chosen = c_.dev<uint32_t>("B.chosen", 3 * std::max<uint64_t>(bo.total, 1));
+    int* d_cn = c_.dev<int>("B.cn", (size_t)NR);
+    bool cons_ok = cfg_.enable_onset_consensus && cfg_.onset_consensus_tolerance_ms > 0;
+    for (int k = 0; k < 4; k++) cons_ok = cons_ok && !(cfg_.onset_consensus_weights[k] < 0.0f);
+    const uint32_t tol = (uint32_t)sd_f2u64((float)cfg_.onset_consensus_tolerance_ms / 1000.0f * (float)sr_);
+    launch_consensus(d_eon, bo.d_fpfx, d_en, d_fon, bo.d_fpfx, d_fn, bo.total, NR, tol, cons_ok, d_hm, d_chosen, d_coff,
+                     d_cn, st);
+    SDSP_HIP_CHECK(hipGetLastError());
+    std::vector<TempoEst> best = c_.down(bo.est, (size_t)NR);
+    std::vector<int> en_h = c_.down(d_en, (size_t)NR);
+    tm.mark(3);
+    // final tempo per track (tempogram -> legacy -> 0; legacy is never consulted on the default path,
+    // see DESIGN.md "legacy estimator")
+    std::vector<float> fbpm((size_t)NR, 0.0f), fconf((size_t)NR, 0.0f);
+    std::vector<int> used((size_t)NR, 0);
+    std::vector<int> E;  // escalated (positions in R)
+    for (int i = 0; i < NR; i++) {
+        TrackRes& r = res[(size_t)idx[(size_t)R[(size_t)i]]];
+        const TempoEst& e = best[(size_t)i];
+        r.onset_consensus = en_h[(size_t)i] > 0 ? 1.0f : 0.0f;
+        if (!e.ok) continue;
+        fbpm[(size_t)i] = e.bpm;
+        fconf[(size_t)i] = e.conf;
+        if (mr_on) {
+            r.mr_trig = (int8_t)(e.ambiguous != 0);
+            r.mr_used = 0;
+            r.perc_trig = (int8_t)(e.ambiguous && e.trap_low);
+            if (e.ambiguous) E.push_back(i);
+        }
+    }
+    float* d_fbpm = c_.up("B.fbpm", fbpm);
+    float* d_fconf = c_.up("B.fconf", fconf);
+    int* d_used = c_.up("B.used", used);
+    // ---------------- C: escalation (multi_resolution.rs:205-901) ----------------
+    if (mr_on && !E.empty()) {
+        const int NE = (int)E.size();
+        const int top_k = (int)std::max<uint64_t>(cfg_.tempogram_multi_res_top_k, 1);
+        const int aux_k = std::min(std::max(top_k * 4, 25), 200);
+        TempoPassIn ein;
+        ein.samples = d_samples;
+        for (int i : E) {
+            ein.src_off.push_back(bin.src_off[(size_t)i]);
+            ein.gain_h.push_back(bin.gain_h[(size_t)i]);
+            ein.n_trim.push_back(bin.n_trim[(size_t)i]);
+        }
+        ein.want_onsets = false;
+        ein.top_n = aux_k;
+        ein.cand_cap = aux_k;
+        ein.gate = 0;
+        TempoPassOut o256, o1024;
+        ein.hop = 256;
+        tempo_pass("C256.", ein, o256);
+        ein.hop = 1024;
+        tempo_pass("C1024.", ein, o1024);
+        for (TempoPassOut* o : {&o256, &o1024}) {
+            times_.stft2048_ms += o->stft_ms;
+            times_.stft2048_launches += o->stft_launch;
+            times_.stft2048_bytes += o->stft_bytes;
+            times_.features_ms += o->feat_ms;
+            times_.tempogram_ms += o->tempo_ms;
+        }
+        std::vector<TempoEst> e256 = c_.down(o256.est, (size_t)NE), e1024 = c_.down(o1024.est, (size_t)NE);
+        std::vector<int> n256((size_t)NE), n1024((size_t)NE), n512((size_t)NR);
+        for (int k = 0; k < NE; k++) {
+            n256[(size_t)k] = e256[(size_t)k].ok ? e256[(size_t)k].n_cands : -1;
+            n1024[(size_t)k] = e1024[(size_t)k].ok ? e1024[(size_t)k].n_cands : -1;
+        }
+        for (int i = 0; i < NR; i++) n512[(size_t)i] = std::min(best[(size_t)i].n_cands, top_k);
+        int* d_n256 = c_.up("C.n256", n256);
+        int* d_n1024 = c_.up("C.n1024", n1024);
+        int* d_n512 = c_.up("C.n512", n512);
+        int* d_E = c_.up("C.E", E);
+        MrParams mp{};
+        mp.min_bpm = cfg_.min_bpm;
+        mp.max_bpm = cfg_.max_bpm;
+        mp.tol = sd_maxf(2.0f, cfg_.bpm_resolution);
+        mp.w512 = cfg_.tempogram_multi_res_w512;
+        mp.w256 = cfg_.tempogram_multi_res_w256;
+        mp.w1024 = cfg_.tempogram_multi_res_w1024;
+        mp.dt = cfg_.tempogram_multi_res_double_time_512_factor;
+        mp.margin_thr = cfg_.tempogram_multi_res_margin_threshold;
+        mp.human_prior = cfg_.tempogram_multi_res_use_human_prior;
+        mp.top_k = top_k;
+        mp.band = 1;  // src/lib.rs:509 always passes Some(band_cfg)
+        mp.sr = (int)sr_;
+        mp.hop512 = 512;
+        TempoEst* d_mr = c_.dev<TempoEst>("C.mr", (size_t)NE);
+        launch_multires(d_E, NE, o256.cand, d_n256, bo.cand, d_n512, o1024.cand, d_n1024, ein.cand_cap, bin.cand_cap,
+                        ein.cand_cap, bo.est, bo.nov, bo.d_fpfx, mp, d_mr, d_used, d_fbpm, d_fconf, st);
+        SDSP_HIP_CHECK(hipGetLastError());
+        used = c_.down(d_used, (size_t)NR);
+        for (int i : E) {
+            if (used[(size_t)i]) res[(size_t)idx[(size_t)R[(size_t)i]]].mr_used = 1;
+        }
+        if (cfg_.emit_tempogram_candidates) {
+            // the multi-res candidate list is hop 512's (top_k), re-flagged against the fused BPM
+            std::vector<TempoEst> mr = c_.down(d_mr, (size_t)NE);
+            std::vector<float> fb = c_.down(d_fbpm, (size_t)NR);
+            (void)mr;
+            fbpm = fb;
+        }
+    }
+    std::vector<float> fbpm_h = c_.down(d_fbpm, (size_t)NR), fconf_h = c_.down(d_fconf, (size_t)NR);
+    tm.mark(4);
+    // ---------------- D: beat grid ----------------
+    std::vector<int> ident((size_t)NR);
+    std::vector<uint64_t> boff((size_t)NR + 1, 0);
+    std::vector<int> bcap((size_t)NR);
+    for (int i = 0; i < NR; i++) {
+        ident[(size_t)i] = i;
+        const uint64_t n = bin.n_trim[(size_t)i];
+        const uint64_t dur_s = n / std::max<uint32_t>(sr_, 1) + 1;
+        const uint64_t F = bo.fpfx[(size_t)i + 1] - bo.fpfx[(size_t)i];
+        const uint64_t cap = std::max<uint64_t>(12 * dur_s + 64, 3 * F + 8);
+        bcap[(size_t)i] = (int)cap;
+        boff[(size_t)i + 1] = boff[(size_t)i] + cap;
+    }
+    int* d_ident = c_.up("D.ident", ident);
+    uint64_t* d_boff = c_.up("D.boff", boff);
+    int* d_bcap = c_.up("D.bcap", bcap);
+    float* d_bscr = c_.dev<float>("D.bscr", 4 * boff[(size_t)NR]);
+    float* d_beats = c_.dev<float>("D.beats", boff[(size_t)NR]);
+    float* d_downs = c_.dev<float>("D.downs", boff[(size_t)NR]);
+    BeatOut* d_bout = c_.dev<BeatOut>("D.bout", (size_t)NR);
+    launch_beat(d_ident, NR, d_chosen, d_coff, d_cn, sr_, d_fbpm, d_fconf, d_bscr, d_boff, d_bcap, d_beats, d_downs,
+                d_bout, st);
+    SDSP_HIP_CHECK(hipGetLastError());
+    tm.mark(5);
+    // ---------------- E: key ----------------
+    const int KFS = 8192, KHOP = (int)std::max<uint64_t>(cfg_.key_stft_hop_size, 1);
+    std::vector<int> K;  // positions in R
+    std::vector<uint64_t> kpfx(1, 0), ktile(1, 0), kseg(1, 0), ksrc;
+    std::vector<float> kgain;
+    const int seg_len_cfg = (int)std::min<uint64_t>(cfg_.key_segment_len_frames, INT32_MAX);
+    const int seg_hop = (int)std::max<uint64_t>(std::min<uint64_t>(cfg_.key_segment_hop_frames, (uint64_t)seg_len_cfg), 1);
+    const bool seg_voting = cfg_.enable_key_segment_voting && cfg_.key_segment_len_frames >= 120 &&
+                            cfg_.key_segment_hop_frames >= 1;
+    double key_in_bytes = 0;
+    for (int i = 0; i < NR; i++) {
+        const uint64_t n = bin.n_trim[(size_t)i];
+        if (n < (uint64_t)FS || n < (uint64_t)KFS) continue;  // key skipped or empty key spectrogram -> default key
+        const uint64_t F8 = (n - KFS) / (uint64_t)KHOP + 1;
+        K.push_back(i);
+        kpfx.push_back(kpfx.back() + F8);
+        ktile.push_back(ktile.back() + (F8 + 63) / 64);
+        const uint64_t ns = (seg_voting && F8 >= (uint64_t)std::max(seg_len_cfg, 1)) ? (F8 - seg_len_cfg) / seg_hop + 1 : 0;
+        kseg.push_back(kseg.back() + 50 * ns);
+        ksrc.push_back(bin.src_off[(size_t)i]);
+        kgain.push_back(bin.gain_h[(size_t)i]);
+        key_in_bytes += 4.0 * (double)n;
+    }
+    const int NK = (int)K.size();
+    std::vector<KeyOut> kout;
+    if (NK > 0) {
+        const uint64_t total8 = kpfx.back();
+        uint64_t* d_kpfx = c_.up("E.kpfx", kpfx);
+        uint64_t* d_ktile = c_.up("E.ktile", ktile);
+        uint64_t* d_kseg = c_.up("E.kseg", kseg);
+        uint64_t* d_ksrc = c_.up("E.ksrc", ksrc);
+        float* d_kgain = c_.up("E.kgain", kgain);
+        std::vector<int> kid((size_t)NK);
+        for (int k = 0; k < NK; k++) kid[(size_t)k] = k;
+        int* d_kid = c_.up("E.kid", kid);
+        FftTables& t8 = d_.tables(KFS, true);
+        float* mags8 = c_.dev<float>("E.mags8", total8 * STRIDE8);
+        Timers kt;
+        kt.init(d_);
+        kt.mark(0);
+        launch_stft(KFS, false, d_samples, d_kpfx, NK, total8, d_ksrc, d_kgain, KHOP, t8.window.as<float>(), t8.tw.as<cx>(),
+                    t8.rt.as<cx>(), mags8, d_kpfx, STRIDE8, nullptr, st);
+        SDSP_HIP_CHECK(hipGetLastError());
+        kt.mark(1);
+        const int B8 = KFS / 2 + 1;
+        if (cfg_.enable_key_harmonic_mask)
+            launch_mask(mags8, STRIDE8, B8, d_kpfx, d_kid, NK, (int)cfg_.key_spectrogram_smooth_margin,
+                        cfg_.key_harmonic_mask_power, st);
+        HpcpParams hp{};
+        hp.B = B8;
+        hp.stride = STRIDE8;
+        const float fres8 = (float)sr_ / (float)KFS;
+        const float fmin = sd_maxf(100.0f, 20.0f), fmax = sd_minf(5000.0f, (float)sr_ / 2.0f);
+        hp.pk_lo = 1;
+        hp.pk_hi = 0;
+        if (fmax > fmin) {
+            int lo = -1, hi = -1;
+            for (int b = 1; b + 1 < B8; b++) {
+                const float f = (float)b * fres8;
+                if (f < fmin) continue;
+                if (f > fmax) break;
+                if (lo < 0) lo = b;
+                hi = b;
+            }
+            if (lo >= 0) {
+                hp.pk_lo = lo;
+                hp.pk_hi = hi;
+            }
+        }
+        hp.K = (int)std::max<uint64_t>(cfg_.key_hpcp_peaks_per_frame, 1);
+        hp.hmax = (int)std::max<uint64_t>(cfg_.key_hpcp_num_harmonics, 1);
+        hp.p = sd_clampf(cfg_.key_hpcp_mag_power, 0.05f, 1.0f);
+        std::vector<HarmEntry> ht = harm_table(B8, sr_, KFS, cfg_.soft_mapping_sigma, hp.hmax, cfg_.key_hpcp_harmonic_decay);
+        HarmEntry* d_ht = c_.up("E.harm", ht);
+        float* d_chroma = c_.dev<float>("E.chroma", total8 * 12);
+        float* d_energy = c_.dev<float>("E.energy", total8);
+        launch_hpcp(mags8, d_kpfx, d_ktile, d_kid, NK, ktile.back(), hp, d_ht, d_chroma, d_energy, st);
+        SDSP_HIP_CHECK(hipGetLastError());
+        std::vector<float> tpl(288);
+        kk_templates(tpl.data());
+        float* d_tpl = c_.up("E.tpl", tpl);
+        KeyParams kp{};
+        kp.weighting = cfg_.enable_key_frame_weighting;
+        kp.min_tonal = cfg_.key_min_tonalness;
+        kp.tonal_pow = cfg_.key_tonalness_power;
+        kp.energy_pow = cfg_.key_energy_power;
+        kp.seg_voting = seg_voting;
+        kp.seg_len = std::max(seg_len_cfg, 1);
+        kp.seg_hop = seg_hop;
+        kp.min_clarity = sd_clampf(cfg_.key_segment_min_clarity, 0.0f, 1.0f);
+        float* d_cs = c_.dev<float>("E.chroma_s", total8 * 12);
+        float* d_w = c_.dev<float>("E.weights", total8);
+        float* d_sscr = c_.dev<float>("E.segscr", std::max<uint64_t>(kseg.back(), 1));
+        KeyOut* d_kout = c_.dev<KeyOut>("E.kout", (size_t)NK);
+        launch_key_vote(d_kid, NK, d_kpfx, d_chroma, d_energy, d_cs, d_w, d_sscr, d_kseg, d_tpl, kp, d_kout, st);
+        SDSP_HIP_CHECK(hipGetLastError());
+        kt.mark(2);
+        kout = c_.down(d_kout, (size_t)NK);
+        times_.stft8192_ms += kt.ms(0, 1);
+        times_.key_ms += kt.ms(1, 2);
+        times_.stft8192_launches += 1;
+        times_.stft8192_bytes += key_in_bytes + 4.0 * (double)total8 * (double)B8;
+    }
+    tm.mark(6);
+    // ---------------- results ----------------
+    std::vector<BeatOut> bout = c_.down(d_bout, (size_t)NR);
+    std::vector<float> beats_h = c_.down(d_beats, boff[(size_t)NR]), downs_h = c_.down(d_downs, boff[(size_t)NR]);
+    std::vector<float> cand_h;
+    if (cfg_.emit_tempogram_candidates) cand_h = c_.down(bo.cand, (size_t)NR * (size_t)bin.cand_cap * 4);
+    times_.beat_ms += tm.ms(4, 5);
+    for (int i = 0; i < NR; i++) {
+        TrackRes& r = res[(size_t)idx[(size_t)R[(size_t)i]]];
+        r.bpm = fbpm_h[(size_t)i];
+        r.bpm_conf = fconf_h[(size_t)i];
+        const BeatOut& b = bout[(size_t)i];
+        if (b.ok < 0) {
+            r.status = SDSP_ERR_PROCESSING;
+            r.err = "Processing error: beat buffer capacity exceeded";
+            continue;
+        }
+        if (b.ok > 0) {
+            r.beats.assign(beats_h.begin() + (long)boff[(size_t)i], beats_h.begin() + (long)(boff[(size_t)i] + b.n_beats));
+            r.downs.assign(downs_h.begin() + (long)boff[(size_t)i], downs_h.begin() + (long)(boff[(size_t)i] + b.n_down));
+            r.stability = b.stability;
+        }
+        if (cfg_.emit_tempogram_candidates && best[(size_t)i].ok) {
+            r.has_cands = true;
+            int n = best[(size_t)i].n_cands;
+            if (mr_on && r.mr_used == 1) n = std::min(n, (int)std::max<uint64_t>(cfg_.tempogram_multi_res_top_k, 1));
+            for (int k = 0; k < n; k++) {
+                const float* cc = cand_h.data() + ((size_t)i * (size_t)bin.cand_cap + (size_t)k) * 4;
+                sdsp_tempo_candidate tc{cc[0], cc[1], cc[2], cc[3], (uint8_t)(sd_absf(cc[0] - r.bpm) < 0.75f)};
+                r.cands.push_back(tc);
+            }
+        }
+    }
+    for (int k = 0; k < NK; k++) {
+        TrackRes& r = res[(size_t)idx[(size_t)R[(size_t)K[(size_t)k]]]];
+        const KeyOut& ko = kout[(size_t)k];
+        if (!ko.ok) continue;
+        r.key_mode = ko.mode;
+        r.key_tonic = ko.tonic;
+        r.key_conf = ko.conf;
+        r.key_clarity = ko.clarity;
+    }
+}
+
+namespace {
+
+char* dup_str(const std::string& s) {
+    char* p = (char*)std::malloc(s.size() + 1);
+    std::memcpy(p, s.c_str(), s.size() + 1);
+    return p;
+}
+float* dup_f(const std::vector<float>& v) {
+    if (v.empty()) return nullptr;
+    float* p = (float*)std::malloc(v.size() * sizeof(float));
+    std::memcpy(p, v.data(), v.size() * sizeof(float));
+    return p;
+}
+
+// result assembly + warnings (src/lib.rs:1561-1619)
+void fill_result(const TrackRes& r, uint32_t sr, float ms, sdsp_result* o) {
+    std::memset(o, 0, sizeof(*o));
+    o->status = r.status;
+    o->tempogram_multi_res_triggered = o->tempogram_multi_res_used = -1;
+    o->tempogram_percussive_triggered = o->tempogram_percussive_used = -1;
+    if (r.status != SDSP_OK) {
+        std::snprintf(o->error_message, sizeof o->error_message, "%s", r.err.c_str());
+        return;
+    }
+    o->bpm = r.bpm;
+    o->bpm_confidence = r.bpm_conf;
+    o->key_mode = r.key_mode;
+    o->key_tonic = (uint32_t)r.key_tonic;
+    o->key_confidence = r.key_conf;
+    o->key_clarity = r.key_clarity;
+    o->beats = dup_f(r.beats);
+    o->n_beats = r.beats.size();
+    o->downbeats = dup_f(r.downs);
+    o->n_downbeats = r.downs.size();
+    o->bars = dup_f(r.downs);
+    o->n_bars = r.downs.size();
+    o->grid_stability = r.stability;
+    o->duration_seconds = r.duration;
+    o->sample_rate = sr;
+    o->processing_time_ms = ms;
+    std::snprintf(o->algorithm_version, sizeof o->algorithm_version, "0.1.0-alpha");
+    o->onset_method_consensus = r.onset_consensus;
+    o->methods_used = 7;
+    std::vector<std::string> w;
+    if (r.bpm == 0.0f) w.push_back("BPM detection failed: insufficient onsets or estimation error");
+    if (r.stability < 0.5f) w.push_back("Low beat grid stability: " + fmt2(r.stability) + " (may indicate tempo variation)");
+    if (r.key_conf < 0.3f)
+        w.push_back("Low key detection confidence: " + fmt2(r.key_conf) + " (may indicate ambiguous or atonal music)");
+    if (r.key_clarity < 0.2f) {
+        w.push_back("Low key clarity: " + fmt2(r.key_clarity) + " (track may be atonal or have weak tonality)");
+        o->flags |= SDSP_FLAG_WEAK_TONALITY;
+    }
+    o->n_warnings = w.size();
+    if (!w.empty()) {
+        o->warnings = (char**)std::malloc(w.size() * sizeof(char*));
+        for (size_t i = 0; i < w.size(); i++) o->warnings[i] = dup_str(w[i]);
+    }
+    o->has_tempogram_candidates = r.has_cands;
+    if (r.has_cands && !r.cands.empty()) {
+        o->n_tempogram_candidates = r.cands.size();
+        o->tempogram_candidates = (sdsp_tempo_candidate*)std::malloc(r.cands.size() * sizeof(sdsp_tempo_candidate));
+        std::memcpy(o->tempogram_candidates, r.cands.data(), r.cands.size() * sizeof(sdsp_tempo_candidate));
+    }
+    o->tempogram_multi_res_triggered = r.mr_trig;
+    o->tempogram_multi_res_used = r.mr_used;
+    o->tempogram_percussive_triggered = r.perc_trig;
+    o->tempogram_percussive_used = r.perc_used;
+}
+
+int32_t run_device(int device, const float* d_samples, const uint64_t* offsets, const uint64_t* lens, uint64_t n,
+                   uint32_t sr, const sdsp_config* cfg, void* user_stream, sdsp_result* outs) {
+    DeviceCtx& d = device_ctx(device);
+    std::lock_guard<std::mutex> lk(d.mu);
+    SDSP_HIP_CHECK(hipSetDevice(device));
+    if (user_stream) {
+        hipEvent_t ev;
+        SDSP_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        SDSP_HIP_CHECK(hipEventRecord(ev, (hipStream_t)user_stream));
+        SDSP_HIP_CHECK(hipStreamWaitEvent(d.stream, ev, 0));
+        SDSP_HIP_CHECK(hipEventDestroy(ev));
+    }
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<uint64_t> off(offsets, offsets + n), ln(lens, lens + n);
+    std::vector<TrackRes> res;
+    Pipeline p(d, *cfg, sr);
+    p.run(d_samples, off, ln, res);
+    const float ms = (float)(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() /
+                             (double)std::max<uint64_t>(n, 1));
+    for (uint64_t i = 0; i < n; i++) fill_result(res[(size_t)i], sr, ms, &outs[i]);
+    return SDSP_OK;
+}
+
+}  // namespace
+}  // namespace sdsp
+
+using namespace sdsp;
+
 extern "C" {
-int32_t sdsp_analyze_audio(const float*, uint64_t, uint32_t, const sdsp_config*, sdsp_result* out, char* err,
-                           uint64_t errlen) {
-    if (out) std::memset(out, 0, sizeof(*out));
-    if (err && errlen) std::snprintf(err, errlen, "Not implemented: pipeline");
-    return SDSP_ERR_NOT_IMPLEMENTED;
+
+int32_t sdsp_analyze_batch_device(const float* d_samples, const uint64_t* offsets, const uint64_t* lens,
+                                  uint64_t n_tracks, uint32_t sample_rate, const sdsp_config* cfg, int32_t device,
+                                  void* stream, sdsp_result* outs) {
+    try {
+        return run_device(device, d_samples, offsets, lens, n_tracks, sample_rate, cfg, stream, outs);
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "sdsp_analyze_batch_device: %s\n", e.what());
+        for (uint64_t i = 0; i < n_tracks; i++) {
+            std::memset(&outs[i], 0, sizeof(outs[i]));
+            outs[i].status = SDSP_ERR_PROCESSING;
+            std::snprintf(outs[i].error_message, sizeof outs[i].error_message, "Processing error: %s", e.what());
+        }
+        return SDSP_ERR_PROCESSING;
+    }
 }
-int32_t sdsp_analyze_batch(const float* const*, const uint64_t*, uint64_t, uint32_t, const sdsp_config*, uint32_t,
-                           sdsp_result*) {
-    return SDSP_ERR_NOT_IMPLEMENTED;
+
+// Host buffers: tracks are copied to HBM (one contiguous shard per device) and analysed there.
+int32_t sdsp_analyze_batch(const float* const* tracks, const uint64_t* lens, uint64_t n_tracks, uint32_t sample_rate,
+                           const sdsp_config* cfg, uint32_t device_mask, sdsp_result* outs) {
+    std::vector<int> devs;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        for (uint64_t i = 0; i < n_tracks; i++) {
+            std::memset(&outs[i], 0, sizeof(outs[i]));
+            outs[i].status = SDSP_ERR_PROCESSING;
+            std::snprintf(outs[i].error_message, sizeof outs[i].error_message, "Processing error: no HIP device");
+        }
+        return SDSP_ERR_PROCESSING;
+    }
+    for (int d = 0; d < ndev && d < 32; d++)
+        if (device_mask == 0 ? d == 0 : ((device_mask >> d) & 1u)) devs.push_back(d);
+    if (devs.empty()) devs.push_back(0);
+    const size_t nd = devs.size();
+    std::vector<int32_t> rc(nd, SDSP_OK);
+    auto work = [&](size_t k) {
+        const uint64_t a = n_tracks * k / nd, b = n_tracks * (k + 1) / nd;
+        if (a >= b) return;
+        try {
+            SDSP_HIP_CHECK(hipSetDevice(devs[k]));
+            std::vector<uint64_t> off(b - a), ln(b - a);
+            uint64_t tot = 0;
+            for (uint64_t i = a; i < b; i++) {
+                off[i - a] = tot;
+                ln[i - a] = lens[i];
+                tot += lens[i];
+            }
+            float* d = nullptr;
+            SDSP_HIP_CHECK(hipMalloc(&d, std::max<uint64_t>(tot, 1) * sizeof(float)));
+            for (uint64_t i = a; i < b; i++)
+                if (lens[i]) SDSP_HIP_CHECK(hipMemcpy(d + off[i - a], tracks[i], lens[i] * sizeof(float), hipMemcpyHostToDevice));
+            rc[k] = run_device(devs[k], d, off.data(), ln.data(), b - a, sample_rate, cfg, nullptr, outs + a);
+            SDSP_HIP_CHECK(hipFree(d));
+        } catch (const std::exception& e) {
+            std::fprintf(stderr, "sdsp_analyze_batch: %s\n", e.what());
+            rc[k] = SDSP_ERR_PROCESSING;
+        }
+    };
+    if (nd == 1) {
+        work(0);
+    } else {
+        std::vector<std::thread> th;
+        for (size_t k = 0; k < nd; k++) th.emplace_back(work, k);
+        for (auto& t : th) t.join();
+    }
+    for (auto v : rc)
+        if (v != SDSP_OK) return v;
+    return SDSP_OK;
 }
-int32_t sdsp_analyze_batch_device(const float*, const uint64_t*, const uint64_t*, uint64_t, uint32_t,
-                                  const sdsp_config*, int32_t, void*, sdsp_result*) {
-    return SDSP_ERR_NOT_IMPLEMENTED;
+
+int32_t sdsp_analyze_audio(const float* samples, uint64_t n_samples, uint32_t sample_rate, const sdsp_config* cfg,
+                           sdsp_result* out, char* err, uint64_t errlen) {
+    std::memset(out, 0, sizeof(*out));
+    if (n_samples == 0 || sample_rate == 0) {
+        const char* m = n_samples == 0 ? "Invalid input: Empty audio samples" : "Invalid input: Invalid sample rate";
+        if (err && errlen) std::snprintf(err, (size_t)errlen, "%s", m);
+        out->status = SDSP_ERR_INVALID_INPUT;
+        return SDSP_ERR_INVALID_INPUT;
+    }
+    const float* const tr[1] = {samples};
+    const uint64_t ln[1] = {n_samples};
+    int32_t rc = sdsp_analyze_batch(tr, ln, 1, sample_rate, cfg, 1u, out);
+    if (rc != SDSP_OK && out->status == SDSP_OK) out->status = rc;
+    if (out->status != SDSP_OK) {
+        if (err && errlen) std::snprintf(err, (size_t)errlen, "%s", out->error_message);
+        const int32_t s = out->status;
+        sdsp_result_free(out);
+        std::memset(out, 0, sizeof(*out));
+        out->status = s;
+        return s;
+    }
+    return SDSP_OK;
 }
-int32_t sdsp_generate_synthetic(float*, uint64_t, uint64_t, uint32_t, uint64_t, int32_t, int32_t, void*, float*,
-                                int32_t*) {
-    return SDSP_ERR_NOT_IMPLEMENTED;
+
+int32_t sdsp_generate_synthetic(float* d_out, uint64_t n_tracks, uint64_t len, uint32_t sample_rate, uint64_t seed0,
+                                int32_t bpm_mode, int32_t device, void* stream, float* bpm_out, int32_t* key_out) {
+    try {
+        DeviceCtx& d = device_ctx(device);
+        std::lock_guard<std::mutex> lk(d.mu);
+        SDSP_HIP_CHECK(hipSetDevice(device));
+        std::vector<float> bpm((size_t)n_tracks);
+        std::vector<int> key((size_t)n_tracks);
+        for (uint64_t i = 0; i < n_tracks; i++) {
+            uint64_t x = 0x5EED0000ull + seed0 + i;
+            auto next = [&]() {  // splitmix64
+                x += 0x9E3779B97F4A7C15ull;
+                uint64_t z = x;
+                z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+                z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+                return z ^ (z >> 31);
+            };
+            float b;
+            if (bpm_mode == 1) {  // config 5: thirds in [55,80], [170,200], [80,170]
+                const int third = (int)(i % 3);
+                const uint64_t r = next();
+                if (third == 0)
+                    b = 55.0f + 0.5f * (float)(r % 51);
+                else if (third == 1)
+                    b = 170.0f + 0.5f * (float)(r % 61);
+                else
+                    b = 80.0f + 0.5f * (float)(r % 181);
+            } else {
+                b = 70.0f + 0.5f * (float)(next() % 221);
+            }
+            bpm[(size_t)i] = b;
+            key[(size_t)i] = (int)(next() % 24);
+        }
+        if (bpm_out) std::memcpy(bpm_out, bpm.data(), bpm.size() * sizeof(float));
+        if (key_out) std::memcpy(key_out, key.data(), key.size() * sizeof(int));
+        hipStream_t st = stream ? (hipStream_t)stream : d.stream;
+        DevBuf& db = d.buf("synth.bpm");
+        db.ensure(bpm.size() * 4 + 16);
+        DevBuf& dk = d.buf("synth.key");
+        dk.ensure(key.size() * 4 + 16);
+        DevBuf& dp = d.buf("synth.peak");
+        dp.ensure(key.size() * 4 + 16);
+        SDSP_HIP_CHECK(hipMemcpyAsync(db.p, bpm.data(), bpm.size() * 4, hipMemcpyHostToDevice, st));
+        SDSP_HIP_CHECK(hipMemcpyAsync(dk.p, key.data(), key.size() * 4, hipMemcpyHostToDevice, st));
+        launch_synth(d_out, n_tracks, len, sample_rate, db.as<float>(), dk.as<int>(), seed0, st);
+        launch_synth_normalize(d_out, n_tracks, len, dp.as<unsigned int>(), st);
+        SDSP_HIP_CHECK(hipGetLastError());
+        SDSP_HIP_CHECK(hipStreamSynchronize(st));
+        return SDSP_OK;
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "sdsp_generate_synthetic: %s\n", e.what());
+        return SDSP_ERR_PROCESSING;
+    }
 }
-}
+
+}  // extern "C"

@@ -1,0 +1,66 @@
+"""Result comparison used by the GPU parity tests (AnalysisResult field by field).
+
+Tolerances: BPM / confidences / clarity / stability / beat times within 1e-4 (BASELINE.json
+north_star), key exact, list lengths, flags, warnings and metadata flags equal.
+processing_time_ms is never compared (wall clock).
+"""
+import wave
+
+import numpy as np
+
+TOL = 1e-4
+
+
+def load_wav(path):
+    """16-bit PCM WAV -> f32 in [-1, 1) as the reference's hound loader does (s / 32768)."""
+    w = wave.open(path)
+    n = w.getnframes()
+    d = np.frombuffer(w.readframes(n), dtype=np.int16).astype(np.float32) / np.float32(32768.0)
+    if w.getnchannels() == 2:
+        d = ((d[0::2] + d[1::2]) / np.float32(2.0)).astype(np.float32)
+    return d, w.getframerate()
+
+
+def diff_results(got, ref, tol=TOL):
+    """List of human-readable mismatches between two AnalysisResult dicts (empty = parity)."""
+    bad = []
+
+    def close(name, a, b):
+        if not (abs(float(a) - float(b)) <= tol):
+            bad.append(f"{name}: got {a!r} ref {b!r}")
+
+    close("bpm", got["bpm"], ref["bpm"])
+    close("bpm_confidence", got["bpm_confidence"], ref["bpm_confidence"])
+    if got["key"] != ref["key"]:
+        bad.append(f"key: got {got['key']} ref {ref['key']}")
+    close("key_confidence", got["key_confidence"], ref["key_confidence"])
+    close("key_clarity", got["key_clarity"], ref["key_clarity"])
+    close("grid_stability", got["grid_stability"], ref["grid_stability"])
+    for k in ("beats", "downbeats", "bars"):
+        a, b = got["beat_grid"][k], ref["beat_grid"][k]
+        if len(a) != len(b):
+            bad.append(f"{k}: len got {len(a)} ref {len(b)}")
+        elif a and np.max(np.abs(np.asarray(a) - np.asarray(b))) > tol:
+            bad.append(f"{k}: max diff {np.max(np.abs(np.asarray(a) - np.asarray(b)))}")
+    gm, rm = got["metadata"], ref["metadata"]
+    close("duration_seconds", gm["duration_seconds"], rm["duration_seconds"])
+    for k in ("sample_rate", "algorithm_version", "onset_method_consensus", "flags", "confidence_warnings",
+              "tempogram_multi_res_triggered", "tempogram_multi_res_used", "tempogram_percussive_triggered",
+              "tempogram_percussive_used"):
+        if gm[k] != rm[k]:
+            bad.append(f"metadata.{k}: got {gm[k]!r} ref {rm[k]!r}")
+    return bad
+
+
+def exact_fraction(got, ref):
+    """1.0 when every float field is bit-identical (the design target), else the share that is."""
+    pairs = [(got["bpm"], ref["bpm"]), (got["bpm_confidence"], ref["bpm_confidence"]),
+             (got["key_confidence"], ref["key_confidence"]), (got["key_clarity"], ref["key_clarity"]),
+             (got["grid_stability"], ref["grid_stability"])]
+    same = sum(1 for a, b in pairs if np.float32(a).tobytes() == np.float32(b).tobytes())
+    a, b = got["beat_grid"]["beats"], ref["beat_grid"]["beats"]
+    if len(a) == len(b):
+        same_b = bool(np.array_equal(np.asarray(a, np.float32), np.asarray(b, np.float32)))
+    else:
+        same_b = False
+    return (same + same_b) / (len(pairs) + 1)

@@ -1,0 +1,135 @@
+"""End-to-end parity of the HIP engine against the CPU restatement (oracle) on the same inputs.
+
+Inputs: the reference's own WAV fixtures (tests/golden/*.wav, copied from
+/root/reference/tests/fixtures), seeded synthetic tracks generated on the device (copied back to
+the host for the oracle), and edge cases (empty, silent, ultra-short, silence-padded, ragged
+batches).  Everything goes through the C ABI (libstratum_hip.so).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+import parity
+import sdsp
+import synth
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+FIXTURES = ["120bpm_4bar.wav", "128bpm_4bar.wav", "cmajor_scale.wav", "mixed_silence.wav"]
+
+
+def _check(x, sr=44100, label=""):
+    st, ref = oracle.analyze(x, sr)
+    if st != 0:
+        with pytest.raises(sdsp.AnalysisError) as ei:
+            sdsp.analyze_audio(x, sr)
+        assert ei.value.code == st, (label, ei.value, ref)
+        assert str(ei.value) == ref, (label, str(ei.value), ref)
+        return None
+    got = sdsp.analyze_audio(x, sr)
+    bad = parity.diff_results(got, ref)
+    assert not bad, f"{label}: {bad}"
+    return got, ref
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_reference_fixtures(name):
+    x, sr = parity.load_wav(os.path.join(GOLDEN, name))
+    got, ref = _check(x, sr, name)
+    assert parity.exact_fraction(got, ref) == 1.0, (got, ref)
+
+
+def test_reference_integration_ranges():
+    """tests/integration_tests.rs:46-256 assertions, on the GPU results."""
+    x, sr = parity.load_wav(os.path.join(GOLDEN, "120bpm_4bar.wav"))
+    r = sdsp.analyze_audio(x, sr)
+    assert 7.0 < r["metadata"]["duration_seconds"] < 9.0
+    assert abs(r["bpm"] - 120.0) < 2.0 and r["bpm_confidence"] > 0.0
+    b = r["beat_grid"]["beats"]
+    assert len(b) >= 4 and abs((b[1] - b[0]) - 0.5) < 0.1
+    x, sr = parity.load_wav(os.path.join(GOLDEN, "128bpm_4bar.wav"))
+    r = sdsp.analyze_audio(x, sr)
+    assert abs(r["bpm"] - 128.0) <= 2.0
+    x, sr = parity.load_wav(os.path.join(GOLDEN, "cmajor_scale.wav"))
+    r = sdsp.analyze_audio(x, sr)
+    assert r["key"] == {"Major": 0} or r["key_confidence"] < 0.3
+    x, sr = parity.load_wav(os.path.join(GOLDEN, "mixed_silence.wav"))
+    r = sdsp.analyze_audio(x, sr)
+    assert 4.0 <= r["metadata"]["duration_seconds"] <= 6.0
+
+
+def test_errors():
+    with pytest.raises(sdsp.AnalysisError) as e:
+        sdsp.analyze_audio(np.zeros(0, np.float32), 44100)
+    assert e.value.kind == "InvalidInput" and str(e.value) == "Invalid input: Empty audio samples"
+    with pytest.raises(sdsp.AnalysisError) as e:
+        sdsp.analyze_audio(np.zeros(44100 * 30, np.float32), 44100)
+    assert e.value.kind == "ProcessingError" and "silent" in str(e.value)
+    with pytest.raises(sdsp.AnalysisError) as e:
+        sdsp.analyze_audio(np.ones(100, np.float32), 0)
+    assert e.value.kind == "InvalidInput"
+
+
+@pytest.mark.parametrize("n", [1, 100, 2047, 2048, 2600, 5000, 8191, 8192, 9000, 44100])
+def test_short_tracks(n):
+    rng = np.random.default_rng(n)
+    x = (rng.standard_normal(n) * 0.2).astype(np.float32)
+    _check(x, 44100, f"short{n}")
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2, 3])
+def test_synthetic_30s(seed):
+    x, *_ = synth.make_track(seed, seconds=30.0)
+    _check(x, 44100, f"synth{seed}")
+
+
+def test_silence_padded():
+    x, *_ = synth.make_track(11, seconds=20.0, silence_pad=3.0)
+    _check(x, 44100, "padded")
+
+
+def test_ragged_batch_matches_single():
+    tracks = [synth.make_track(s, seconds=sec)[0] for s, sec in [(21, 12.0), (22, 31.0), (23, 5.0), (24, 47.5)]]
+    tracks.insert(2, np.zeros(0, np.float32))
+    res = sdsp.analyze_batch(tracks, 44100)
+    for i, (x, r) in enumerate(zip(tracks, res)):
+        st, ref = oracle.analyze(x, 44100)
+        if st != 0:
+            assert isinstance(r, sdsp.AnalysisError) and r.code == st
+            continue
+        assert not isinstance(r, sdsp.AnalysisError), r
+        assert not parity.diff_results(r, ref), (i, parity.diff_results(r, ref))
+
+
+def test_device_generated_3min_tracks():
+    """Device-resident batch (the bench path) on two 3-min synthetic tracks, checked on the host."""
+    import torch
+
+    n, L = 2, 44100 * 180
+    buf = torch.empty(n * L, dtype=torch.float32, device="cuda")
+    sdsp.generate_synthetic(buf.data_ptr(), n, L, seed0=100)
+    res = sdsp.analyze_batch_device(buf.data_ptr(), np.arange(n) * L, np.full(n, L))
+    host = buf.cpu().numpy()
+    for i in range(n):
+        st, ref = oracle.analyze(host[i * L:(i + 1) * L], 44100)
+        assert st == 0
+        assert not parity.diff_results(res[i], ref), (i, parity.diff_results(res[i], ref))
+
+
+def test_emit_candidates_config():
+    x, *_ = synth.make_track(5, seconds=25.0)
+    cfg = sdsp.default_config()
+    cfg.emit_tempogram_candidates = 1
+    got = sdsp.analyze_audio(x, 44100, cfg)
+    ocfg = oracle.default_config()
+    ocfg.emit_tempogram_candidates = 1
+    st, ref = oracle.analyze(x, 44100, ocfg)
+    assert st == 0
+    assert not parity.diff_results(got, ref)
+    gc, rc = got["metadata"]["tempogram_candidates"], ref["metadata"]["tempogram_candidates"]
+    assert len(gc) == len(rc)
+    for a, b in zip(gc, rc):
+        assert abs(a["bpm"] - b["bpm"]) <= 1e-4 and abs(a["score"] - b["score"]) <= 1e-4
+        assert a["selected"] == b["selected"]
