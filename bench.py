@@ -1,0 +1,204 @@
+#!/usr/bin/env python3
+"""Throughput benchmark: full default-config analyze_audio() on synthetic 3-min 44.1 kHz tracks.
+
+Metric (BASELINE.json): tracks/sec of full analyze_audio() at 1/2/4/8 MI355X.  One "step" is one
+pass of the whole pipeline over one batch of `--tracks` tracks per GPU (BASELINE config 2: 1024
+per GPU; config 3 = 8 GPUs x 1024).  Tracks are generated on the device before the timed region
+(inputs resident in HBM); every step re-runs everything, results are copied back to the host.
+
+Multi-GPU: one process per GPU (torch.distributed.run), tracks sharded with no data-path
+collective (`scaling: weak`); a gloo (CPU) process group provides the barrier and the max over
+ranks.  The engine's own HIP runtime is loaded before torch so no second GPU runtime is touched.
+
+Also reported: the dominant STFT kernel's HBM roofline (algorithmic bytes / HIP-event kernel time
+vs 8 TB/s) and the CPU restatement (oracle) timed on this box's host cores on a bounded sample.
+"""
+import argparse
+import concurrent.futures as cf
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "stratum-dsp_amd", "python"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import numpy as np  # noqa: E402
+
+import sdsp  # noqa: E402  (loads libstratum_hip.so first)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--tracks", type=int, default=1024, help="tracks per GPU per step")
+    ap.add_argument("--seconds", type=float, default=180.0)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, os.cpu_count())")
+    ap.add_argument("--cpu-tracks", type=int, default=0, help="0 = 2 per thread")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--bpm-mode", type=int, default=0, help="1 = config-5 escalation-heavy BPM mix")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = local
+    sdsp.lib()
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+
+        tdist.init_process_group("gloo", rank=rank, world_size=world)
+        dist = (torch, tdist)
+
+    def barrier():
+        if dist:
+            dist[1].barrier()
+
+    sr = 44100
+    n = args.tracks
+    L = int(args.seconds * sr)
+    buf = sdsp.DeviceBuffer(n * L, device=dev)
+    sdsp.generate_synthetic(buf.ptr, n, L, sr, seed0=rank * n, bpm_mode=args.bpm_mode, device=dev)
+    offs = np.arange(n, dtype=np.uint64) * np.uint64(L)
+    lens = np.full(n, L, dtype=np.uint64)
+
+    for _ in range(args.warmup):
+        sdsp.analyze_batch_device(buf.ptr, offs, lens, sr, device=dev)
+    barrier()
+    sdsp.synchronize(dev)
+    t0 = time.perf_counter()
+    stft = {"ms8": 0.0, "b8": 0.0, "l8": 0, "ms2": 0.0, "b2": 0.0, "l2": 0}
+    res = None
+    for _ in range(args.steps):
+        res = sdsp.analyze_batch_device(buf.ptr, offs, lens, sr, device=dev)
+        st = sdsp.stage_times(dev)
+        stft["ms8"] += st["stft8192_ms"]
+        stft["b8"] += st["stft8192_bytes"]
+        stft["l8"] += st["stft8192_launches"]
+        stft["ms2"] += st["stft2048_ms"]
+        stft["b2"] += st["stft2048_bytes"]
+        stft["l2"] += st["stft2048_launches"]
+    sdsp.synchronize(dev)
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        torch, tdist = dist
+        t = torch.tensor([dt], dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        dt = float(t.item())
+    n_err = sum(1 for r in res if isinstance(r, sdsp.AnalysisError))
+    total_tracks = n * world * args.steps
+    value = total_tracks / dt
+    stages = sdsp.stage_times(dev)
+
+    # roofline of the dominant STFT kernel (k_stft_mag<8192>): algorithmic bytes per launch
+    # (4*N_in + 4*F*(nfft/2+1)) / average launch time (HIP events on the engine stream)
+    l8 = max(stft["l8"], 1)
+    bytes_per_launch = stft["b8"] / l8
+    ms_per_launch = stft["ms8"] / l8
+    achieved = bytes_per_launch / (ms_per_launch * 1e-3) / 1e9 if ms_per_launch > 0 else 0.0
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_stft8192.json")
+    if os.path.exists(pmc_path):
+        # rocprofv3 PMC passes (profiles/README.md): measured HBM bytes / algorithmic bytes for
+        # this kernel; scales to the per-launch traffic of whatever batch this run used
+        with open(pmc_path) as f:
+            ratio = json.load(f).get("hbm_over_algorithmic")
+        if ratio is not None:
+            traffic = round(ratio * bytes_per_launch)
+    roofline = {
+        "bound": "hbm",
+        "kernel": "k_stft_mag<8192> (key STFT, 8192/512)",
+        "achieved": round(achieved, 2),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": traffic,
+        "bytes_per_launch": bytes_per_launch,
+        "ms_per_launch": ms_per_launch,
+        "stft2048_GBps": round(stft["b2"] / (stft["ms2"] * 1e-3) / 1e9, 2) if stft["ms2"] > 0 else None,
+        "stft_stage_GBps": round((stft["b2"] + stft["b8"]) / ((stft["ms2"] + stft["ms8"]) * 1e-3) / 1e9, 2)
+        if (stft["ms2"] + stft["ms8"]) > 0 else None,
+    }
+
+    cpu = None
+    parity = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu, parity = cpu_baseline(buf, res, n, L, sr, args)
+
+    if rank == 0:
+        out = {
+            "metric": "tracks/sec full analyze_audio(), 3-min 44.1 kHz mono, at 1/2/4/8 MI355X",
+            "value": round(value, 3),
+            "unit": "tracks/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1000.0, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded on-device generator: kick/hat/triad/diatonic line, 3-min 44.1 kHz mono)",
+            "config": {
+                "workload": f"batch of {n} synthetic {args.seconds:g}-s 44.1 kHz mono tracks per GPU, "
+                            "AnalysisConfig::default(), full BPM + key + beat grid",
+                "tracks_per_gpu": n,
+                "seconds_per_track": args.seconds,
+                "sample_rate": sr,
+                "bpm_mode": args.bpm_mode,
+                "parallelism": f"track-sharded x{world} (no collectives)",
+            },
+            "errors": n_err,
+            "stage_ms_last_step": {k: round(v, 3) for k, v in stages.items() if k.endswith("_ms")},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "parity_sample": parity,
+        }
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist[1].destroy_process_group()
+
+
+def cpu_baseline(buf, res, n, L, sr, args):
+    """The oracle (C++ restatement, single-threaded per track, one track per thread as
+    examples/analyze_batch.rs:239-268 does with rayon) on a bounded sample of the same tracks."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    import parity
+
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    k = min(n, args.cpu_tracks or 2 * threads)
+    xs = [buf.to_host(i * L, L) for i in range(k)]
+    oracle.lib()
+
+    def one(x):
+        return oracle.analyze(x, sr)
+
+    t0 = time.perf_counter()
+    with cf.ThreadPoolExecutor(threads) as ex:
+        outs = list(ex.map(one, xs))
+    dt = time.perf_counter() - t0
+    match = sum(1 for i, (st, ref) in enumerate(outs) if st == 0 and not parity.diff_results(res[i], ref))
+    exact = sum(1 for i, (st, ref) in enumerate(outs) if st == 0 and parity.exact_fraction(res[i], ref) == 1.0)
+    cpu = {
+        "value": round(k / dt, 4),
+        "unit": "tracks/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{k} of the benchmark's own {args.seconds:g}-s tracks, one track per thread, "
+                  f"{dt:.1f} s wall ({dt * threads:.0f} thread-s); C++ restatement -O3, FFT per sdsp_fft_spec.h",
+    }
+    par = {"checked": k, "within_tolerance": match, "bit_exact": exact}
+    return cpu, par
+
+
+if __name__ == "__main__":
+    main()

@@ -286,6 +286,17 @@ int32_t sdsp_generate_synthetic(float* d_out, uint64_t n_tracks, uint64_t len, u
                                 uint64_t seed0, int32_t bpm_mode, int32_t device, void* stream,
                                 float* bpm_out, int32_t* key_out);
 
+/*
+ * Device-memory plumbing for harnesses that hold tracks in HBM (benchmarks, tests).  The engine
+ * links the system ROCm HIP runtime; callers that use these need no second GPU runtime.
+ */
+int32_t sdsp_device_count(void);
+int32_t sdsp_device_malloc(int32_t device, uint64_t bytes, void** ptr);
+int32_t sdsp_device_free(int32_t device, void* ptr);
+int32_t sdsp_memcpy_h2d(int32_t device, void* dst, const void* src, uint64_t bytes);
+int32_t sdsp_memcpy_d2h(int32_t device, void* dst, const void* src, uint64_t bytes);
+int32_t sdsp_device_synchronize(int32_t device);
+
 /* Library identification: "stratum-hip <abi> gfx950" */
 const char* sdsp_version(void);
 

@@ -314,6 +314,10 @@ std::string unsupported(const sdsp_config& c) {
     if (c.enable_key_multi_scale && c.key_multi_scale_lengths_len > 0) return "multi-scale key";
     if (c.enable_key_mode_heuristic || c.enable_key_minor_harmonic_bonus) return "key mode heuristic";
     if (c.enable_ml_refinement) return "ML refinement";
+    const bool use_aux = c.enable_tempogram_band_fusion || c.enable_tempogram_mel_novelty ||
+                         c.tempogram_band_consensus_bonus > 0.0f;
+    if (c.enable_tempogram_multi_resolution && (c.hop_size != 512 || !use_aux))
+        return "multi-resolution escalation with hop_size != 512 or without band/mel variants";
     return "";
 }
 

@@ -164,6 +164,32 @@ void sdsp_config_default(sdsp_config* c) {
 
 const char* sdsp_version(void) { return "stratum-hip 1 gfx950"; }
 
+int32_t sdsp_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+int32_t sdsp_device_malloc(int32_t device, uint64_t bytes, void** ptr) {
+    if (hipSetDevice(device) != hipSuccess) return SDSP_ERR_PROCESSING;
+    return hipMalloc(ptr, bytes ? bytes : 1) == hipSuccess ? SDSP_OK : SDSP_ERR_PROCESSING;
+}
+int32_t sdsp_device_free(int32_t device, void* ptr) {
+    if (hipSetDevice(device) != hipSuccess) return SDSP_ERR_PROCESSING;
+    return hipFree(ptr) == hipSuccess ? SDSP_OK : SDSP_ERR_PROCESSING;
+}
+int32_t sdsp_memcpy_h2d(int32_t device, void* dst, const void* src, uint64_t bytes) {
+    if (hipSetDevice(device) != hipSuccess) return SDSP_ERR_PROCESSING;
+    return hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess ? SDSP_OK : SDSP_ERR_PROCESSING;
+}
+int32_t sdsp_memcpy_d2h(int32_t device, void* dst, const void* src, uint64_t bytes) {
+    if (hipSetDevice(device) != hipSuccess) return SDSP_ERR_PROCESSING;
+    return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) == hipSuccess ? SDSP_OK : SDSP_ERR_PROCESSING;
+}
+int32_t sdsp_device_synchronize(int32_t device) {
+    if (hipSetDevice(device) != hipSuccess) return SDSP_ERR_PROCESSING;
+    return hipDeviceSynchronize() == hipSuccess ? SDSP_OK : SDSP_ERR_PROCESSING;
+}
+
 void sdsp_result_free(sdsp_result* r) {
     if (!r) return;
     std::free(r->beats);

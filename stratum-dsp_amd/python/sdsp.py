@@ -60,6 +60,15 @@ def lib():
         L.sdsp_last_stage_times.restype = C.c_int32
         L.sdsp_debug_stft.argtypes = [fp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_float, fp, fp, C.c_int32]
         L.sdsp_debug_stft.restype = C.c_int32
+        L.sdsp_device_count.restype = C.c_int32
+        L.sdsp_device_malloc.argtypes = [C.c_int32, C.c_uint64, C.POINTER(C.c_void_p)]
+        L.sdsp_device_free.argtypes = [C.c_int32, C.c_void_p]
+        L.sdsp_memcpy_h2d.argtypes = [C.c_int32, C.c_void_p, C.c_void_p, C.c_uint64]
+        L.sdsp_memcpy_d2h.argtypes = [C.c_int32, C.c_void_p, C.c_void_p, C.c_uint64]
+        L.sdsp_device_synchronize.argtypes = [C.c_int32]
+        for f in ("sdsp_device_malloc", "sdsp_device_free", "sdsp_memcpy_h2d", "sdsp_memcpy_d2h",
+                  "sdsp_device_synchronize"):
+            getattr(L, f).restype = C.c_int32
         _lib = L
     return _lib
 
@@ -153,6 +162,50 @@ def stage_times(device=0):
     t = SdspStageTimes()
     lib().sdsp_last_stage_times(device, C.byref(t))
     return {k: getattr(t, k) for k, _ in SdspStageTimes._fields_}
+
+
+class DeviceBuffer:
+    """A float32 buffer in HBM owned through the engine's own HIP runtime."""
+
+    def __init__(self, n_floats, device=0):
+        self.device = device
+        self.n = int(n_floats)
+        p = C.c_void_p()
+        if lib().sdsp_device_malloc(device, self.n * 4, C.byref(p)) != 0:
+            raise MemoryError(f"sdsp_device_malloc({self.n * 4} bytes) failed")
+        self.ptr = p.value
+
+    def to_host(self, start=0, count=None):
+        count = self.n - start if count is None else count
+        out = np.empty(count, np.float32)
+        if lib().sdsp_memcpy_d2h(self.device, out.ctypes.data, self.ptr + 4 * start, 4 * count) != 0:
+            raise RuntimeError("sdsp_memcpy_d2h failed")
+        return out
+
+    def from_host(self, arr, start=0):
+        a = np.ascontiguousarray(arr, dtype=np.float32)
+        if lib().sdsp_memcpy_h2d(self.device, self.ptr + 4 * start, a.ctypes.data, 4 * a.size) != 0:
+            raise RuntimeError("sdsp_memcpy_h2d failed")
+
+    def free(self):
+        if self.ptr:
+            lib().sdsp_device_free(self.device, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def device_count():
+    return int(lib().sdsp_device_count())
+
+
+def synchronize(device=0):
+    if lib().sdsp_device_synchronize(device) != 0:
+        raise RuntimeError("sdsp_device_synchronize failed")
 
 
 def debug_stft(x, nfft, hop, gain=1.0, device=0):

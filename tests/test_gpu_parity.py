@@ -105,13 +105,11 @@ def test_ragged_batch_matches_single():
 
 def test_device_generated_3min_tracks():
     """Device-resident batch (the bench path) on two 3-min synthetic tracks, checked on the host."""
-    import torch
-
     n, L = 2, 44100 * 180
-    buf = torch.empty(n * L, dtype=torch.float32, device="cuda")
-    sdsp.generate_synthetic(buf.data_ptr(), n, L, seed0=100)
-    res = sdsp.analyze_batch_device(buf.data_ptr(), np.arange(n) * L, np.full(n, L))
-    host = buf.cpu().numpy()
+    buf = sdsp.DeviceBuffer(n * L)
+    sdsp.generate_synthetic(buf.ptr, n, L, seed0=100)
+    res = sdsp.analyze_batch_device(buf.ptr, np.arange(n) * L, np.full(n, L))
+    host = buf.to_host()
     for i in range(n):
         st, ref = oracle.analyze(host[i * L:(i + 1) * L], 44100)
         assert st == 0
