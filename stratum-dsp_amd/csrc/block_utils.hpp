@@ -20,6 +20,26 @@ __device__ inline float block_max(float v, float* red) {
     return r;
 }
 
+// Sequential f32 sum p[0] + p[1] + ... + p[n-1] (the reference's fold order), returned to every
+// thread.  The block stages SEQ_CH values at a time into LDS with coalesced loads; thread 0
+// folds them in order.  buf: SEQ_CH floats of LDS.
+constexpr int SEQ_CH = 2048;
+__device__ inline float block_seq_sum(const float* p, int64_t n, float* buf) {
+    __shared__ float res;
+    float sum = 0.0f;
+    for (int64_t c0 = 0; c0 < n; c0 += SEQ_CH) {
+        const int64_t m = n - c0 < SEQ_CH ? n - c0 : SEQ_CH;
+        __syncthreads();
+        for (int i = threadIdx.x; i < m; i += blockDim.x) buf[i] = p[c0 + i];
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (int i = 0; i < m; i++) sum += buf[i];
+    }
+    if (threadIdx.x == 0) res = sum;
+    __syncthreads();
+    return res;
+}
+
 // Block-wide integer sum.
 __device__ inline int block_sum_i(int v, int* red) {
     v = wave_sum_i(v);

@@ -5,33 +5,42 @@
 //   H[v][t]   = sum_k (k*|X_t[k]|)*|X_t[k]|           hfc_novelty(_band) / detect_hfc_onsets  :738-747,810-821, hfc.rs:130-137
 //   SFX[v][t] = sqrt(sum_k max(0, L_t[k] - max_{|j-k|<=K, j in band} L_{t-1}[j])^2)   superflux(_band) :353-376,419-442
 //   SFO[t]    = sqrt(sum_k max(0, X_t[k]/max_t - X_{t-1}[k]/max_{t-1})^2)            spectral_flux.rs:116-157
-//   MEL[t][m] = sum_k L_t[k] * w_{k,m}  (HTK triangles, bins ascending)               MelFilterbank::apply_logmag :174-190
+//   MEL[m][t] = sum_k L_t[k] * w_{k,m}  (HTK triangles, bins ascending)               MelFilterbank::apply_logmag :174-190
 //   with L = ln(1 + max(X, 0)), v in {full, low, mid, high}.
 //
-// Each workgroup owns 128 consecutive frames of one track, one thread per frame.  Bins are
-// streamed in 32-bin chunks: the workgroup stages rows t-1..t+127 of the chunk into LDS with
-// coalesced 128-B row segments (log values computed once per element, with a +-K halo for
-// the SuperFlux max filter), then each thread walks its frame's bins *in order*, so every f32
-// accumulation happens in exactly the reference's sequence and the results are bit-identical
-// to the CPU restatement.  Band membership is uniform across the workgroup (all threads
-// visit the same bin at the same time), so the band logic never diverges.
+// Each workgroup owns FT_FRAMES consecutive frames of one track, one thread per frame, so
+// every per-frame fold runs in exactly the reference's bin order (bit-identical to the CPU
+// restatement).  Bins are streamed through two circular LDS windows of W columns (slot =
+// bin mod W): raw magnitudes and their logs.  Each step loads the CW bins K ahead of the
+// ones it processes (coalesced row segments, log computed once per element), so the
+// SuperFlux max filter over [b-K, b+K] of the previous frame always finds its halo resident
+// and no column is loaded or logged twice.  Row stride W+1 (odd) keeps the per-thread row
+// walks bank-conflict-free.
+//
+// Mel bands: every bin feeds at most two adjacent triangles (or one narrow triangle twice,
+// rising then falling edge) and the triangles start in bin order, so a thread keeps only two
+// running sums (mels mA, mA+1) in registers; the host precomputes, per bin, how many
+// finished mels to flush before the bin (uniform across the workgroup) and the ordered
+// (accumulator, weight) contributions.  Flushed mels are stored mel-major (MEL[m*total + t]),
+// coalesced across the workgroup.
 #include "kernels.hpp"
 
 namespace sdsp {
 
-constexpr int FT_CW = 32;
-
+template <int CW, int W>
 __global__ __launch_bounds__(FT_FRAMES) void k_features(const float* __restrict__ mags,
                                                         const float* __restrict__ fmax,
                                                         const uint64_t* __restrict__ frame_pfx,
                                                         const uint64_t* __restrict__ tile_pfx, int T, FeatParams P,
-                                                        const int* __restrict__ mel_m, const float* __restrict__ mel_w,
-                                                        float* __restrict__ E, float* __restrict__ H,
-                                                        float* __restrict__ SFX, float* __restrict__ SFO,
-                                                        float* __restrict__ MEL, uint64_t total) {
-    __shared__ float Mt[FT_FRAMES + 1][FT_CW + 1];
-    __shared__ float Lt[FT_FRAMES + 1][FT_CW + 2 * FT_KMAX + 1];
-    __shared__ float melacc[FT_MELMAX][FT_FRAMES];
+                                                        const MelPlan* __restrict__ mel, float* __restrict__ E,
+                                                        float* __restrict__ H, float* __restrict__ SFX,
+                                                        float* __restrict__ SFO, float* __restrict__ MEL,
+                                                        uint64_t total) {
+    static_assert((W & (W - 1)) == 0, "W must be a power of two");
+    constexpr int ROWS = FT_FRAMES + 1;
+    constexpr int LS = W + 1;
+    __shared__ float Mt[ROWS][LS];
+    __shared__ float Lt[ROWS][LS];
 
     const uint64_t gb = blockIdx.x;
     const int trk = find_track(tile_pfx, T, gb);
@@ -43,32 +52,46 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const float* __restrict_
     const bool valid = f < F;
     const bool has_prev = valid && f >= 1;
     const int K = P.K, B = P.B;
+    const uint64_t g = g0 + (uint64_t)f;
 
-    for (int m = 0; m < P.n_mels; m++) melacc[m][i] = 0.0f;
     float e[4] = {0, 0, 0, 0}, h[4] = {0, 0, 0, 0}, sx[4] = {0, 0, 0, 0}, so = 0.0f;
-    const float mx_c = valid ? fmax[g0 + f] : 0.0f;
-    const float mx_p = has_prev ? fmax[g0 + f - 1] : 0.0f;
+    float accA = 0.0f, accB = 0.0f;
+    int mA = 0;
+    const float mx_c = valid ? fmax[g] : 0.0f;
+    const float mx_p = has_prev ? fmax[g - 1] : 0.0f;
     const bool cn = mx_c > EPS, pn = mx_p > EPS;
 
-    for (int c0 = 0; c0 < B; c0 += FT_CW) {
-        __syncthreads();
-        // stage rows f0-1 .. f0+127 of [c0-K, c0+CW+K)
-        const int LW = FT_CW + 2 * K;
-        for (int idx = i; idx < (FT_FRAMES + 1) * LW; idx += FT_FRAMES) {
-            const int r = idx / LW, j = idx - r * LW;
-            const int64_t fr = f0 - 1 + r;
-            const int b = c0 - K + j;
+    // rows f0-1 .. f0+FT_FRAMES-1 of the track; row r <-> frame f0-1+r
+    const int64_t r_lo = f0 >= 1 ? 0 : 1;
+    const int64_t r_hi = F - f0 + 1 < ROWS ? F - f0 + 1 : ROWS;  // rows [r_lo, r_hi) exist
+    const float* base = mags + (g0 + (uint64_t)f0) * (uint64_t)P.stride;  // row r at base + (r-1)*stride
+    const int sub = i / CW, jj = i % CW;
+
+    // stage bins [b0, b0+CW) (columns beyond B or rows outside the track read as 0)
+    auto stage = [&](int b0) {
+        const int b = b0 + jj;
+        const bool col_ok = b < B;
+        const int slot = b & (W - 1);
+#pragma unroll 4
+        for (int r = sub; r < ROWS; r += FT_FRAMES / CW) {
             float v = 0.0f;
-            if (fr >= 0 && fr < F && b >= 0 && b < B) v = mags[(g0 + (uint64_t)fr) * (uint64_t)P.stride + b];
-            Lt[r][j] = sd_logf(1.0f + sd_maxf(v, 0.0f));
-            if (j >= K && j < K + FT_CW) Mt[r][j - K] = v;
+            if (col_ok && r >= r_lo && r < r_hi) v = base[(int64_t)(r - 1) * P.stride + b];
+            Mt[r][slot] = v;
+            Lt[r][slot] = sd_logf(1.0f + sd_maxf(v, 0.0f));
         }
+    };
+    // prologue: bins [0, K) (K <= CW)
+    if (jj < K) stage(0);
+    for (int c0 = 0; c0 < B; c0 += CW) {
+        __syncthreads();  // previous step's readers are done with the slots overwritten here
+        stage(c0 + K);
         __syncthreads();
+        const int nb = B - c0 < CW ? B - c0 : CW;
         if (!valid) continue;
-        const int nb = B - c0 < FT_CW ? B - c0 : FT_CW;
         for (int j = 0; j < nb; j++) {
             const int b = c0 + j;
-            const float m = Mt[i + 1][j];
+            const int s = b & (W - 1);
+            const float m = Mt[i + 1][s];
             const float ee = m * m;
             const float hh = (float)b * m * m;
             e[0] += ee;
@@ -79,15 +102,29 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const float* __restrict_
                     e[v] += ee;
                     h[v] += hh;
                 }
-            const float lc = Lt[i + 1][j + K];
-            // mel accumulation, contributions in ascending mel index (novelty.rs:181-186)
-            if (lc > 0.0f) {
-                const int m1 = mel_m[2 * b], m2 = mel_m[2 * b + 1];
-                if (m1 >= 0) melacc[m1][i] += lc * mel_w[2 * b];
-                if (m2 >= 0) melacc[m2][i] += lc * mel_w[2 * b + 1];
+            const float lc = Lt[i + 1][s];
+            if (P.n_mels > 0) {
+                const MelPlan mp = mel[b];
+                for (int q = 0; q < mp.nflush; q++) {
+                    MEL[(uint64_t)mA * total + g] = accA;
+                    accA = accB;
+                    accB = 0.0f;
+                    mA++;
+                }
+                // novelty.rs:181-186 skips v <= 0; adding +0 to a non-negative sum is exact
+                if (lc > 0.0f) {
+                    if (mp.w0 != 0.0f) {
+                        if (mp.s0 == 0) accA += lc * mp.w0;
+                        else accB += lc * mp.w0;
+                    }
+                    if (mp.w1 != 0.0f) {
+                        if (mp.s1 == 0) accA += lc * mp.w1;
+                        else accB += lc * mp.w1;
+                    }
+                }
             }
             if (has_prev) {
-                const float mp = Mt[i][j];
+                const float mp = Mt[i][s];
                 const float pv = pn ? mp / mx_p : 0.0f;
                 const float cv = cn ? m / mx_c : 0.0f;
                 const float d = sd_maxf(cv - pv, 0.0f);
@@ -96,7 +133,7 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const float* __restrict_
                 const int lo = b - K < 0 ? 0 : b - K;
                 const int hi = b + K + 1 < B ? b + K + 1 : B;
                 float pm = 0.0f;
-                for (int q = lo; q < hi; q++) pm = sd_maxf(pm, Lt[i][q - c0 + K]);
+                for (int q = lo; q < hi; q++) pm = sd_maxf(pm, Lt[i][q & (W - 1)]);
                 const float df = sd_maxf(lc - pm, 0.0f);
                 sx[0] += df * df;
 #pragma unroll
@@ -107,7 +144,7 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const float* __restrict_
                             const int lb = lo < P.bs[v] ? P.bs[v] : lo;
                             const int hb = hi > P.be[v] ? P.be[v] : hi;
                             pmb = 0.0f;
-                            for (int q = lb; q < hb; q++) pmb = sd_maxf(pmb, Lt[i][q - c0 + K]);
+                            for (int q = lb; q < hb; q++) pmb = sd_maxf(pmb, Lt[i][q & (W - 1)]);
                         }
                         const float db = sd_maxf(lc - pmb, 0.0f);
                         sx[v] += db * db;
@@ -117,13 +154,16 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const float* __restrict_
         }
     }
     if (!valid) return;
-    const uint64_t g = g0 + (uint64_t)f;
+    for (; mA < P.n_mels; mA++) {
+        MEL[(uint64_t)mA * total + g] = accA;
+        accA = accB;
+        accB = 0.0f;
+    }
 #pragma unroll
     for (int v = 0; v < 4; v++) {
         E[(uint64_t)v * total + g] = e[v];
         H[(uint64_t)v * total + g] = h[v];
     }
-    for (int m = 0; m < P.n_mels; m++) MEL[g * (uint64_t)P.n_mels + m] = melacc[m][i];
     if (has_prev) {
         const uint64_t gp = g - 1;  // pair (t-1, t) stored at t-1
         SFO[gp] = __builtin_sqrtf(so);
@@ -133,11 +173,16 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const float* __restrict_
 }
 
 void launch_features(const float* mags, const float* fmax, const uint64_t* frame_pfx, const uint64_t* tile_pfx,
-                     int T, uint64_t n_tiles, const FeatParams& P, const int* mel_m, const float* mel_w, float* E,
-                     float* H, float* SFX, float* SFO, float* MEL, uint64_t total, hipStream_t st) {
+                     int T, uint64_t n_tiles, const FeatParams& P, const MelPlan* mel, float* E, float* H, float* SFX,
+                     float* SFO, float* MEL, uint64_t total, hipStream_t st) {
     if (n_tiles == 0) return;
-    hipLaunchKernelGGL(k_features, dim3((unsigned)n_tiles), dim3(FT_FRAMES), 0, st, mags, fmax, frame_pfx, tile_pfx,
-                       T, P, mel_m, mel_w, E, H, SFX, SFO, MEL, total);
+    // window must hold [c0-K, c0+CW+K): CW + 2K <= W
+    if (P.K <= 4)
+        hipLaunchKernelGGL((k_features<8, 16>), dim3((unsigned)n_tiles), dim3(FT_FRAMES), 0, st, mags, fmax,
+                           frame_pfx, tile_pfx, T, P, mel, E, H, SFX, SFO, MEL, total);
+    else
+        hipLaunchKernelGGL((k_features<16, 32>), dim3((unsigned)n_tiles), dim3(FT_FRAMES), 0, st, mags, fmax,
+                           frame_pfx, tile_pfx, T, P, mel, E, H, SFX, SFO, MEL, total);
 }
 
 }  // namespace sdsp

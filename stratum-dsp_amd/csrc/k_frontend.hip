@@ -15,18 +15,29 @@
 namespace sdsp {
 
 // ---- peak |x| per track (order-free max via atomicMax on the IEEE bits of |x| >= 0) ----
+// PK_CH samples per workgroup, PK_U independent loads in flight per thread.
+constexpr int PK_U = 8;
 __global__ __launch_bounds__(256) void k_peak_abs(const float* __restrict__ x, const uint64_t* __restrict__ in_off,
                                                   const uint64_t* __restrict__ n_raw,
                                                   const uint64_t* __restrict__ chunk_pfx, int T,
                                                   unsigned int* __restrict__ peak_bits) {
-    constexpr int CH = 4096;
     const uint64_t g = blockIdx.x;
     const int trk = find_track(chunk_pfx, T, g);
     const uint64_t c = g - chunk_pfx[trk];
-    const uint64_t s0 = c * CH, n = n_raw[trk];
+    const uint64_t s0 = c * PK_CH, n = n_raw[trk];
+    const uint64_t lim = s0 + PK_CH < n ? s0 + PK_CH : n;
     const float* p = x + in_off[trk];
     float m = 0.0f;
-    for (uint64_t i = s0 + threadIdx.x; i < s0 + CH && i < n; i += 256) m = sd_maxf(m, sd_absf(p[i]));
+    for (uint64_t i0 = s0 + threadIdx.x; i0 < lim; i0 += 256 * PK_U) {
+        float v[PK_U];
+#pragma unroll
+        for (int u = 0; u < PK_U; u++) {
+            const uint64_t i = i0 + (uint64_t)u * 256;
+            v[u] = i < lim ? sd_absf(p[i]) : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < PK_U; u++) m = sd_maxf(m, v[u]);
+    }
     m = wave_max(m);
     if ((threadIdx.x & 63) == 0 && m > 0.0f) atomicMax(&peak_bits[trk], sd_bits_f(m));
 }
@@ -42,27 +53,57 @@ __global__ void k_gain(const unsigned int* __restrict__ peak_bits, int T, float 
     gain[t] = g;
 }
 
-// RMS of frame f = sqrt(sum_{k<len} (x*g)^2 / len), sequential f32 sum (silence.rs:154-169).
-__global__ __launch_bounds__(256) void k_frame_rms(const float* __restrict__ x, const uint64_t* __restrict__ src_off,
-                                                   const float* __restrict__ gain,
-                                                   const uint64_t* __restrict__ n_len,
-                                                   const uint64_t* __restrict__ frame_pfx, int T,
-                                                   uint64_t total, int fs, int hop, float* __restrict__ rms) {
-    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= total) return;
-    const int trk = find_track(frame_pfx, T, g);
-    const uint64_t f = g - frame_pfx[trk];
-    const uint64_t n = n_len[trk];
-    const uint64_t s = f * (uint64_t)hop;
-    const uint64_t e = s + (uint64_t)fs < n ? s + (uint64_t)fs : n;
-    const float* p = x + src_off[trk];
-    const float gn = gain[trk];
-    float sum = 0.0f;
-    for (uint64_t k = s; k < e; k++) {
-        const float v = p[k] * gn;
-        sum += v * v;
+// ---- frame RMS: sqrt(sum_{k in frame} (x_k*gain)^2 / len), the sum folded in sample order ----
+// One thread per frame, RMS_ROWS frames per workgroup.  The frames' samples are staged through
+// LDS in RMS_KC-sample column chunks (row-contiguous, coalesced loads, RMS_KC loads in flight
+// per thread), then each thread folds its own row in order.  Overlapping frames re-read their
+// shared samples from L2 / Infinity Cache, not HBM.
+constexpr int RMS_ROWS = 256;
+constexpr int RMS_KC = 32;
+__global__ __launch_bounds__(RMS_ROWS) void k_frame_rms(const float* __restrict__ x,
+                                                        const uint64_t* __restrict__ src_off,
+                                                        const float* __restrict__ gain,
+                                                        const uint64_t* __restrict__ n_len,
+                                                        const uint64_t* __restrict__ frame_pfx, int T,
+                                                        uint64_t total, int fs, int hop, float* __restrict__ rms) {
+    __shared__ float tile[RMS_ROWS][RMS_KC + 1];
+    __shared__ uint64_t r_beg[RMS_ROWS];
+    __shared__ uint32_t r_len[RMS_ROWS];
+    __shared__ float r_gain[RMS_ROWS];
+    const int tid = threadIdx.x;
+    const uint64_t g = (uint64_t)blockIdx.x * RMS_ROWS + tid;
+    uint32_t len = 0;
+    if (g < total) {
+        const int trk = find_track(frame_pfx, T, g);
+        const uint64_t f = g - frame_pfx[trk];
+        const uint64_t n = n_len[trk];
+        const uint64_t s = f * (uint64_t)hop;
+        const uint64_t e = s + (uint64_t)fs < n ? s + (uint64_t)fs : n;
+        len = e > s ? (uint32_t)(e - s) : 0u;
+        r_beg[tid] = src_off[trk] + s;
+        r_gain[tid] = gain[trk];
+    } else {
+        r_beg[tid] = 0;
+        r_gain[tid] = 0.0f;
     }
-    rms[g] = e > s ? __builtin_sqrtf(sum / (float)(e - s)) : 0.0f;
+    r_len[tid] = len;
+    float sum = 0.0f;
+    const int sub = tid / RMS_KC, j = tid % RMS_KC;
+    for (int c0 = 0; c0 < fs; c0 += RMS_KC) {
+        __syncthreads();
+#pragma unroll 8
+        for (int r = sub; r < RMS_ROWS; r += RMS_ROWS / RMS_KC) {
+            const uint32_t k = (uint32_t)(c0 + j);
+            tile[r][j] = k < r_len[r] ? x[r_beg[r] + k] * r_gain[r] : 0.0f;
+        }
+        __syncthreads();
+        const int lim = (int)len - c0 < RMS_KC ? (int)len - c0 : RMS_KC;
+        for (int q = 0; q < lim; q++) {
+            const float v = tile[tid][q];
+            sum += v * v;
+        }
+    }
+    if (g < total) rms[g] = len > 0 ? __builtin_sqrtf(sum / (float)len) : 0.0f;
 }
 
 // Silence regions and trim bounds, one thread per track (silence.rs:171-263).

@@ -14,114 +14,225 @@
 
 namespace sdsp {
 
-constexpr int MASK_T = 256;
-constexpr int MASK_RING_MAX = 64;
+constexpr int MASK_T = 64;  // bins per workgroup (one wave): 4097 bins = 64 full waves + 1 lane
+constexpr int MASK_U = 16;  // frames loaded ahead per thread (independent HBM loads in flight)
 
+// LDS: prefix ring pre[2M+2][MASK_T] and raw ring raw[M+1][MASK_T] (dynamic, sized by M).
+// Ring slots advance by counters (no runtime modulo): the prefix for en = min(t+M+1, F) is
+// always the last one written; st = max(t-M, 0) advances once t > M; raw[t] was written M
+// frames earlier.
+// PW: 2 -> power 2 (x*x, the default), 1 -> power 1, 0 -> any other power (sd_powf); keeps the
+// unrolled body free of the general pow code.
+template <int PW>
+__device__ __forceinline__ float mask_pow(float x, float p) {
+    if (PW == 2) return x * x;
+    if (PW == 1) return x;
+    return sd_powf(x, p);
+}
+
+template <int PW>
 __global__ __launch_bounds__(MASK_T) void k_mask(float* __restrict__ mags, int stride, int B,
                                                   const uint64_t* __restrict__ frame_pfx, const int* __restrict__ tracks,
                                                   int blocks_per_track, int margin, float power) {
-    __shared__ float ring[MASK_RING_MAX][MASK_T];
+    extern __shared__ float mask_lds[];
     const int it = blockIdx.x / blocks_per_track;
     const int trk = tracks[it];
     const int b = (blockIdx.x % blocks_per_track) * MASK_T + threadIdx.x;
     const int64_t F = (int64_t)(frame_pfx[trk + 1] - frame_pfx[trk]);
     if (b >= B || F <= 0) return;
     float* col = mags + frame_pfx[trk] * (uint64_t)stride + b;
-    const int R = 2 * margin + 2;
+    const int M = margin;
+    const int R = 2 * M + 2, RX = M + 1;
+    float* pre = mask_lds + threadIdx.x;
+    float* raw = mask_lds + (size_t)R * MASK_T + threadIdx.x;
     const float p = sd_maxf(power, 1.0f);
     const float eps = 1e-12f;
-    float* rg = &ring[0][threadIdx.x];
-    rg[0] = 0.0f;
+    pre[0] = 0.0f;
     float prev = 0.0f;
-    for (int64_t tin = 0; tin < F + margin; tin++) {
-        if (tin < F) {
-            prev = prev + col[tin * stride];
-            rg[((tin + 1) % R) * MASK_T] = prev;
+    int w_slot = 0;   // slot of prefix[min(tin+1, F)] after this step's write (= en's slot)
+    int s_slot = 0;   // slot of prefix[st]
+    int xw = 0;       // raw write slot (tin % RX)
+    int xr = 0;       // raw read slot (t % RX)
+    for (int64_t base = 0; base < F + M; base += MASK_U) {
+        float xv[MASK_U];
+#pragma unroll
+        for (int u = 0; u < MASK_U; u++) {
+            const int64_t tin = base + u;
+            xv[u] = tin < F ? col[tin * stride] : 0.0f;
         }
-        const int64_t t = tin - margin;
-        if (t < 0) continue;
-        if (t >= F) break;
-        const int64_t st = t >= margin ? t - margin : 0;
-        const int64_t en = t + margin + 1 < F ? t + margin + 1 : F;
-        const float denom = (float)(en - st > 1 ? en - st : 1);
-        const float xr = col[t * stride];
-        // margin 0: smooth_spectrogram_time returns its input unchanged (extractor.rs:1250-1252)
-        const float hm = margin == 0 ? xr : (rg[(en % R) * MASK_T] - rg[(st % R) * MASK_T]) / denom;
-        const float x = sd_maxf(xr, 0.0f);
-        const float h = sd_maxf(hm, 0.0f);
-        const float r = sd_maxf(x - h, 0.0f);
-        const float hp = sd_powf(h, p);
-        const float rp = sd_powf(r, p);
-        const float m = hp / (hp + rp + eps);
-        col[t * stride] = x * m;
+#pragma unroll
+        for (int u = 0; u < MASK_U; u++) {
+            const int64_t tin = base + u;
+            if (tin >= F + M) break;
+            if (tin < F) {
+                prev = prev + xv[u];
+                w_slot = w_slot + 1 == R ? 0 : w_slot + 1;
+                pre[w_slot * MASK_T] = prev;
+                raw[xw * MASK_T] = xv[u];
+                xw = xw + 1 == RX ? 0 : xw + 1;
+            }
+            const int64_t t = tin - M;
+            if (t < 0) continue;
+            const int64_t st = t >= M ? t - M : 0;
+            const int64_t en = t + M + 1 < F ? t + M + 1 : F;
+            const float denom = (float)(en - st > 1 ? en - st : 1);
+            const float x_raw = M == 0 ? xv[u] : raw[xr * MASK_T];
+            // margin 0: smooth_spectrogram_time returns its input unchanged (extractor.rs:1250-1252)
+            const float hm = M == 0 ? x_raw : (pre[w_slot * MASK_T] - pre[s_slot * MASK_T]) / denom;
+            const float x = sd_maxf(x_raw, 0.0f);
+            const float h = sd_maxf(hm, 0.0f);
+            const float r = sd_maxf(x - h, 0.0f);
+            const float hp = mask_pow<PW>(h, p);
+            const float rp = mask_pow<PW>(r, p);
+            const float m = hp / (hp + rp + eps);
+            col[t * stride] = x * m;
+            if (M > 0) xr = xr + 1 == RX ? 0 : xr + 1;
+            if (t >= M) s_slot = s_slot + 1 == R ? 0 : s_slot + 1;
+        }
+    }
+}
+
+// Register-ring variant for a compile-time margin M (the default 12): the prefix ring
+// (R = 2M+2 slots) and the raw ring (M+1 slots) live in VGPRs and the frame loop is unrolled
+// by R, so every slot index is static.  Edges need no special case: frames past the end
+// contribute x = 0 (prefix + 0 == prefix, so P[min(t+M+1, F)] is read as P[t+M+1]), and
+// prefixes of negative index are the ring's initial zeros (== P[0]) because slot (t-M) mod R
+// is not written before t >= M.  R loads are issued ahead of each unrolled block.
+template <int M, int PW>
+__global__ __launch_bounds__(MASK_T) void k_mask_r(float* __restrict__ mags, int stride, int B,
+                                                    const uint64_t* __restrict__ frame_pfx,
+                                                    const int* __restrict__ tracks, int blocks_per_track,
+                                                    float power) {
+    constexpr int R = 2 * M + 2, RX = M + 1;
+    static_assert(M >= 1, "margin 0 uses k_mask");
+    const int it = blockIdx.x / blocks_per_track;
+    const int trk = tracks[it];
+    const int b = (blockIdx.x % blocks_per_track) * MASK_T + threadIdx.x;
+    const int64_t F = (int64_t)(frame_pfx[trk + 1] - frame_pfx[trk]);
+    if (b >= B || F <= 0) return;
+    float* col = mags + frame_pfx[trk] * (uint64_t)stride + b;
+    const float p = sd_maxf(power, 1.0f);
+    const float eps = 1e-12f;
+    float P[R], X[RX];
+#pragma unroll
+    for (int j = 0; j < R; j++) P[j] = 0.0f;
+#pragma unroll
+    for (int j = 0; j < RX; j++) X[j] = 0.0f;
+    float prev = 0.0f;
+    for (int64_t base = 0; base < F + M; base += R) {
+        float xv[R];
+#pragma unroll
+        for (int u = 0; u < R; u++) xv[u] = base + u < F ? col[(base + u) * stride] : 0.0f;
+#pragma unroll
+        for (int u = 0; u < R; u++) {
+            const int64_t tin = base + u;
+            prev = prev + xv[u];  // == prev once tin >= F (x = 0)
+            P[(u + 1) % R] = prev;
+            X[u % RX] = xv[u];
+            const int64_t t = tin - M;
+            if (t >= 0 && t < F) {
+                const int64_t st = t >= M ? t - M : 0;
+                const int64_t en = t + M + 1 < F ? t + M + 1 : F;
+                const float denom = (float)(en - st > 1 ? en - st : 1);
+                const float hm = (P[(u + 1) % R] - P[(u + R - 2 * M) % R]) / denom;
+                const float x = sd_maxf(X[(u + 1) % RX], 0.0f);
+                const float h = sd_maxf(hm, 0.0f);
+                const float r = sd_maxf(x - h, 0.0f);
+                const float hp = mask_pow<PW>(h, p);
+                const float rp = mask_pow<PW>(r, p);
+                const float m = hp / (hp + rp + eps);
+                col[t * stride] = x * m;
+            }
+        }
     }
 }
 
 // ----------------------------------------------------------------------------------------
-constexpr int HP_T = 64;     // frames per workgroup (one per thread)
-constexpr int HP_CW = 64;    // bins per staged chunk
+constexpr int HP_CW = 16;  // bins per staged chunk (LDS row stride 17: conflict-free)
 
-__global__ __launch_bounds__(HP_T) void k_hpcp(const float* __restrict__ mags, const uint64_t* __restrict__ frame_pfx,
-                                               const uint64_t* __restrict__ tile_pfx, const int* __restrict__ tracks,
-                                               int n_items, HpcpParams P, const HarmEntry* __restrict__ harm,
-                                               float* __restrict__ chroma, float* __restrict__ energy) {
-    __shared__ float tile[HP_T][HP_CW + 1];
-    __shared__ float pk_m[HP_KMAX][HP_T];
-    __shared__ int pk_b[HP_KMAX][HP_T];
-    __shared__ float pc[12][HP_T];
+// One thread per frame, HP_FRAMES frames per workgroup.  Bins are staged through LDS in
+// HP_CW-column chunks (coalesced row segments) and each thread walks its frame's bins in
+// order: energy fold, local-maximum test, and insertion into a register-resident top-K list
+// ordered (magnitude desc, bin asc).  KCAP is the compile-time list capacity (>= K); the
+// insertion is branch-free straight-line code over the KCAP slots.
+template <int KCAP>
+__global__ __launch_bounds__(HP_FRAMES) void k_hpcp(const float* __restrict__ mags,
+                                                    const uint64_t* __restrict__ frame_pfx,
+                                                    const uint64_t* __restrict__ tile_pfx,
+                                                    const int* __restrict__ tracks, int n_items, HpcpParams P,
+                                                    const HarmEntry* __restrict__ harm, float* __restrict__ chroma,
+                                                    float* __restrict__ energy) {
+    __shared__ float tile[HP_FRAMES][HP_CW + 1];
+    __shared__ float pc[12][HP_FRAMES];
     const uint64_t gb = blockIdx.x;
     const int it = find_track(tile_pfx, n_items, gb);
     const int trk = tracks[it];
     const int64_t F = (int64_t)(frame_pfx[trk + 1] - frame_pfx[trk]);
-    const int64_t f0 = (int64_t)(gb - tile_pfx[it]) * HP_T;
+    const int64_t f0 = (int64_t)(gb - tile_pfx[it]) * HP_FRAMES;
     const int i = threadIdx.x;
     const int64_t f = f0 + i;
     const bool valid = f < F;
     const uint64_t g0 = frame_pfx[trk];
+    const int K = P.K;
     float e = 0.0f, m1 = 0.0f, m2 = 0.0f;  // m1 = m[b-1], m2 = m[b-2]
-    int npk = 0;
+    float pm[KCAP];
+    int pb[KCAP];
+#pragma unroll
+    for (int q = 0; q < KCAP; q++) {
+        pm[q] = -1.0f;  // empty slot; every real peak is > 0
+        pb[q] = 0;
+    }
+    // Slots K..KCAP-1 hold the runners-up and are ignored at the end (the first K slots are
+    // exactly the top-K in order).  thr = pm[KCAP-1]: a candidate must beat it to move anything.
+    float thr = -1.0f;
+    const int sub = i / HP_CW, jj = i % HP_CW;
+    const int64_t rows = F - f0 < HP_FRAMES ? F - f0 : HP_FRAMES;
     for (int c0 = 0; c0 < P.B; c0 += HP_CW) {
         __syncthreads();
-        const int cw = P.B - c0 < HP_CW ? P.B - c0 : HP_CW;
-        for (int idx = i; idx < HP_T * HP_CW; idx += HP_T) {
-            const int r = idx / HP_CW, j = idx % HP_CW;
-            float v = 0.0f;
-            if (f0 + r < F && j < cw) v = mags[(g0 + (uint64_t)(f0 + r)) * (uint64_t)P.stride + c0 + j];
-            tile[r][j] = v;
-        }
+        const bool col_ok = c0 + jj < P.B;
+        const float* src = mags + (g0 + (uint64_t)f0) * (uint64_t)P.stride + c0 + jj;
+#pragma unroll 4
+        for (int r = sub; r < HP_FRAMES; r += HP_FRAMES / HP_CW)
+            tile[r][jj] = (r < rows && col_ok) ? src[(uint64_t)r * P.stride] : 0.0f;
         __syncthreads();
         if (!valid) continue;
+        const int cw = P.B - c0 < HP_CW ? P.B - c0 : HP_CW;
         for (int j = 0; j < cw; j++) {
             const int b = c0 + j;
             const float m = tile[i][j];
             e += m * m;
             const int c = b - 1;  // candidate peak bin, needs m[c-1] = m2, m[c] = m1, m[c+1] = m
-            if (c >= P.pk_lo && c <= P.pk_hi) {
-                if (!(m1 <= m2 || m1 < m)) {
-                    // insert (m1, c) keeping (mag desc, bin asc); bins arrive ascending
-                    int pos = npk;
-                    while (pos > 0 && pk_m[pos - 1][i] < m1) pos--;
-                    if (pos < P.K) {
-                        const int last = npk < P.K ? npk : P.K - 1;
-                        for (int q = last; q > pos; q--) {
-                            pk_m[q][i] = pk_m[q - 1][i];
-                            pk_b[q][i] = pk_b[q - 1][i];
-                        }
-                        pk_m[pos][i] = m1;
-                        pk_b[pos][i] = c;
-                        if (npk < P.K) npk++;
-                    }
+            if (c >= P.pk_lo && c <= P.pk_hi && !(m1 <= m2 || m1 < m) && m1 > thr) {
+                // insertion into the descending list; once inserted, every later slot shifts
+                // (an equal magnitude already listed has the lower bin and stays ahead)
+                float v = m1;
+                int vb = c;
+                bool ins = false;
+#pragma unroll
+                for (int q = 0; q < KCAP; q++) {
+                    const bool sw = ins || v > pm[q];
+                    const float tv = pm[q];
+                    const int tb = pb[q];
+                    pm[q] = sw ? v : tv;
+                    pb[q] = sw ? vb : tb;
+                    v = sw ? tv : v;
+                    vb = sw ? tb : vb;
+                    ins = sw;
                 }
+                thr = pm[KCAP - 1];
             }
             m2 = m1;
             m1 = m;
         }
     }
     if (!valid) return;
+#pragma unroll
     for (int q = 0; q < 12; q++) pc[q][i] = 0.0f;
-    for (int k = 0; k < npk; k++) {
-        const int bin = pk_b[k][i];
-        const float w0 = sd_powf(sd_maxf(pk_m[k][i], 0.0f), P.p);
+#pragma unroll
+    for (int k = 0; k < KCAP; k++) {
+        if (k >= K || !(pm[k] > 0.0f)) continue;
+        const int bin = pb[k];
+        const float w0 = sd_powf_ool(sd_maxf(pm[k], 0.0f), P.p);
         if (w0 <= 0.0f) continue;
         for (int h = 1; h <= P.hmax; h++) {
             const HarmEntry he = harm[bin * HP_HMAX + (h - 1)];
@@ -132,9 +243,11 @@ __global__ __launch_bounds__(HP_T) void k_hpcp(const float* __restrict__ mags, c
         }
     }
     float nsq = 0.0f;
+#pragma unroll
     for (int q = 0; q < 12; q++) nsq += pc[q][i] * pc[q][i];
     const float norm = __builtin_sqrtf(nsq);
     const uint64_t g = g0 + (uint64_t)f;
+#pragma unroll
     for (int q = 0; q < 12; q++) {
         float v = pc[q][i];
         if (norm > EPS) v /= norm;
@@ -415,15 +528,40 @@ void launch_mask(float* mags, int stride, int B, const uint64_t* frame_pfx, cons
                  float power, hipStream_t st) {
     if (n_items == 0) return;
     const int bpt = (B + MASK_T - 1) / MASK_T;
-    hipLaunchKernelGGL(k_mask, dim3(n_items * bpt), dim3(MASK_T), 0, st, mags, stride, B, frame_pfx, tracks, bpt,
-                       margin, power);
+    const size_t lds = (size_t)(2 * margin + 2 + margin + 1) * MASK_T * sizeof(float);
+    const float p = sd_maxf(power, 1.0f);
+    if (margin == 12 && p == 2.0f) {
+        hipLaunchKernelGGL((k_mask_r<12, 2>), dim3(n_items * bpt), dim3(MASK_T), 0, st, mags, stride, B, frame_pfx,
+                           tracks, bpt, power);
+        return;
+    }
+    if (p == 2.0f)
+        hipLaunchKernelGGL(k_mask<2>, dim3(n_items * bpt), dim3(MASK_T), lds, st, mags, stride, B, frame_pfx, tracks,
+                           bpt, margin, power);
+    else if (p == 1.0f)
+        hipLaunchKernelGGL(k_mask<1>, dim3(n_items * bpt), dim3(MASK_T), lds, st, mags, stride, B, frame_pfx, tracks,
+                           bpt, margin, power);
+    else
+        hipLaunchKernelGGL(k_mask<0>, dim3(n_items * bpt), dim3(MASK_T), lds, st, mags, stride, B, frame_pfx, tracks,
+                           bpt, margin, power);
 }
 void launch_hpcp(const float* mags, const uint64_t* frame_pfx, const uint64_t* tile_pfx, const int* tracks,
                  int n_items, uint64_t n_tiles, const HpcpParams& P, const HarmEntry* harm, float* chroma,
                  float* energy, hipStream_t st) {
     if (n_tiles == 0) return;
-    hipLaunchKernelGGL(k_hpcp, dim3((unsigned)n_tiles), dim3(HP_T), 0, st, mags, frame_pfx, tile_pfx, tracks, n_items,
-                       P, harm, chroma, energy);
+    const dim3 grid((unsigned)n_tiles), block(HP_FRAMES);
+    if (P.K <= 8)
+        hipLaunchKernelGGL(k_hpcp<8>, grid, block, 0, st, mags, frame_pfx, tile_pfx, tracks, n_items, P, harm, chroma,
+                           energy);
+    else if (P.K <= 16)
+        hipLaunchKernelGGL(k_hpcp<16>, grid, block, 0, st, mags, frame_pfx, tile_pfx, tracks, n_items, P, harm, chroma,
+                           energy);
+    else if (P.K <= 24)
+        hipLaunchKernelGGL(k_hpcp<24>, grid, block, 0, st, mags, frame_pfx, tile_pfx, tracks, n_items, P, harm, chroma,
+                           energy);
+    else
+        hipLaunchKernelGGL(k_hpcp<HP_KMAX>, grid, block, 0, st, mags, frame_pfx, tile_pfx, tracks, n_items, P, harm,
+                           chroma, energy);
 }
 void launch_key_vote(const int* tracks, int n_items, const uint64_t* frame_pfx, const float* chroma_raw,
                      const float* energy, float* chroma_s, float* weights, float* seg_scratch, const uint64_t* seg_off,

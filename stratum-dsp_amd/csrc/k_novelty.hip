@@ -95,61 +95,88 @@ __global__ __launch_bounds__(1024) void k_novelty(const float* __restrict__ E, c
     mf = block_max(mf, red);
     for (int64_t i = tid; i < L; i += NT) out[i] = mf > EPS ? cur[i] / mf : cur[i];
     __syncthreads();
-    if (tid == 0) {
-        float sum = 0.0f;
-        for (int64_t i = 0; i < L; i++) sum += out[i];
-        nov_sum[(uint64_t)v * T + trk] = sum;
+    __shared__ float sbuf[SEQ_CH];
+    const float sum = block_seq_sum(out, L, sbuf);
+    if (tid == 0) nov_sum[(uint64_t)v * T + trk] = sum;
+}
+
+// mel SuperFlux novelty (novelty.rs:553-609), variant index 4, in two kernels:
+// k_mel_flux, one thread per frame pair over the whole batch (MEL is mel-major, so the
+// reads are coalesced), raw flux + per-track max (atomicMax on the bits of a value >= 0);
+// k_mel_norm, one workgroup per track: normalise, then the curve's sequential sum.
+__device__ inline float mel_flux_frame(const float* mtile, int RW, int i, int n_mels, int K) {
+    float sum = 0.0f;
+    for (int b = 0; b < n_mels; b++) {
+        const int lo = b - K < 0 ? 0 : b - K;
+        const int hi = b + K + 1 < n_mels ? b + K + 1 : n_mels;
+        float pm = 0.0f;
+        for (int q = lo; q < hi; q++) pm = sd_maxf(pm, mtile[q * RW + i]);
+        const float d = sd_maxf(mtile[b * RW + i + 1] - pm, 0.0f);
+        sum += d * d;
+    }
+    return __builtin_sqrtf(sum);
+}
+
+__global__ __launch_bounds__(256) void k_mel_flux(const float* __restrict__ MEL, int n_mels, int K,
+                                                  const uint64_t* __restrict__ frame_pfx, int T, uint64_t total,
+                                                  float* __restrict__ nov, unsigned int* __restrict__ mx_bits) {
+    extern __shared__ float mtile[];  // [n_mels][257]: frames gb .. gb+256
+    constexpr int RW = 257;
+    const uint64_t gb = (uint64_t)blockIdx.x * 256;
+    for (int m = 0; m < n_mels; m++)
+        for (int r = threadIdx.x; r < RW; r += 256)
+            mtile[m * RW + r] = gb + r < total ? MEL[(uint64_t)m * total + gb + r] : 0.0f;
+    __syncthreads();
+    const int i = threadIdx.x;
+    const uint64_t g = gb + i;
+    const int trk = g < total ? find_track(frame_pfx, T, g) : -1;
+    // frames without a successor in their track (and padding lanes) contribute 0 to the max
+    float fl = 0.0f;
+    if (trk >= 0 && g + 1 < frame_pfx[trk + 1]) {
+        fl = mel_flux_frame(mtile, RW, i, n_mels, K);
+        nov[4 * total + g] = fl;
+    }
+    // one atomic per wave when the wave lies in one track (the common case)
+    const int t0 = __shfl(trk, 0, 64);
+    if (__all(trk == t0)) {
+        const float wm = wave_max(fl);
+        if ((threadIdx.x & 63) == 0 && t0 >= 0 && wm > 0.0f) atomicMax(&mx_bits[t0], sd_bits_f(wm));
+    } else if (trk >= 0 && fl > 0.0f) {
+        atomicMax(&mx_bits[trk], sd_bits_f(fl));
     }
 }
 
-// mel SuperFlux novelty (novelty.rs:553-609), variant index 4
-__global__ __launch_bounds__(256) void k_mel_novelty(const float* __restrict__ MEL, int n_mels, int K,
-                                                     const uint64_t* __restrict__ frame_pfx, int T, uint64_t total,
-                                                     float* __restrict__ nov, float* __restrict__ nov_sum) {
-    __shared__ float red[8];
+
+__global__ __launch_bounds__(256) void k_mel_norm(const uint64_t* __restrict__ frame_pfx, int T, uint64_t total,
+                                                  const unsigned int* __restrict__ mx_bits, float* __restrict__ nov,
+                                                  float* __restrict__ nov_sum) {
+    __shared__ float sbuf[SEQ_CH];
     const int trk = blockIdx.x;
     const int64_t F = (int64_t)(frame_pfx[trk + 1] - frame_pfx[trk]);
     if (F < 2) return;
     const int64_t L = F - 1;
-    const uint64_t g0 = frame_pfx[trk];
-    float* out = nov + 4 * total + g0;
-    float mf = 0.0f;
-    for (int64_t i = threadIdx.x; i < L; i += blockDim.x) {
-        const float* pv = MEL + (g0 + (uint64_t)i) * (uint64_t)n_mels;
-        const float* cv = pv + n_mels;
-        float sum = 0.0f;
-        for (int b = 0; b < n_mels; b++) {
-            const int lo = b - K < 0 ? 0 : b - K;
-            const int hi = b + K + 1 < n_mels ? b + K + 1 : n_mels;
-            float pm = 0.0f;
-            for (int q = lo; q < hi; q++) pm = sd_maxf(pm, pv[q]);
-            const float d = sd_maxf(cv[b] - pm, 0.0f);
-            sum += d * d;
-        }
-        const float fl = __builtin_sqrtf(sum);
-        out[i] = fl;
-        mf = sd_maxf(mf, fl);
-    }
-    mf = block_max(mf, red);
+    float* out = nov + 4 * total + frame_pfx[trk];
+    const float mf = sd_from_bits_f(mx_bits[trk]);
     if (mf > EPS)
         for (int64_t i = threadIdx.x; i < L; i += blockDim.x) out[i] /= mf;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        float sum = 0.0f;
-        for (int64_t i = 0; i < L; i++) sum += out[i];
-        nov_sum[4 * (uint64_t)T + trk] = sum;
-    }
+    const float sum = block_seq_sum(out, L, sbuf);
+    if (threadIdx.x == 0) nov_sum[4 * (uint64_t)T + trk] = sum;
 }
 
 void launch_novelty(const float* E, const float* H, const float* SFX, const uint64_t* frame_pfx, int T, uint64_t total,
                     const NovParams& P, float* scratch, float* nov, float* nov_sum, const float* MEL, int n_mels,
-                    int mel_k, bool mel_on, hipStream_t st) {
+                    int mel_k, bool mel_on, unsigned int* mel_max, hipStream_t st) {
     if (T == 0) return;
     hipLaunchKernelGGL(k_novelty, dim3(4 * T), dim3(1024), 0, st, E, H, SFX, frame_pfx, T, total, P, scratch, nov,
                        nov_sum);
-    if (mel_on)
-        hipLaunchKernelGGL(k_mel_novelty, dim3(T), dim3(256), 0, st, MEL, n_mels, mel_k, frame_pfx, T, total, nov,
-                           nov_sum);
+    if (mel_on && total > 0) {
+        (void)hipMemsetAsync(mel_max, 0, (size_t)T * sizeof(unsigned int), st);
+        hipLaunchKernelGGL(k_mel_flux, dim3((unsigned)((total + 255) / 256)), dim3(256),
+                           (size_t)n_mels * 257 * sizeof(float), st, MEL, n_mels, mel_k,
+                           frame_pfx, T, total, nov, mel_max);
+        hipLaunchKernelGGL(k_mel_norm, dim3(T), dim3(256), 0, st, frame_pfx, T, total, mel_max, nov, nov_sum);
+    }
 }
 
 }  // namespace sdsp

@@ -20,7 +20,16 @@ struct FeatParams {
     int band_on[4];    // variant enabled (full always)
     int n_mels;
 };
-constexpr int FT_FRAMES = 128;
+// per-bin mel accumulation plan (k_features): flush `nflush` finished mels before the bin,
+// then, in the reference's contribution order, add L*w0 to accumulator s0 and L*w1 to s1
+// (accumulator 0 = mel mA, 1 = mel mA+1; w = 0 means no contribution)
+struct MelPlan {
+    int nflush;
+    int s0, s1;
+    float w0, w1;
+};
+constexpr int PK_CH = 16384;  // samples per k_peak_abs workgroup
+constexpr int FT_FRAMES = 256;
 constexpr int FT_KMAX = 8;
 constexpr int FT_MELMAX = 48;
 
@@ -73,6 +82,7 @@ struct BeatOut {
 
 // ---- k_key ----
 constexpr int HP_KMAX = 32;
+constexpr int HP_FRAMES = 256;  // frames per k_hpcp workgroup
 constexpr int HP_HMAX = 8;
 struct HarmEntry {
     int state;
@@ -122,11 +132,11 @@ void launch_consensus(const uint32_t* energy, const uint64_t* e_off, const int* 
                       const uint64_t* f_off, const int* f_n, uint64_t kind_stride, int T, uint32_t tol, int enable,
                       const int* has_mags, uint32_t* chosen, const uint64_t* c_off, int* c_n, hipStream_t st);
 void launch_features(const float* mags, const float* fmax, const uint64_t* frame_pfx, const uint64_t* tile_pfx,
-                     int T, uint64_t n_tiles, const FeatParams& P, const int* mel_m, const float* mel_w, float* E,
-                     float* H, float* SFX, float* SFO, float* MEL, uint64_t total, hipStream_t st);
+                     int T, uint64_t n_tiles, const FeatParams& P, const MelPlan* mel, float* E, float* H, float* SFX,
+                     float* SFO, float* MEL, uint64_t total, hipStream_t st);
 void launch_novelty(const float* E, const float* H, const float* SFX, const uint64_t* frame_pfx, int T, uint64_t total,
                     const NovParams& P, float* scratch, float* nov, float* nov_sum, const float* MEL, int n_mels,
-                    int mel_k, bool mel_on, hipStream_t st);
+                    int mel_k, bool mel_on, unsigned int* mel_max, hipStream_t st);
 void launch_fft_tempogram(const int* items, int n_items, int T, const float* nov, const float* nov_sum,
                           const uint64_t* frame_pfx, uint64_t total, const FftTgParams& P, const cx* tw, const cx* rt,
                           cx* gscratch, const uint64_t* out_off, float* out_bpm, float* out_pow, hipStream_t st);

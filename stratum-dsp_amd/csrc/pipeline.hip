@@ -100,6 +100,30 @@ MelTable mel_table(uint32_t sr, int n_bins, int n_mels_in, float fmin_hz, float 
     return t;
 }
 
+// Register-pair schedule for the mel sums (see k_features.hip): mels are flushed in index
+// order; every contribution of a bin must land on the two live accumulators mA, mA+1.
+std::vector<MelPlan> mel_plan(const MelTable& t, int n_bins, std::string* err) {
+    std::vector<MelPlan> p((size_t)n_bins, MelPlan{0, 0, 0, 0.0f, 0.0f});
+    int mA = 0;
+    for (int b = 0; b < n_bins; b++) {
+        int mx = -1;
+        for (int s = 0; s < 2; s++) mx = std::max(mx, t.m[(size_t)b * 2 + s]);
+        if (mx < 0) continue;
+        const int nf = std::max(0, mx - (mA + 1));
+        MelPlan& q = p[(size_t)b];
+        q.nflush = nf;
+        mA += nf;
+        for (int s = 0; s < 2; s++) {
+            const int m = t.m[(size_t)b * 2 + s];
+            if (m < 0) continue;
+            if (m != mA && m != mA + 1) *err = "mel filterbank: contributions not on adjacent mels";
+            (s == 0 ? q.s0 : q.s1) = m - mA;
+            (s == 0 ? q.w0 : q.w1) = t.w[(size_t)b * 2 + s];
+        }
+    }
+    return p;
+}
+
 // hz_to_bin, tempogram.rs:279-289
 int hz_to_bin(float f, float fres, int n_bins) {
     if (!sd_isfinite_f(f) || f <= 0.0f || !sd_isfinite_f(fres) || fres <= 0.0f) return 0;
@@ -256,7 +280,7 @@ struct Timers {
         d = &dc;
         for (auto& e : ev) SDSP_HIP_CHECK(hipEventCreate(&e));
     }
-    void mark(int i) { SDSP_HIP_CHECK(hipEventRecord(ev[i], d->stream)); }
+    void mark(int i, hipStream_t s = nullptr) { SDSP_HIP_CHECK(hipEventRecord(ev[i], s ? s : d->stream)); }
     double ms(int a, int b) {
         float t = 0.0f;
         if (hipEventElapsedTime(&t, ev[a], ev[b]) != hipSuccess) return 0.0;
@@ -482,14 +506,15 @@ void Pipeline::tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPa
                             &merr);
     if (!merr.empty()) throw HipError(merr);
     fp.n_mels = mel_on ? mt.n_mels : 0;
-    int* d_melm = c_.up(tag + "melm", mt.m);
-    float* d_melw = c_.up(tag + "melw", mt.w);
+    std::vector<MelPlan> mplan = mel_plan(mt, B, &merr);
+    if (!merr.empty()) throw HipError(merr);
+    MelPlan* d_mplan = c_.up(tag + "melplan", mplan);
     o.E = c_.dev<float>(tag + "E", 4 * total);
     o.H = c_.dev<float>(tag + "H", 4 * total);
     o.SFX = c_.dev<float>(tag + "SFX", 4 * total);
     o.SFO = c_.dev<float>(tag + "SFO", total);
     o.MEL = c_.dev<float>(tag + "MEL", std::max<uint64_t>(total * (uint64_t)std::max(fp.n_mels, 1), 1));
-    launch_features(o.mags, o.fmax, o.d_fpfx, d_tpfx, P_T, tpfx[(size_t)P_T], fp, d_melm, d_melw, o.E, o.H, o.SFX, o.SFO,
+    launch_features(o.mags, o.fmax, o.d_fpfx, d_tpfx, P_T, tpfx[(size_t)P_T], fp, d_mplan, o.E, o.H, o.SFX, o.SFO,
                     o.MEL, total, d_.stream);
     SDSP_HIP_CHECK(hipGetLastError());
     // novelty
@@ -513,7 +538,8 @@ void Pipeline::tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPa
     o.nov = c_.dev<float>(tag + "nov", NVAR * std::max<uint64_t>(total, 1));
     o.nov_sum = c_.dev<float>(tag + "novsum", NVAR * (size_t)std::max(P_T, 1));
     launch_novelty(o.E, o.H, o.SFX, o.d_fpfx, P_T, total, np, scratch, o.nov, o.nov_sum, o.MEL, fp.n_mels,
-                   (int)std::max<uint64_t>(cfg_.tempogram_mel_max_filter_bins, 1), mel_on, d_.stream);
+                   (int)std::max<uint64_t>(cfg_.tempogram_mel_max_filter_bins, 1), mel_on,
+                   c_.dev<unsigned int>(tag + "melmax", (size_t)std::max(P_T, 1)), d_.stream);
     SDSP_HIP_CHECK(hipGetLastError());
     tm.mark(2);
     // tempograms: items (track, variant) for active tracks
@@ -655,7 +681,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     for (int t = 0; t < T; t++) {
         off[(size_t)t] = in_off[(size_t)idx[(size_t)t]];
         nr[(size_t)t] = n_raw[(size_t)idx[(size_t)t]];
-        cpfx[(size_t)t + 1] = cpfx[(size_t)t] + (nr[(size_t)t] + 4095) / 4096;
+        cpfx[(size_t)t + 1] = cpfx[(size_t)t] + (nr[(size_t)t] + PK_CH - 1) / PK_CH;
         const uint64_t fs = nr[(size_t)t] >= (uint64_t)FS ? (nr[(size_t)t] - FS) / (FS / 2) + 1 : 1;
         spfx[(size_t)t + 1] = spfx[(size_t)t] + (cfg_.enable_silence_trimming ? fs : 0);
     }
@@ -711,6 +737,120 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     bin.top_n = mr_on ? base_top_n : (cfg_.emit_tempogram_candidates ? (int)cfg_.tempogram_candidates_top_n : 1);
     bin.cand_cap = std::max(bin.top_n, 1);
     bin.gate = mr_on;
+    // ---------------- E: key (second stream; overlaps B-D) ----------------
+    // The key path depends only on the trimmed signal, so it is forked onto the context's key
+    // stream right after trimming and joined before the results are read back: its
+    // bandwidth-bound STFT/mask/HPCP kernels run under the latency-bound tempo and beat
+    // kernels of the main stream.
+    const int KFS = 8192, KHOP = (int)std::max<uint64_t>(cfg_.key_stft_hop_size, 1);
+    std::vector<int> K;  // positions in R
+    std::vector<uint64_t> kpfx(1, 0), ktile(1, 0), kseg(1, 0), ksrc;
+    std::vector<float> kgain;
+    const int seg_len_cfg = (int)std::min<uint64_t>(cfg_.key_segment_len_frames, INT32_MAX);
+    const int seg_hop = (int)std::max<uint64_t>(std::min<uint64_t>(cfg_.key_segment_hop_frames, (uint64_t)seg_len_cfg), 1);
+    const bool seg_voting = cfg_.enable_key_segment_voting && cfg_.key_segment_len_frames >= 120 &&
+                            cfg_.key_segment_hop_frames >= 1;
+    double key_in_bytes = 0;
+    for (int i = 0; i < NR; i++) {
+        const uint64_t n = bin.n_trim[(size_t)i];
+        if (n < (uint64_t)FS || n < (uint64_t)KFS) continue;  // key skipped or empty key spectrogram -> default key
+        const uint64_t F8 = (n - KFS) / (uint64_t)KHOP + 1;
+        K.push_back(i);
+        kpfx.push_back(kpfx.back() + F8);
+        ktile.push_back(ktile.back() + (F8 + HP_FRAMES - 1) / HP_FRAMES);
+        const uint64_t ns = (seg_voting && F8 >= (uint64_t)std::max(seg_len_cfg, 1)) ? (F8 - seg_len_cfg) / seg_hop + 1 : 0;
+        kseg.push_back(kseg.back() + 50 * ns);
+        ksrc.push_back(bin.src_off[(size_t)i]);
+        kgain.push_back(bin.gain_h[(size_t)i]);
+        key_in_bytes += 4.0 * (double)n;
+    }
+    const int NK = (int)K.size();
+    std::vector<KeyOut> kout;
+    KeyOut* d_kout = nullptr;
+    Timers kt;
+    kt.init(d_);
+    // SDSP_SERIAL_STREAMS=1 keeps the key path on the main stream (per-kernel profiling)
+    static const bool serial_streams = std::getenv("SDSP_SERIAL_STREAMS") != nullptr;
+    hipStream_t st2 = serial_streams ? st : d_.stream2;
+    if (NK > 0) {
+        const uint64_t total8 = kpfx.back();
+        uint64_t* d_kpfx = c_.up("E.kpfx", kpfx);
+        uint64_t* d_ktile = c_.up("E.ktile", ktile);
+        uint64_t* d_kseg = c_.up("E.kseg", kseg);
+        uint64_t* d_ksrc = c_.up("E.ksrc", ksrc);
+        float* d_kgain = c_.up("E.kgain", kgain);
+        std::vector<int> kid((size_t)NK);
+        for (int k = 0; k < NK; k++) kid[(size_t)k] = k;
+        int* d_kid = c_.up("E.kid", kid);
+        FftTables& t8 = d_.tables(KFS, true);
+        float* mags8 = c_.dev<float>("E.mags8", total8 * STRIDE8);
+        // uploads above were queued on the main stream: order the key stream after them
+        kt.mark(7);
+        SDSP_HIP_CHECK(hipStreamWaitEvent(st2, kt.ev[7], 0));
+        kt.mark(0, st2);
+        launch_stft(KFS, false, d_samples, d_kpfx, NK, total8, d_ksrc, d_kgain, KHOP, t8.window.as<float>(), t8.tw.as<cx>(),
+                    t8.rt.as<cx>(), mags8, d_kpfx, STRIDE8, nullptr, st2);
+        SDSP_HIP_CHECK(hipGetLastError());
+        kt.mark(1, st2);
+        const int B8 = KFS / 2 + 1;
+        if (cfg_.enable_key_harmonic_mask)
+            launch_mask(mags8, STRIDE8, B8, d_kpfx, d_kid, NK, (int)cfg_.key_spectrogram_smooth_margin,
+                        cfg_.key_harmonic_mask_power, st2);
+        HpcpParams hp{};
+        hp.B = B8;
+        hp.stride = STRIDE8;
+        const float fres8 = (float)sr_ / (float)KFS;
+        const float fmin = sd_maxf(100.0f, 20.0f), fmax = sd_minf(5000.0f, (float)sr_ / 2.0f);
+        hp.pk_lo = 1;
+        hp.pk_hi = 0;
+        if (fmax > fmin) {
+            int lo = -1, hi = -1;
+            for (int b = 1; b + 1 < B8; b++) {
+                const float f = (float)b * fres8;
+                if (f < fmin) continue;
+                if (f > fmax) break;
+                if (lo < 0) lo = b;
+                hi = b;
+            }
+            if (lo >= 0) {
+                hp.pk_lo = lo;
+                hp.pk_hi = hi;
+            }
+        }
+        hp.K = (int)std::max<uint64_t>(cfg_.key_hpcp_peaks_per_frame, 1);
+        hp.hmax = (int)std::max<uint64_t>(cfg_.key_hpcp_num_harmonics, 1);
+        hp.p = sd_clampf(cfg_.key_hpcp_mag_power, 0.05f, 1.0f);
+        std::vector<HarmEntry> ht = harm_table(B8, sr_, KFS, cfg_.soft_mapping_sigma, hp.hmax, cfg_.key_hpcp_harmonic_decay);
+        HarmEntry* d_ht = c_.up("E.harm", ht);
+        float* d_chroma = c_.dev<float>("E.chroma", total8 * 12);
+        float* d_energy = c_.dev<float>("E.energy", total8);
+        launch_hpcp(mags8, d_kpfx, d_ktile, d_kid, NK, ktile.back(), hp, d_ht, d_chroma, d_energy, st2);
+        SDSP_HIP_CHECK(hipGetLastError());
+        std::vector<float> tpl(288);
+        kk_templates(tpl.data());
+        float* d_tpl = c_.up("E.tpl", tpl);
+        KeyParams kp{};
+        kp.weighting = cfg_.enable_key_frame_weighting;
+        kp.min_tonal = cfg_.key_min_tonalness;
+        kp.tonal_pow = cfg_.key_tonalness_power;
+        kp.energy_pow = cfg_.key_energy_power;
+        kp.seg_voting = seg_voting;
+        kp.seg_len = std::max(seg_len_cfg, 1);
+        kp.seg_hop = seg_hop;
+        kp.min_clarity = sd_clampf(cfg_.key_segment_min_clarity, 0.0f, 1.0f);
+        float* d_cs = c_.dev<float>("E.chroma_s", total8 * 12);
+        float* d_w = c_.dev<float>("E.weights", total8);
+        float* d_sscr = c_.dev<float>("E.segscr", std::max<uint64_t>(kseg.back(), 1));
+        d_kout = c_.dev<KeyOut>("E.kout", (size_t)NK);
+        // the template upload above is on the main stream too
+        kt.mark(8);
+        SDSP_HIP_CHECK(hipStreamWaitEvent(st2, kt.ev[8], 0));
+        launch_key_vote(d_kid, NK, d_kpfx, d_chroma, d_energy, d_cs, d_w, d_sscr, d_kseg, d_tpl, kp, d_kout, st2);
+        SDSP_HIP_CHECK(hipGetLastError());
+        kt.mark(2, st2);
+        times_.stft8192_launches += 1;
+        times_.stft8192_bytes += key_in_bytes + 4.0 * (double)total8 * (double)B8;
+    }
     TempoPassOut bo;
     tempo_pass("B.", bin, bo);
     times_.stft2048_ms += bo.stft_ms;
@@ -872,110 +1012,13 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
                 d_bout, st);
     SDSP_HIP_CHECK(hipGetLastError());
     tm.mark(5);
-    // ---------------- E: key ----------------
-    const int KFS = 8192, KHOP = (int)std::max<uint64_t>(cfg_.key_stft_hop_size, 1);
-    std::vector<int> K;  // positions in R
-    std::vector<uint64_t> kpfx(1, 0), ktile(1, 0), kseg(1, 0), ksrc;
-    std::vector<float> kgain;
-    const int seg_len_cfg = (int)std::min<uint64_t>(cfg_.key_segment_len_frames, INT32_MAX);
-    const int seg_hop = (int)std::max<uint64_t>(std::min<uint64_t>(cfg_.key_segment_hop_frames, (uint64_t)seg_len_cfg), 1);
-    const bool seg_voting = cfg_.enable_key_segment_voting && cfg_.key_segment_len_frames >= 120 &&
-                            cfg_.key_segment_hop_frames >= 1;
-    double key_in_bytes = 0;
-    for (int i = 0; i < NR; i++) {
-        const uint64_t n = bin.n_trim[(size_t)i];
-        if (n < (uint64_t)FS || n < (uint64_t)KFS) continue;  // key skipped or empty key spectrogram -> default key
-        const uint64_t F8 = (n - KFS) / (uint64_t)KHOP + 1;
-        K.push_back(i);
-        kpfx.push_back(kpfx.back() + F8);
-        ktile.push_back(ktile.back() + (F8 + 63) / 64);
-        const uint64_t ns = (seg_voting && F8 >= (uint64_t)std::max(seg_len_cfg, 1)) ? (F8 - seg_len_cfg) / seg_hop + 1 : 0;
-        kseg.push_back(kseg.back() + 50 * ns);
-        ksrc.push_back(bin.src_off[(size_t)i]);
-        kgain.push_back(bin.gain_h[(size_t)i]);
-        key_in_bytes += 4.0 * (double)n;
-    }
-    const int NK = (int)K.size();
-    std::vector<KeyOut> kout;
-    if (NK > 0) {
-        const uint64_t total8 = kpfx.back();
-        uint64_t* d_kpfx = c_.up("E.kpfx", kpfx);
-        uint64_t* d_ktile = c_.up("E.ktile", ktile);
-        uint64_t* d_kseg = c_.up("E.kseg", kseg);
-        uint64_t* d_ksrc = c_.up("E.ksrc", ksrc);
-        float* d_kgain = c_.up("E.kgain", kgain);
-        std::vector<int> kid((size_t)NK);
-        for (int k = 0; k < NK; k++) kid[(size_t)k] = k;
-        int* d_kid = c_.up("E.kid", kid);
-        FftTables& t8 = d_.tables(KFS, true);
-        float* mags8 = c_.dev<float>("E.mags8", total8 * STRIDE8);
-        Timers kt;
-        kt.init(d_);
-        kt.mark(0);
-        launch_stft(KFS, false, d_samples, d_kpfx, NK, total8, d_ksrc, d_kgain, KHOP, t8.window.as<float>(), t8.tw.as<cx>(),
-                    t8.rt.as<cx>(), mags8, d_kpfx, STRIDE8, nullptr, st);
-        SDSP_HIP_CHECK(hipGetLastError());
-        kt.mark(1);
-        const int B8 = KFS / 2 + 1;
-        if (cfg_.enable_key_harmonic_mask)
-            launch_mask(mags8, STRIDE8, B8, d_kpfx, d_kid, NK, (int)cfg_.key_spectrogram_smooth_margin,
-                        cfg_.key_harmonic_mask_power, st);
-        HpcpParams hp{};
-        hp.B = B8;
-        hp.stride = STRIDE8;
-        const float fres8 = (float)sr_ / (float)KFS;
-        const float fmin = sd_maxf(100.0f, 20.0f), fmax = sd_minf(5000.0f, (float)sr_ / 2.0f);
-        hp.pk_lo = 1;
-        hp.pk_hi = 0;
-        if (fmax > fmin) {
-            int lo = -1, hi = -1;
-            for (int b = 1; b + 1 < B8; b++) {
-                const float f = (float)b * fres8;
-                if (f < fmin) continue;
-                if (f > fmax) break;
-                if (lo < 0) lo = b;
-                hi = b;
-            }
-            if (lo >= 0) {
-                hp.pk_lo = lo;
-                hp.pk_hi = hi;
-            }
-        }
-        hp.K = (int)std::max<uint64_t>(cfg_.key_hpcp_peaks_per_frame, 1);
-        hp.hmax = (int)std::max<uint64_t>(cfg_.key_hpcp_num_harmonics, 1);
-        hp.p = sd_clampf(cfg_.key_hpcp_mag_power, 0.05f, 1.0f);
-        std::vector<HarmEntry> ht = harm_table(B8, sr_, KFS, cfg_.soft_mapping_sigma, hp.hmax, cfg_.key_hpcp_harmonic_decay);
-        HarmEntry* d_ht = c_.up("E.harm", ht);
-        float* d_chroma = c_.dev<float>("E.chroma", total8 * 12);
-        float* d_energy = c_.dev<float>("E.energy", total8);
-        launch_hpcp(mags8, d_kpfx, d_ktile, d_kid, NK, ktile.back(), hp, d_ht, d_chroma, d_energy, st);
-        SDSP_HIP_CHECK(hipGetLastError());
-        std::vector<float> tpl(288);
-        kk_templates(tpl.data());
-        float* d_tpl = c_.up("E.tpl", tpl);
-        KeyParams kp{};
-        kp.weighting = cfg_.enable_key_frame_weighting;
-        kp.min_tonal = cfg_.key_min_tonalness;
-        kp.tonal_pow = cfg_.key_tonalness_power;
-        kp.energy_pow = cfg_.key_energy_power;
-        kp.seg_voting = seg_voting;
-        kp.seg_len = std::max(seg_len_cfg, 1);
-        kp.seg_hop = seg_hop;
-        kp.min_clarity = sd_clampf(cfg_.key_segment_min_clarity, 0.0f, 1.0f);
-        float* d_cs = c_.dev<float>("E.chroma_s", total8 * 12);
-        float* d_w = c_.dev<float>("E.weights", total8);
-        float* d_sscr = c_.dev<float>("E.segscr", std::max<uint64_t>(kseg.back(), 1));
-        KeyOut* d_kout = c_.dev<KeyOut>("E.kout", (size_t)NK);
-        launch_key_vote(d_kid, NK, d_kpfx, d_chroma, d_energy, d_cs, d_w, d_sscr, d_kseg, d_tpl, kp, d_kout, st);
-        SDSP_HIP_CHECK(hipGetLastError());
-        kt.mark(2);
+    tm.mark(6);
+    if (NK > 0) {  // join the key stream
+        SDSP_HIP_CHECK(hipStreamWaitEvent(st, kt.ev[2], 0));
         kout = c_.down(d_kout, (size_t)NK);
         times_.stft8192_ms += kt.ms(0, 1);
         times_.key_ms += kt.ms(1, 2);
-        times_.stft8192_launches += 1;
-        times_.stft8192_bytes += key_in_bytes + 4.0 * (double)total8 * (double)B8;
     }
-    tm.mark(6);
     // ---------------- results ----------------
     std::vector<BeatOut> bout = c_.down(d_bout, (size_t)NR);
     std::vector<float> beats_h = c_.down(d_beats, boff[(size_t)NR]), downs_h = c_.down(d_downs, boff[(size_t)NR]);

@@ -20,6 +20,7 @@ DeviceCtx& device_ctx(int device) {
         c->device = device;
         SDSP_HIP_CHECK(hipSetDevice(device));
         SDSP_HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        SDSP_HIP_CHECK(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
     }
     return *c;
 }

@@ -22,6 +22,11 @@ __device__ __forceinline__ cx cadd(cx a, cx b) { return {a.re + b.re, a.im + b.i
 __device__ __forceinline__ cx csub(cx a, cx b) { return {a.re - b.re, a.im - b.im}; }
 __device__ __forceinline__ cx cmul(cx w, cx z) { return {w.re * z.re - w.im * z.im, w.re * z.im + w.im * z.re}; }
 
+// Out-of-line copies of the general transcendental paths, for unrolled loops that would
+// otherwise inline them once per iteration (instruction-cache pressure).
+__device__ __noinline__ inline float sd_powf_ool(float x, float y) { return sd_powf(x, y); }
+__device__ __noinline__ inline float sd_logf_ool(float x) { return sd_logf(x); }
+
 // ---- wave / block reductions (order-free ops only: max, min, integer sums) ----
 __device__ __forceinline__ float wave_max(float v) {
     for (int o = 32; o > 0; o >>= 1) v = sd_maxf(v, __shfl_xor(v, o, 64));

@@ -59,7 +59,8 @@ struct StageTimer;
 
 struct DeviceCtx {
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;   // main (tempo / beat) stream
+    hipStream_t stream2 = nullptr;  // key-path stream, forked from and joined to `stream`
     std::mutex mu;
     std::map<int, std::unique_ptr<FftTables>> fft;  // keyed by real FFT size N
     std::map<std::string, std::unique_ptr<DevBuf>> bufs;
