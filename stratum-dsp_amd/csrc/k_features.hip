@@ -67,25 +67,42 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const float* __restrict_
     const float* base = mags + (g0 + (uint64_t)f0) * (uint64_t)P.stride;  // row r at base + (r-1)*stride
     const int sub = i / CW, jj = i % CW;
 
-    // stage bins [b0, b0+CW) (columns beyond B or rows outside the track read as 0)
-    auto stage = [&](int b0) {
+    // stage bins [b0, b0+CW) (columns beyond B or rows outside the track read as 0), in two
+    // halves so the loads of the next step are in flight while the current step is walked
+    constexpr int RSTEP = FT_FRAMES / CW;
+    constexpr int NLD = (ROWS + RSTEP - 1) / RSTEP;
+    float nx[NLD];
+    auto load = [&](int b0) {
         const int b = b0 + jj;
         const bool col_ok = b < B;
-        const int slot = b & (W - 1);
-#pragma unroll 4
-        for (int r = sub; r < ROWS; r += FT_FRAMES / CW) {
-            float v = 0.0f;
-            if (col_ok && r >= r_lo && r < r_hi) v = base[(int64_t)(r - 1) * P.stride + b];
-            Mt[r][slot] = v;
-            Lt[r][slot] = sd_logf(1.0f + sd_maxf(v, 0.0f));
+#pragma unroll
+        for (int u = 0; u < NLD; u++) {
+            const int r = sub + u * RSTEP;
+            nx[u] = (col_ok && r >= r_lo && r < r_hi) ? base[(int64_t)(r - 1) * P.stride + b] : 0.0f;
+        }
+    };
+    auto commit = [&](int b0) {
+        const int slot = (b0 + jj) & (W - 1);
+#pragma unroll
+        for (int u = 0; u < NLD; u++) {
+            const int r = sub + u * RSTEP;
+            if (r < ROWS) {
+                Mt[r][slot] = nx[u];
+                Lt[r][slot] = sd_logf(1.0f + sd_maxf(nx[u], 0.0f));
+            }
         }
     };
     // prologue: bins [0, K) (K <= CW)
-    if (jj < K) stage(0);
+    if (jj < K) {
+        load(0);
+        commit(0);
+    }
+    load(K);
     for (int c0 = 0; c0 < B; c0 += CW) {
         __syncthreads();  // previous step's readers are done with the slots overwritten here
-        stage(c0 + K);
+        commit(c0 + K);
         __syncthreads();
+        if (c0 + CW < B) load(c0 + CW + K);
         const int nb = B - c0 < CW ? B - c0 : CW;
         if (!valid) continue;
         for (int j = 0; j < nb; j++) {

@@ -89,14 +89,24 @@ __global__ __launch_bounds__(RMS_ROWS) void k_frame_rms(const float* __restrict_
     r_len[tid] = len;
     float sum = 0.0f;
     const int sub = tid / RMS_KC, j = tid % RMS_KC;
+    constexpr int RSTEP = RMS_ROWS / RMS_KC, NLD = RMS_ROWS / RSTEP;
+    __syncthreads();
+    float nx[NLD];
+    auto load = [&](int c0) {
+        const uint32_t k = (uint32_t)(c0 + j);
+#pragma unroll
+        for (int u = 0; u < NLD; u++) {
+            const int r = sub + u * RSTEP;
+            nx[u] = k < r_len[r] ? x[r_beg[r] + k] : 0.0f;
+        }
+    };
+    load(0);
     for (int c0 = 0; c0 < fs; c0 += RMS_KC) {
         __syncthreads();
-#pragma unroll 8
-        for (int r = sub; r < RMS_ROWS; r += RMS_ROWS / RMS_KC) {
-            const uint32_t k = (uint32_t)(c0 + j);
-            tile[r][j] = k < r_len[r] ? x[r_beg[r] + k] * r_gain[r] : 0.0f;
-        }
+#pragma unroll
+        for (int u = 0; u < NLD; u++) tile[sub + u * RSTEP][j] = nx[u] * r_gain[sub + u * RSTEP];
         __syncthreads();
+        if (c0 + RMS_KC < fs) load(c0 + RMS_KC);
         const int lim = (int)len - c0 < RMS_KC ? (int)len - c0 : RMS_KC;
         for (int q = 0; q < lim; q++) {
             const float v = tile[tid][q];

@@ -187,14 +187,25 @@ __global__ __launch_bounds__(HP_FRAMES) void k_hpcp(const float* __restrict__ ma
     float thr = -1.0f;
     const int sub = i / HP_CW, jj = i % HP_CW;
     const int64_t rows = F - f0 < HP_FRAMES ? F - f0 : HP_FRAMES;
+    // software pipeline: chunk c0+HP_CW is loaded into registers while chunk c0 is walked
+    constexpr int NLD = HP_FRAMES * HP_CW / HP_FRAMES;  // loads per thread per chunk
+    constexpr int RSTEP = HP_FRAMES / HP_CW;
+    const float* rowp = mags + (g0 + (uint64_t)f0 + (uint64_t)sub) * (uint64_t)P.stride + jj;
+    const uint64_t rstride = (uint64_t)RSTEP * (uint64_t)P.stride;
+    float nx[NLD];
+    auto load_chunk = [&](int c0) {
+        const bool col_ok = c0 + jj < P.B;
+#pragma unroll
+        for (int u = 0; u < NLD; u++)
+            nx[u] = (sub + u * RSTEP < rows && col_ok) ? rowp[(uint64_t)u * rstride + c0] : 0.0f;
+    };
+    load_chunk(0);
     for (int c0 = 0; c0 < P.B; c0 += HP_CW) {
         __syncthreads();
-        const bool col_ok = c0 + jj < P.B;
-        const float* src = mags + (g0 + (uint64_t)f0) * (uint64_t)P.stride + c0 + jj;
-#pragma unroll 4
-        for (int r = sub; r < HP_FRAMES; r += HP_FRAMES / HP_CW)
-            tile[r][jj] = (r < rows && col_ok) ? src[(uint64_t)r * P.stride] : 0.0f;
+#pragma unroll
+        for (int u = 0; u < NLD; u++) tile[sub + u * RSTEP][jj] = nx[u];
         __syncthreads();
+        if (c0 + HP_CW < P.B) load_chunk(c0 + HP_CW);
         if (!valid) continue;
         const int cw = P.B - c0 < HP_CW ? P.B - c0 : HP_CW;
         for (int j = 0; j < cw; j++) {

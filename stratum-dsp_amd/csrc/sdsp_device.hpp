@@ -27,6 +27,15 @@ __device__ __forceinline__ cx cmul(cx w, cx z) { return {w.re * z.re - w.im * z.
 __device__ __noinline__ inline float sd_powf_ool(float x, float y) { return sd_powf(x, y); }
 __device__ __noinline__ inline float sd_logf_ool(float x) { return sd_logf(x); }
 
+// Workgroups are dispatched round-robin over the 8 XCDs (each with its own L2).  Renumber so
+// that XCD x owns one contiguous range of logical blocks: kernels whose neighbouring blocks
+// share input (overlapping STFT frames) then find it in their own L2.  Speed only; any
+// placement is correct.
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
+    const uint32_t per = nb / 8, rem = nb % 8, x = b % 8, l = b / 8;
+    return x < rem ? x * (per + 1) + l : rem * (per + 1) + (x - rem) * per + l;
+}
+
 // ---- wave / block reductions (order-free ops only: max, min, integer sums) ----
 __device__ __forceinline__ float wave_max(float v) {
     for (int o = 32; o > 0; o >>= 1) v = sd_maxf(v, __shfl_xor(v, o, 64));
