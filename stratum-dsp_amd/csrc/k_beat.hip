@@ -1,4 +1,4 @@
-// k_beat.hip — beat grid, one thread per track (reference src/features/beat_tracking/):
+// k_beat.hip — beat grid, one wavefront per track (reference src/features/beat_tracking/):
 //
 //   HmmBeatTracker::track_beats   hmm.rs:121-441
 //   detect_tempo_variations       tempo_variation.rs:95-227
@@ -6,9 +6,14 @@
 //   detect_time_signature         time_signature.rs:90-199
 //   generate_beat_grid, downbeats, stability   beat_tracking/mod.rs:108-485
 //
-// Work per track is a few thousand scalar steps; the reference's O(frames x onsets) nearest-
-// onset scans become binary searches over the sorted onsets.  |o - t| is monotone on each
-// side of t in f32, so the nearest neighbour's distance is exactly the reference's minimum.
+// The reference's O(frames x onsets) nearest-onset scans become binary searches over the
+// sorted onsets (|o - t| is monotone on each side of t in f32, so the nearest neighbour's
+// distance is exactly the reference's minimum).  The 64 lanes of the track's wave split the
+// independent work: HMM frames (ordered compaction by ballot), Bayesian candidate tempos
+// (one lane each, each likelihood folded sequentially as in the reference), the refined-beat
+// sort (bitonic with index tie-break == the reference's stable sort) and the three
+// time-signature scores.  Sequential folds (interval means, variances, autocorrelation) stay
+// on one lane in the reference's order.  The onsets are staged in LDS when they fit.
 // The Viterbi pass is not run: the emission is identical for all five states (hmm.rs:264-294),
 // so the extracted beats cannot depend on the path and Viterbi cannot fail.
 #include "kernels.hpp"
@@ -48,30 +53,73 @@ __device__ inline float nearest_dist(const float* on, int n, float t) {
     return md;
 }
 
-// hmm.rs:121-441; returns number of beats or -1 (Err)
+// hmm.rs:121-441, all lanes of the wave (uniform arguments); returns the number of beats or
+// -1 (Err).  *overflow is set when more than `cap` beats would be emitted.
 __device__ int hmm_track(float bpm, const float* on, int n, float* out, int cap, int* overflow) {
     if (bpm <= EPS || bpm > 300.0f) return -1;
     if (n <= 0) return -1;
+    const int lane = threadIdx.x & 63;
     const float start = on[0], end = on[n - 1];
     const float interval = 60.0f / bpm;
     const uint64_t nf = sd_f2u64(__builtin_ceilf((end - start) / interval)) + 1;
     const float sigma = 0.05f / 2.0f;
     const float sigma_sq = sigma * sigma;
     int nb = 0;
-    for (uint64_t t = 0; t < nf; t++) {
-        const float ft = start + ((float)t * interval);
-        const float md = nearest_dist(on, n, ft);
-        const float dsq = md * md;
-        const float em = sd_expf(-dsq / (2.0f * sigma_sq));
-        if (em > 0.1f) {
-            if (nb >= cap) {
-                *overflow = 1;
-                return nb;
-            }
-            out[nb++] = ft;
+    for (uint64_t t0 = 0; t0 < nf; t0 += 64) {
+        const uint64_t t = t0 + (uint64_t)lane;
+        bool keep = false;
+        float ft = 0.0f;
+        if (t < nf) {
+            ft = start + ((float)t * interval);
+            const float md = nearest_dist(on, n, ft);
+            const float dsq = md * md;
+            const float em = sd_expf(-dsq / (2.0f * sigma_sq));
+            keep = em > 0.1f;
         }
+        const unsigned long long bal = __ballot(keep);
+        const int pos = nb + __popcll(bal & ((1ull << lane) - 1ull));
+        const int cnt = __popcll(bal);
+        if (keep && pos < cap) out[pos] = ft;
+        if (nb + cnt > cap) {
+            *overflow = 1;
+            return cap;
+        }
+        nb += cnt;
     }
     return nb;
+}
+
+// Stable ascending sort of a[0..n) (the reference's sort_by(partial_cmp) on NaN-free data):
+// bitonic over (value, index) keys in LDS, the index breaking ties.  n <= 2*cap_pow2 slots.
+__device__ void wave_sort_stable(float* a, int n, float* kv, int* ki, int npow2) {
+    const int lane = threadIdx.x & 63;
+    for (int i = lane; i < npow2; i += 64) {
+        kv[i] = i < n ? a[i] : SD_INF_F;
+        ki[i] = i < n ? i : 0x7fffffff;
+    }
+    __syncthreads();
+    for (int k = 2; k <= npow2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = lane; i < npow2; i += 64) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const bool up = (i & k) == 0;
+                    const float vi = kv[i], vl = kv[l];
+                    const int ii = ki[i], il = ki[l];
+                    const bool gt = (vi > vl) || (vi == vl && ii > il);
+                    if (gt == up) {
+                        kv[i] = vl;
+                        kv[l] = vi;
+                        ki[i] = il;
+                        ki[l] = ii;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int i = lane; i < n; i += 64) a[i] = kv[i];
+    __syncthreads();
 }
 
 // stable bottom-up merge sort (partial_cmp semantics on NaN-free data)
@@ -197,15 +245,20 @@ __device__ bool seg_init(SegGen& g, const float* b, int n, float nominal) {
     return true;
 }
 
-// bayesian.rs:104-178; returns false on Err
+// bayesian.rs:104-178, all lanes (uniform arguments); returns false on Err.  Lane c
+// evaluates the c-th candidate tempo (cb advanced by c sequential +0.5 steps, exactly the
+// reference's loop variable) with the likelihood folded over the onsets in order; the winner
+// is the first candidate reaching the maximum (the reference's strict `lik > best`).
 __device__ bool bayes_update(float* cur_bpm, const float* on, int n, float* out_bpm) {
     if (n <= 0) return false;
     if (*cur_bpm <= EPS || *cur_bpm > 300.0f) return false;
+    const int lane = threadIdx.x & 63;
     const float lo = sd_maxf(*cur_bpm - 5.0f, 60.0f), hi = sd_minf(*cur_bpm + 5.0f, 180.0f);
-    float best_bpm = *cur_bpm, best_l = 0.0f;
     const float sig_sq = 0.05f * 0.05f;
-    for (float cb = lo; cb <= hi; cb += 0.5f) {
-        if (cb <= EPS) return false;
+    float cb = lo;
+    for (int k = 0; k < lane; k++) cb += 0.5f;
+    float lik = -1.0f;  // lanes past `hi` take no part
+    if (cb <= hi) {
         const float bi = 60.0f / cb;
         const float st0 = on[0];
         float ll = 0.0f;
@@ -218,11 +271,16 @@ __device__ bool bayes_update(float* cur_bpm, const float* on, int n, float* out_
             ll += -(d * d) / (2.0f * sig_sq);
             valid++;
         }
-        const float lik = valid == 0 ? 0.0f : sd_expf(ll / (float)valid);
-        if (lik > best_l) {
-            best_l = lik;
-            best_bpm = cb;
-        }
+        lik = valid == 0 ? 0.0f : sd_expf(ll / (float)valid);
+    }
+    // (lo >= 60 so the reference's `cb <= EPS -> Err` never fires; with 64 lanes and at most
+    // 21 candidates every candidate is covered)
+    const float m = wave_max(lik);
+    float best_bpm = *cur_bpm;
+    if (m > 0.0f) {
+        const unsigned long long bal = __ballot(lik == m);
+        const int w = __ffsll((long long)bal) - 1;
+        best_bpm = __shfl(cb, w, 64);
     }
     *cur_bpm = best_bpm;
     *out_bpm = best_bpm;
@@ -268,14 +326,21 @@ __device__ float score_ts(const float* b, int nb, int bpb, float mean, int n_iv)
     return sd_minf(ac * 0.7f + cons * 0.3f, 1.0f);
 }
 
-__global__ void k_beat(const int* __restrict__ tracks, int n_items, const uint32_t* __restrict__ onsets,
-                       const uint64_t* __restrict__ on_off, const int* __restrict__ on_n, uint32_t sr,
-                       const float* __restrict__ bpm_in, const float* __restrict__ conf_in,
-                       float* __restrict__ scratch, const uint64_t* __restrict__ beat_off,
-                       const int* __restrict__ beat_cap, float* __restrict__ beats, float* __restrict__ downs,
-                       BeatOut* __restrict__ out) {
-    const int it = blockIdx.x * blockDim.x + threadIdx.x;
-    if (it >= n_items) return;
+constexpr int BEAT_LDS_ON = 8192;   // onsets staged in LDS up to this count
+constexpr int BEAT_SORT_MAX = 2048;  // LDS bitonic sort capacity (larger: serial merge sort)
+
+__global__ __launch_bounds__(64) void k_beat(const int* __restrict__ tracks, int n_items,
+                                             const uint32_t* __restrict__ onsets, const uint64_t* __restrict__ on_off,
+                                             const int* __restrict__ on_n, uint32_t sr,
+                                             const float* __restrict__ bpm_in, const float* __restrict__ conf_in,
+                                             float* __restrict__ scratch, const uint64_t* __restrict__ beat_off,
+                                             const int* __restrict__ beat_cap, float* __restrict__ beats,
+                                             float* __restrict__ downs, BeatOut* __restrict__ out) {
+    __shared__ float s_on[BEAT_LDS_ON];
+    __shared__ float s_kv[BEAT_SORT_MAX];
+    __shared__ int s_ki[BEAT_SORT_MAX];
+    const int it = blockIdx.x;
+    const int lane = threadIdx.x;
     const int trk = tracks[it];
     BeatOut r{0, 0, 0.0f, 0};
     const float bpm = bpm_in[trk];
@@ -288,30 +353,37 @@ __global__ void k_beat(const int* __restrict__ tracks, int n_items, const uint32
     float* tmp = rb + cap;
     float* ob = beats + beat_off[trk];
     float* od = downs + beat_off[trk];
+    auto finish = [&]() {
+        if (lane == 0) out[trk] = r;
+    };
     int overflow = 0;
     if (!(bpm > 0.0f && n >= 2)) {  // src/lib.rs:913, 944-957
-        out[trk] = r;
+        finish();
         return;
     }
     if (bpm > 300.0f) {  // generate_beat_grid InvalidInput
-        out[trk] = r;
+        finish();
         return;
     }
     const uint32_t* os = onsets + on_off[trk];
-    for (int k = 0; k < n; k++) ons[k] = (float)os[k] / (float)sr;
+    float* onp = n <= BEAT_LDS_ON ? s_on : ons;
+    for (int k = lane; k < n; k += 64) onp[k] = (float)os[k] / (float)sr;
+    __syncthreads();
     // (already ascending; the reference's sort_by(partial_cmp) is a no-op here)
-    int nh = hmm_track(bpm, ons, n, hb, cap, &overflow);
+    int nh = hmm_track(bpm, onp, n, hb, cap, &overflow);
+    __syncthreads();
     if (nh <= 0 || overflow) {
         if (overflow) r.ok = -1;
-        out[trk] = r;
+        finish();
         return;
     }
     const float* fin = hb;
     int nfin = nh;
-    // tempo variations + Bayesian refinement (mod.rs:140-219)
+    // tempo variations + Bayesian refinement (mod.rs:140-219); every lane replays the segment
+    // generator identically (uniform control flow)
     SegGen g;
     if (!seg_init(g, hb, nh, bpm)) {
-        out[trk] = r;
+        finish();
         return;
     }
     bool any = false, has_var = false;
@@ -326,18 +398,19 @@ __global__ void k_beat(const int* __restrict__ tracks, int n_items, const uint32
         int nr = 0;
         while (seg_next(g, &s, &any)) {
             if (s.variable) {
-                const int i0 = lower_bound_f(ons, n, s.start);
-                const int i1 = upper_bound_f(ons, n, s.end);
+                const int i0 = lower_bound_f(onp, n, s.start);
+                const int i1 = upper_bound_f(onp, n, s.end);
                 if (i1 > i0) {
                     float ub;
-                    if (!bayes_update(&cur_bpm, ons + i0, i1 - i0, &ub)) {
-                        out[trk] = r;  // Err propagates -> empty grid
+                    if (!bayes_update(&cur_bpm, onp + i0, i1 - i0, &ub)) {
+                        finish();  // Err propagates -> empty grid
                         return;
                     }
-                    const int got = hmm_track(ub, ons + i0, i1 - i0, rb + nr, cap - nr, &overflow);
+                    const int got = hmm_track(ub, onp + i0, i1 - i0, rb + nr, cap - nr, &overflow);
+                    __syncthreads();
                     if (overflow) {
                         r.ok = -1;
-                        out[trk] = r;
+                        finish();
                         return;
                     }
                     if (got > 0) nr += got;
@@ -347,19 +420,28 @@ __global__ void k_beat(const int* __restrict__ tracks, int n_items, const uint32
                 const int j1 = upper_bound_f(hb, nh, s.end);
                 if (nr + (j1 - j0) > cap) {
                     r.ok = -1;
-                    out[trk] = r;
+                    finish();
                     return;
                 }
-                for (int k = j0; k < j1; k++) rb[nr++] = hb[k];
+                for (int k = j0 + lane; k < j1; k += 64) rb[nr + (k - j0)] = hb[k];
+                nr += j1 - j0;
+                __syncthreads();
             }
         }
         if (nr > 0) {
-            merge_sort_f(rb, tmp, nr);
+            int np2 = 1;
+            while (np2 < nr) np2 <<= 1;
+            if (np2 <= BEAT_SORT_MAX) {
+                wave_sort_stable(rb, nr, s_kv, s_ki, np2);
+            } else {
+                if (lane == 0) merge_sort_f(rb, tmp, nr);
+                __syncthreads();
+            }
             fin = rb;
             nfin = nr;
         }
     }
-    // time signature (time_signature.rs:90-149)
+    // time signature (time_signature.rs:90-149): lanes 0/1/2 score 4/4, 3/4, 6/8
     int bpb = 4;
     if (nfin >= 8) {
         float sum = 0.0f;
@@ -373,8 +455,9 @@ __global__ void k_beat(const int* __restrict__ tracks, int n_items, const uint32
         }
         if (niv > 0) {
             const float mean = sum / (float)niv;
-            const float s44 = score_ts(fin, nfin, 4, mean, niv), s34 = score_ts(fin, nfin, 3, mean, niv),
-                        s68 = score_ts(fin, nfin, 6, mean, niv);
+            float sc = 0.0f;
+            if (lane < 3) sc = score_ts(fin, nfin, lane == 0 ? 4 : lane == 1 ? 3 : 6, mean, niv);
+            const float s44 = __shfl(sc, 0, 64), s34 = __shfl(sc, 1, 64), s68 = __shfl(sc, 2, 64);
             float bs = s44;
             if (!(s34 < bs)) {
                 bpb = 3;
@@ -387,57 +470,59 @@ __global__ void k_beat(const int* __restrict__ tracks, int n_items, const uint32
         }
     }
     // beats + downbeats (mod.rs:290-404)
-    for (int k = 0; k < nfin; k++) ob[k] = fin[k];
-    const float bi = 60.0f / bpm;
-    const float bar = bi * (float)bpb;
-    const float tolb = bar * 0.1f;
+    for (int k = lane; k < nfin; k += 64) ob[k] = fin[k];
     int nd = 0;
-    od[nd++] = fin[0];
-    for (int k = 1; k < nfin; k++) {
-        const float et = od[nd - 1] + bar;
-        if (sd_absf(fin[k] - et) <= tolb) od[nd++] = fin[k];
-    }
-    // stability (mod.rs:425-485)
-    float stab = 0.0f;
-    if (nfin >= 2) {
-        float sum = 0.0f;
-        int niv = 0;
+    if (lane == 0) {
+        const float bi = 60.0f / bpm;
+        const float bar = bi * (float)bpb;
+        const float tolb = bar * 0.1f;
+        od[nd++] = fin[0];
         for (int k = 1; k < nfin; k++) {
-            const float d = fin[k] - fin[k - 1];
-            if (d > 0.0f) {
-                sum += d;
-                niv++;
-            }
+            const float et = od[nd - 1] + bar;
+            if (sd_absf(fin[k] - et) <= tolb) od[nd++] = fin[k];
         }
-        if (niv > 0) {
-            const float mean = sum / (float)niv;
-            if (mean > 1e-10f) {
-                float vs = 0.0f;
-                for (int k = 1; k < nfin; k++) {
-                    const float d = fin[k] - fin[k - 1];
-                    if (d > 0.0f) {
-                        const float dd = d - mean;
-                        vs += dd * dd;
-                    }
+        // stability (mod.rs:425-485)
+        float stab = 0.0f;
+        if (nfin >= 2) {
+            float sum = 0.0f;
+            int niv = 0;
+            for (int k = 1; k < nfin; k++) {
+                const float d = fin[k] - fin[k - 1];
+                if (d > 0.0f) {
+                    sum += d;
+                    niv++;
                 }
-                const float var = vs / (float)niv;
-                const float cv = __builtin_sqrtf(var) / mean;
-                stab = 1.0f / (1.0f + cv);
+            }
+            if (niv > 0) {
+                const float mean = sum / (float)niv;
+                if (mean > 1e-10f) {
+                    float vs = 0.0f;
+                    for (int k = 1; k < nfin; k++) {
+                        const float d = fin[k] - fin[k - 1];
+                        if (d > 0.0f) {
+                            const float dd = d - mean;
+                            vs += dd * dd;
+                        }
+                    }
+                    const float var = vs / (float)niv;
+                    const float cv = __builtin_sqrtf(var) / mean;
+                    stab = 1.0f / (1.0f + cv);
+                }
             }
         }
+        r.n_beats = nfin;
+        r.n_down = nd;
+        r.stability = stab;
+        r.ok = 1;
+        out[trk] = r;
     }
-    r.n_beats = nfin;
-    r.n_down = nd;
-    r.stability = stab;
-    r.ok = 1;
-    out[trk] = r;
 }
 
 void launch_beat(const int* tracks, int n_items, const uint32_t* onsets, const uint64_t* on_off, const int* on_n,
                  uint32_t sr, const float* bpm, const float* conf, float* scratch, const uint64_t* beat_off,
                  const int* beat_cap, float* beats, float* downs, BeatOut* out, hipStream_t st) {
     if (n_items == 0) return;
-    hipLaunchKernelGGL(k_beat, dim3((n_items + 63) / 64), dim3(64), 0, st, tracks, n_items, onsets, on_off, on_n, sr,
+    hipLaunchKernelGGL(k_beat, dim3(n_items), dim3(64), 0, st, tracks, n_items, onsets, on_off, on_n, sr,
                        bpm, conf, scratch, beat_off, beat_cap, beats, downs, out);
 }
 

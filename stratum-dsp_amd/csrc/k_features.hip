@@ -144,14 +144,14 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const float* __restrict_
                 const float mp = Mt[i][s];
                 const float pv = pn ? mp / mx_p : 0.0f;
                 const float cv = cn ? m / mx_c : 0.0f;
-                const float d = sd_maxf(cv - pv, 0.0f);
+                const float d = max_bnn(cv - pv, 0.0f);
                 so += d * d;
                 // SuperFlux, full band window [b-K, b+K] clipped to [0, B)
                 const int lo = b - K < 0 ? 0 : b - K;
                 const int hi = b + K + 1 < B ? b + K + 1 : B;
                 float pm = 0.0f;
-                for (int q = lo; q < hi; q++) pm = sd_maxf(pm, Lt[i][q & (W - 1)]);
-                const float df = sd_maxf(lc - pm, 0.0f);
+                for (int q = lo; q < hi; q++) pm = max_bnn(pm, Lt[i][q & (W - 1)]);  // L is never NaN
+                const float df = max_bnn(lc - pm, 0.0f);
                 sx[0] += df * df;
 #pragma unroll
                 for (int v = 1; v < 4; v++) {
@@ -161,9 +161,9 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const float* __restrict_
                             const int lb = lo < P.bs[v] ? P.bs[v] : lo;
                             const int hb = hi > P.be[v] ? P.be[v] : hi;
                             pmb = 0.0f;
-                            for (int q = lb; q < hb; q++) pmb = sd_maxf(pmb, Lt[i][q & (W - 1)]);
+                            for (int q = lb; q < hb; q++) pmb = max_bnn(pmb, Lt[i][q & (W - 1)]);
                         }
-                        const float db = sd_maxf(lc - pmb, 0.0f);
+                        const float db = max_bnn(lc - pmb, 0.0f);
                         sx[v] += db * db;
                     }
                 }

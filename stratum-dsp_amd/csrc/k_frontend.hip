@@ -116,50 +116,58 @@ __global__ __launch_bounds__(RMS_ROWS) void k_frame_rms(const float* __restrict_
     if (g < total) rms[g] = len > 0 ? __builtin_sqrtf(sum / (float)len) : 0.0f;
 }
 
-// Silence regions and trim bounds, one thread per track (silence.rs:171-263).
-__global__ void k_trim(const float* __restrict__ rms, const uint64_t* __restrict__ frame_pfx, int T,
-                       const uint64_t* __restrict__ n_raw, int hop, float thr, uint64_t min_frames, int enable,
-                       uint64_t* __restrict__ trim_start, uint64_t* __restrict__ trim_end) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= T) return;
+// Silence regions and trim bounds (silence.rs:171-279), one workgroup per track.  Only two
+// regions can move the trim: the run of silent frames starting at frame 0 (always kept, its
+// end becomes the trim start) and the run reaching the last frame (kept when at least
+// min_frames long or starting at 0; its start becomes the trim end).  Both follow from the
+// first and the last non-silent frame, found by an order-free min/max reduction.
+__global__ __launch_bounds__(256) void k_trim(const float* __restrict__ rms, const uint64_t* __restrict__ frame_pfx,
+                                              int T, const uint64_t* __restrict__ n_raw, int hop, float thr,
+                                              uint64_t min_frames, int enable, uint64_t* __restrict__ trim_start,
+                                              uint64_t* __restrict__ trim_end) {
+    __shared__ long long red_lo[4], red_hi[4];
+    const int t = blockIdx.x;
     const uint64_t n = n_raw[t];
     if (!enable || n == 0) {
-        trim_start[t] = 0;
-        trim_end[t] = n;
+        if (threadIdx.x == 0) {
+            trim_start[t] = 0;
+            trim_end[t] = n;
+        }
         return;
     }
-    const uint64_t nf = frame_pfx[t + 1] - frame_pfx[t];
+    const int64_t nf = (int64_t)(frame_pfx[t + 1] - frame_pfx[t]);
     const float* r = rms + frame_pfx[t];
-    // Only the first region (if it starts at sample 0) and the last region (if it reaches the
-    // end) influence the trim; track both while replaying the reference's region scan.
-    bool have_first = false, have_last = false;
-    uint64_t first_s = 0, first_e = 0, last_s = 0, last_e = 0;
-    bool in_sil = false;
-    uint64_t ss = 0;
-    auto push = [&](uint64_t s, uint64_t e) {
-        if (!have_first) {
-            have_first = true;
-            first_s = s;
-            first_e = e;
+    long long lo = nf, hi = -1;  // first / last non-silent frame
+    for (int64_t f = threadIdx.x; f < nf; f += blockDim.x)
+        if (!(r[f] <= thr)) {
+            lo = lo < f ? lo : f;
+            hi = hi > f ? hi : f;
         }
-        have_last = true;
-        last_s = s;
-        last_e = e;
-    };
-    for (uint64_t f = 0; f < nf; f++) {
-        const bool sil = r[f] <= thr;
-        if (sil && !in_sil) {
-            in_sil = true;
-            ss = f;
-        } else if (!sil && in_sil) {
-            in_sil = false;
-            if (f - ss >= min_frames || ss == 0 || f == nf) push(ss * (uint64_t)hop, f < nf ? f * (uint64_t)hop : n);
-        }
+    for (int o = 32; o > 0; o >>= 1) {
+        const long long l2 = __shfl_xor(lo, o, 64), h2 = __shfl_xor(hi, o, 64);
+        lo = lo < l2 ? lo : l2;
+        hi = hi > h2 ? hi : h2;
     }
-    if (in_sil && (nf - ss >= min_frames || ss == 0)) push(ss * (uint64_t)hop, n);
+    if ((threadIdx.x & 63) == 0) {
+        red_lo[threadIdx.x >> 6] = lo;
+        red_hi[threadIdx.x >> 6] = hi;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    for (int w = 1; w < (int)(blockDim.x >> 6); w++) {
+        lo = red_lo[0] < red_lo[w] ? red_lo[0] : red_lo[w];
+        red_lo[0] = lo;
+        hi = red_hi[0] > red_hi[w] ? red_hi[0] : red_hi[w];
+        red_hi[0] = hi;
+    }
+    lo = red_lo[0];
+    hi = red_hi[0];
     uint64_t ts = 0, te = n;
-    if (have_first && first_s == 0) ts = first_e;
-    if (have_last && last_e == n) te = last_s;
+    if (nf > 0 && lo > 0) ts = lo < nf ? (uint64_t)lo * (uint64_t)hop : n;  // frame 0 silent
+    if (nf > 0 && hi < nf - 1) {                                             // last frame silent
+        const uint64_t ss = (uint64_t)(hi + 1);
+        if ((uint64_t)nf - ss >= min_frames || ss == 0) te = ss * (uint64_t)hop;
+    }
     if (ts > te) ts = te;
     if (te < ts) te = ts;
     if (!(ts < te && te <= n)) ts = te = 0;
@@ -274,82 +282,148 @@ __global__ __launch_bounds__(256) void k_flux_onsets(const float* __restrict__ s
     if (threadIdx.x == 0) on_n[trk] = base;
 }
 
-// Onset consensus (consensus.rs:111-287) + selection (src/lib.rs:258-290), one thread per track.
-// Onsets arrive sorted, so a new cluster is only ever created once every earlier cluster is
-// out of reach; "join the first cluster with any member within tol" reduces to comparing
-// against the newest cluster's largest member.  Clusters are therefore disjoint and their
-// integer centres strictly increasing.
-__global__ void k_consensus(const uint32_t* __restrict__ energy, const uint64_t* __restrict__ e_off,
-                            const int* __restrict__ e_n, const uint32_t* __restrict__ flux_on,
-                            const uint64_t* __restrict__ f_off, const int* __restrict__ f_n, uint64_t kind_stride,
-                            int T, uint32_t tol, int enable, const int* __restrict__ has_mags,
-                            uint32_t* __restrict__ chosen, const uint64_t* __restrict__ c_off,
-                            int* __restrict__ c_n) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= T) return;
+// Onset consensus (consensus.rs:111-287) + selection (src/lib.rs:258-290), one workgroup per
+// track.  The reference merges the three sorted lists (stable: energy, spectral, HFC on equal
+// samples) and joins each onset to the first cluster with a member within tol.  Onsets arrive
+// sorted, so a new cluster is only ever created once every earlier cluster is out of reach:
+// joining reduces to comparing against the newest cluster's largest member, i.e. a new
+// cluster starts wherever the gap to the previous merged onset exceeds tol.  Every cluster is
+// a maximal run of the merged order (and the integer centres strictly increase), so it
+// parallelises exactly: merged positions by rank (binary searches), cluster starts by
+// ordered compaction, integer sums per cluster, then the strong (>= 2 methods) centres, or
+// all centres when none is strong, or the energy onsets when nothing clustered.
+// scr: 5 * (3F) uint32 per track at scr_off (merged value, method, cluster start, centre, strong).
+__device__ inline int lb_u32(const uint32_t* a, int n, uint32_t x) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (a[mid] < x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+__device__ inline int ub_u32(const uint32_t* a, int n, uint32_t x) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (!(x < a[mid])) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(256) void k_consensus(const uint32_t* __restrict__ energy,
+                                                   const uint64_t* __restrict__ e_off, const int* __restrict__ e_n,
+                                                   const uint32_t* __restrict__ flux_on,
+                                                   const uint64_t* __restrict__ f_off, const int* __restrict__ f_n,
+                                                   uint64_t kind_stride, int T, uint32_t tol, int enable,
+                                                   const int* __restrict__ has_mags, uint32_t* __restrict__ chosen,
+                                                   const uint64_t* __restrict__ c_off, int* __restrict__ c_n,
+                                                   uint32_t* __restrict__ scr) {
+    __shared__ int red[8];
+    const int t = blockIdx.x;
+    const int tid = threadIdx.x;
     const uint32_t* L0 = energy + e_off[t];
     const int n0 = e_n[t];
     uint32_t* out = chosen + c_off[t];
+    auto keep_energy = [&]() {
+        for (int i = tid; i < n0; i += blockDim.x) out[i] = L0[i];
+        if (tid == 0) c_n[t] = n0;
+    };
     if (!enable || !has_mags[t]) {
-        for (int i = 0; i < n0; i++) out[i] = L0[i];
-        c_n[t] = n0;
+        keep_energy();
         return;
     }
     const uint32_t* L1 = flux_on + f_off[t];
     const uint32_t* L2 = flux_on + f_off[t] + kind_stride;
     const int n1 = f_n[t], n2 = f_n[T + t];
-    int i0 = 0, i1 = 0, i2 = 0;
-    // current cluster state
-    bool have = false;
-    uint64_t sum = 0, cnt = 0;
-    uint32_t cmax = 0;
-    int voted = 0;
-    int ns = 0;  // strong (>= 2 methods) written from the front
-    // pass 1 writes strong centres; remember whether any strong exists, else pass 2 writes all
-    auto flush = [&](bool strong_pass) {
-        if (!have) return;
-        const uint32_t centre = (uint32_t)(sum / cnt);
-        const int vb = __popc(voted);
-        if (!strong_pass || vb >= 2) {
-            if (ns == 0 || out[ns - 1] != centre) out[ns++] = centre;
+    const int N = n0 + n1 + n2;
+    const uint64_t cap = (uint64_t)N > 0 ? (uint64_t)N : 1;
+    uint32_t* mv = scr + c_off[t] * 5;  // c_off = 3 * frame offset: 3F slots per array
+    uint32_t* mm = mv + cap;
+    uint32_t* cs = mm + cap;
+    uint32_t* cc = cs + cap;
+    uint32_t* sg = cc + cap;
+    // merged order by rank
+    for (int e = tid; e < N; e += blockDim.x) {
+        int a, i;
+        uint32_t s;
+        if (e < n0) {
+            a = 0;
+            i = e;
+            s = L0[i];
+        } else if (e < n0 + n1) {
+            a = 1;
+            i = e - n0;
+            s = L1[i];
+        } else {
+            a = 2;
+            i = e - n0 - n1;
+            s = L2[i];
         }
-    };
-    for (int pass = 0; pass < 2; pass++) {
-        i0 = i1 = i2 = 0;
-        have = false;
-        ns = 0;
-        while (i0 < n0 || i1 < n1 || i2 < n2) {
-            // stable merge by sample: energy, spectral, hfc order on ties (sort_by_key is stable)
-            uint32_t s = 0xffffffffu;
-            int m = -1;
-            if (i0 < n0 && L0[i0] < s) s = L0[i0], m = 0;
-            if (i1 < n1 && L1[i1] < s) s = L1[i1], m = 1;
-            if (i2 < n2 && L2[i2] < s) s = L2[i2], m = 2;
-            if (m == 0) i0++;
-            else if (m == 1) i1++;
-            else i2++;
-            if (have && (uint64_t)(s - cmax) <= (uint64_t)tol) {
-                sum += s;
-                cnt++;
-                cmax = s;
-                voted |= 1 << m;
-            } else {
-                flush(pass == 0);
-                have = true;
-                sum = s;
-                cnt = 1;
-                cmax = s;
-                voted = 1 << m;
-            }
+        int pos = i;
+        pos += a == 0 ? 0 : ub_u32(L0, n0, s);  // earlier lists win ties
+        pos += a == 1 ? 0 : (a < 1 ? lb_u32(L1, n1, s) : ub_u32(L1, n1, s));
+        pos += a == 2 ? 0 : lb_u32(L2, n2, s);
+        mv[pos] = s;
+        mm[pos] = (uint32_t)a;
+    }
+    __syncthreads();
+    // cluster starts, in order
+    int C = 0;
+    for (int p0 = 0; p0 < N; p0 += blockDim.x) {
+        const int p = p0 + tid;
+        const bool st = p < N && (p == 0 || (uint64_t)(mv[p] - mv[p - 1]) > (uint64_t)tol);
+        int tot;
+        const int slot = block_exclusive_flag(st, red, &tot);
+        if (st) cs[C + slot] = (uint32_t)p;
+        C += tot;
+    }
+    __syncthreads();
+    // per-cluster centre and vote
+    for (int c = tid; c < C; c += blockDim.x) {
+        const int b = (int)cs[c], e = c + 1 < C ? (int)cs[c + 1] : N;
+        uint64_t sum = 0;
+        int voted = 0;
+        for (int p = b; p < e; p++) {
+            sum += mv[p];
+            voted |= 1 << mm[p];
         }
-        flush(pass == 0);
-        if (pass == 0 && ns > 0) break;  // strong set non-empty
+        cc[c] = (uint32_t)(sum / (uint64_t)(e - b));
+        sg[c] = __popc(voted) >= 2;
+    }
+    __syncthreads();
+    // pass 1: strong centres, consecutive duplicates dropped
+    int K = 0;
+    for (int c0 = 0; c0 < C; c0 += blockDim.x) {
+        const int c = c0 + tid;
+        const bool f = c < C && sg[c];
+        int tot;
+        const int slot = block_exclusive_flag(f, red, &tot);
+        if (f) mv[K + slot] = cc[c];  // mv is free now
+        K += tot;
+    }
+    __syncthreads();
+    const uint32_t* src = mv;
+    int S = K;
+    if (K == 0) {  // no strong cluster: every centre
+        src = cc;
+        S = C;
+    }
+    int ns = 0;
+    for (int k0 = 0; k0 < S; k0 += blockDim.x) {
+        const int k = k0 + tid;
+        const bool f = k < S && (k == 0 || src[k] != src[k - 1]);
+        int tot;
+        const int slot = block_exclusive_flag(f, red, &tot);
+        if (f) out[ns + slot] = src[k];
+        ns += tot;
     }
     if (ns == 0) {  // nothing clustered: keep the energy-flux onsets (lib.rs:283-285)
-        for (int i = 0; i < n0; i++) out[i] = L0[i];
-        ns = n0;
+        keep_energy();
+        return;
     }
-    c_n[t] = ns;
+    if (tid == 0) c_n[t] = ns;
 }
 
 // ---- launchers ----
@@ -370,7 +444,7 @@ void launch_frame_rms(const float* x, const uint64_t* src_off, const float* gain
 void launch_trim(const float* rms, const uint64_t* frame_pfx, int T, const uint64_t* n_raw, int hop, float thr,
                  uint64_t min_frames, int enable, uint64_t* trim_start, uint64_t* trim_end, hipStream_t st) {
     if (T == 0) return;
-    hipLaunchKernelGGL(k_trim, dim3((T + 63) / 64), dim3(64), 0, st, rms, frame_pfx, T, n_raw, hop, thr, min_frames,
+    hipLaunchKernelGGL(k_trim, dim3(T), dim3(256), 0, st, rms, frame_pfx, T, n_raw, hop, thr, min_frames,
                        enable, trim_start, trim_end);
 }
 void launch_energy_onsets(const float* rms, const uint64_t* frame_pfx, const uint64_t* n_trim, int hop, float factor,
@@ -388,10 +462,11 @@ void launch_flux_onsets(const float* sfo, const float* hfc, float* scratch, cons
 }
 void launch_consensus(const uint32_t* energy, const uint64_t* e_off, const int* e_n, const uint32_t* flux_on,
                       const uint64_t* f_off, const int* f_n, uint64_t kind_stride, int T, uint32_t tol, int enable,
-                      const int* has_mags, uint32_t* chosen, const uint64_t* c_off, int* c_n, hipStream_t st) {
+                      const int* has_mags, uint32_t* chosen, const uint64_t* c_off, int* c_n, uint32_t* scratch,
+                      hipStream_t st) {
     if (T == 0) return;
-    hipLaunchKernelGGL(k_consensus, dim3((T + 63) / 64), dim3(64), 0, st, energy, e_off, e_n, flux_on, f_off, f_n,
-                       kind_stride, T, tol, enable, has_mags, chosen, c_off, c_n);
+    hipLaunchKernelGGL(k_consensus, dim3(T), dim3(256), 0, st, energy, e_off, e_n, flux_on, f_off, f_n, kind_stride, T,
+                       tol, enable, has_mags, chosen, c_off, c_n, scratch);
 }
 
 }  // namespace sdsp

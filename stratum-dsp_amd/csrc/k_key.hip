@@ -79,9 +79,9 @@ __global__ __launch_bounds__(MASK_T) void k_mask(float* __restrict__ mags, int s
             const float x_raw = M == 0 ? xv[u] : raw[xr * MASK_T];
             // margin 0: smooth_spectrogram_time returns its input unchanged (extractor.rs:1250-1252)
             const float hm = M == 0 ? x_raw : (pre[w_slot * MASK_T] - pre[s_slot * MASK_T]) / denom;
-            const float x = sd_maxf(x_raw, 0.0f);
-            const float h = sd_maxf(hm, 0.0f);
-            const float r = sd_maxf(x - h, 0.0f);
+            const float x = max_bnn(x_raw, 0.0f);
+            const float h = max_bnn(hm, 0.0f);
+            const float r = max_bnn(x - h, 0.0f);
             const float hp = mask_pow<PW>(h, p);
             const float rp = mask_pow<PW>(r, p);
             const float m = hp / (hp + rp + eps);
@@ -135,9 +135,9 @@ __global__ __launch_bounds__(MASK_T) void k_mask_r(float* __restrict__ mags, int
                 const int64_t en = t + M + 1 < F ? t + M + 1 : F;
                 const float denom = (float)(en - st > 1 ? en - st : 1);
                 const float hm = (P[(u + 1) % R] - P[(u + R - 2 * M) % R]) / denom;
-                const float x = sd_maxf(X[(u + 1) % RX], 0.0f);
-                const float h = sd_maxf(hm, 0.0f);
-                const float r = sd_maxf(x - h, 0.0f);
+                const float x = max_bnn(X[(u + 1) % RX], 0.0f);
+                const float h = max_bnn(hm, 0.0f);
+                const float r = max_bnn(x - h, 0.0f);
                 const float hp = mask_pow<PW>(h, p);
                 const float rp = mask_pow<PW>(r, p);
                 const float m = hp / (hp + rp + eps);
@@ -409,11 +409,9 @@ __global__ __launch_bounds__(256) void k_key_vote(const int* __restrict__ tracks
         }
         const int used = block_sum_i(used_local, redi);
         __syncthreads();
-        if (threadIdx.x == 0) {
-            float sw = 0.0f;
-            for (int64_t f = 0; f < F; f++) sw += w[f];
-            use_w_s = !(sw <= 1e-12f || used < 10);
-        }
+        __shared__ float sbuf[SEQ_CH];
+        const float sw = block_seq_sum(w, F, sbuf);  // weights.iter().sum(), in order
+        if (threadIdx.x == 0) use_w_s = !(sw <= 1e-12f || used < 10);
     } else if (threadIdx.x == 0) {
         use_w_s = 0;
     }

@@ -384,6 +384,7 @@ __global__ __launch_bounds__(256) void k_tempo_select(const int* __restrict__ ac
 // One 64-lane wave per track: lane 0 runs the decision logic; beat_contrast_score's phase
 // loop is spread over the lanes (each phase's sums stay sequential; the max over phases is
 // order-free).
+constexpr int MR_CAP_LDS = 256;
 struct CandList {
     const float* c;  // 4 floats per candidate: bpm, score, fft_norm, ac_norm
     int n;
@@ -401,22 +402,15 @@ __device__ float lookup_c(CandList L, float bpm, float tol) {
     return bs;
 }
 
-__device__ float beat_contrast_wave(const float* nov, int n, int sr, int hop, float bpm, float* red) {
+// nov_total: novelty.iter().sum() (sequential), computed once per track by the caller
+__device__ float beat_contrast_wave(const float* nov, int n, int sr, int hop, float bpm, float nov_total) {
     if (n < 16 || !(sd_isfinite_f(bpm) && bpm > 0.0f) || sr == 0 || hop == 0) return 0.0f;
     const float fpb = (60.0f * (float)sr) / (bpm * (float)hop);
     if (!sd_isfinite_f(fpb) || fpb < 3.0f) return 0.0f;
     const int64_t pi = sd_f2i64(sd_roundf(fpb));
     if (!(pi >= 3 && pi <= 512)) return 0.0f;
     const int period = (int)pi, w = 2;
-    // total = novelty.iter().sum() (sequential), lane 0
-    float total = 0.0f;
-    if (threadIdx.x == 0) {
-        for (int i = 0; i < n; i++) total += nov[i];
-        red[0] = total;
-    }
-    __syncthreads();
-    total = sd_maxf(red[0], 1e-6f);
-    __syncthreads();
+    const float total = sd_maxf(nov_total, 1e-6f);
     auto wmax = [&](int i) {
         const int s = i >= w ? i - w : 0, e = i + w + 1 < n ? i + w + 1 : n;
         float mx = 0.0f;
@@ -467,7 +461,6 @@ __global__ __launch_bounds__(64) void k_multires(const int* __restrict__ tracks,
                                                  const float* __restrict__ nov512, const uint64_t* __restrict__ fpfx512,
                                                  MrParams P, TempoEst* __restrict__ mr_est, int* __restrict__ used,
                                                  float* __restrict__ final_bpm, float* __restrict__ final_conf) {
-    __shared__ float red[4];
     __shared__ float fam_bpm[5], fam_sup[5], fam_align[5];
     __shared__ int n_fam_s, do_fam_s;
     __shared__ float best_bpm_s, best_score_s, second_s;
@@ -481,9 +474,20 @@ __global__ __launch_bounds__(64) void k_multires(const int* __restrict__ tracks,
         }
         return;
     }
+    // candidate lists staged in LDS when they fit (lane 0's lookups are latency-bound)
+    __shared__ float s_c[3][4 * MR_CAP_LDS];
     CandList L256{c256 + (uint64_t)i * cap256 * 4, n256[i]};
     CandList L512{c512 + (uint64_t)trk * cap512 * 4, n512[trk]};
     CandList L1024{c1024 + (uint64_t)i * cap1024 * 4, n1024[i]};
+    CandList* Ls[3] = {&L256, &L512, &L1024};
+    for (int l = 0; l < 3; l++) {
+        CandList& L = *Ls[l];
+        if (L.n <= MR_CAP_LDS) {
+            for (int k = threadIdx.x; k < 4 * L.n; k += blockDim.x) s_c[l][k] = L.c[k];
+            L.c = s_c[l];
+        }
+    }
+    __syncthreads();
     const float tol = P.tol;
     if (threadIdx.x == 0) {
         ok_s = 0;
@@ -631,9 +635,11 @@ __global__ __launch_bounds__(64) void k_multires(const int* __restrict__ tracks,
     const uint64_t g0 = fpfx512[trk];
     const int nn = (int)(fpfx512[trk + 1] - g0) - 1;
     const float* nov = nov512 + g0;
+    __shared__ float sbuf[SEQ_CH];
+    const float nov_total = (nf >= 2 && nn > 0) ? block_seq_sum(nov, nn, sbuf) : 0.0f;
     if (nf >= 2 && nn > 0) {
         for (int k = 0; k < nf; k++) {
-            const float a = beat_contrast_wave(nov, nn, P.sr, P.hop512, fam_bpm[k], red);
+            const float a = beat_contrast_wave(nov, nn, P.sr, P.hop512, fam_bpm[k], nov_total);
             if (threadIdx.x == 0) fam_align[k] = a;
             __syncthreads();
         }
@@ -667,7 +673,7 @@ __global__ __launch_bounds__(64) void k_multires(const int* __restrict__ tracks,
     }
     __syncthreads();
     if (do_fam_s) {
-        cur_align = beat_contrast_wave(nov, nn, P.sr, P.hop512, best_bpm_s, red);
+        cur_align = beat_contrast_wave(nov, nn, P.sr, P.hop512, best_bpm_s, nov_total);
         if (threadIdx.x == 0) {
             if (sd_absf(fam_bpm[4] - best_bpm_s) > 0.75f && fam_align[4] >= cur_align + 0.40f) {
                 best_bpm_s = fam_bpm[4];

@@ -130,7 +130,8 @@ void launch_flux_onsets(const float* sfo, const float* hfc, float* scratch, cons
                         int* out_n, int T, hipStream_t st);
 void launch_consensus(const uint32_t* energy, const uint64_t* e_off, const int* e_n, const uint32_t* flux_on,
                       const uint64_t* f_off, const int* f_n, uint64_t kind_stride, int T, uint32_t tol, int enable,
-                      const int* has_mags, uint32_t* chosen, const uint64_t* c_off, int* c_n, hipStream_t st);
+                      const int* has_mags, uint32_t* chosen, const uint64_t* c_off, int* c_n, uint32_t* scratch,
+                      hipStream_t st);
 void launch_features(const float* mags, const float* fmax, const uint64_t* frame_pfx, const uint64_t* tile_pfx,
                      int T, uint64_t n_tiles, const FeatParams& P, const MelPlan* mel, float* E, float* H, float* SFX,
                      float* SFO, float* MEL, uint64_t total, hipStream_t st);

@@ -889,8 +889,9 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     bool cons_ok = cfg_.enable_onset_consensus && cfg_.onset_consensus_tolerance_ms > 0;
     for (int k = 0; k < 4; k++) cons_ok = cons_ok && !(cfg_.onset_consensus_weights[k] < 0.0f);
     const uint32_t tol = (uint32_t)sd_f2u64((float)cfg_.onset_consensus_tolerance_ms / 1000.0f * (float)sr_);
+    uint32_t* d_cscr = c_.dev<uint32_t>("B.cscr", 15 * std::max<uint64_t>(bo.total, 1));
     launch_consensus(d_eon, bo.d_fpfx, d_en, d_fon, bo.d_fpfx, d_fn, bo.total, NR, tol, cons_ok, d_hm, d_chosen, d_coff,
-                     d_cn, st);
+                     d_cn, d_cscr, st);
     SDSP_HIP_CHECK(hipGetLastError());
     std::vector<TempoEst> best = c_.down(bo.est, (size_t)NR);
     std::vector<int> en_h = c_.down(d_en, (size_t)NR);

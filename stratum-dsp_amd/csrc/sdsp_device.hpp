@@ -36,6 +36,10 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
     return x < rem ? x * (per + 1) + l : rem * (per + 1) + (x - rem) * per + l;
 }
 
+// sd_maxf(a, b) for a second operand that is never NaN (a may be): identical result, without
+// the NaN tests (sd_maxf(NaN, b) = b = (NaN > b ? NaN : b)).
+__device__ __forceinline__ float max_bnn(float a, float b) { return a > b ? a : b; }
+
 // ---- wave / block reductions (order-free ops only: max, min, integer sums) ----
 __device__ __forceinline__ float wave_max(float v) {
     for (int o = 32; o > 0; o >>= 1) v = sd_maxf(v, __shfl_xor(v, o, 64));

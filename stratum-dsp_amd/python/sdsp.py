@@ -125,9 +125,40 @@ def analyze_batch(tracks, sample_rate=44100, config=None, device_mask=0):
     return res
 
 
-def analyze_batch_device(d_ptr, offsets, lens, sample_rate=44100, config=None, device=0, stream=None,
-                         keep_raw=False):
-    """Tracks already resident in HBM (d_ptr: device address).  Returns results (dicts)."""
+class ResultBatch:
+    """The C-ABI result array of one batch call, kept as native structs (no per-track Python
+    objects are built until asked for).  Index it for AnalysisResult dicts / AnalysisError."""
+
+    def __init__(self, outs, n):
+        self._outs = outs
+        self.n = n
+        self.status = [outs[i].status for i in range(n)]
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, i):
+        o = self._outs[i]
+        if o.status != 0:
+            return AnalysisError(o.status, o.error_message.decode())
+        return result_to_dict(o)
+
+    def free(self):
+        if self._outs is not None:
+            for i in range(self.n):
+                lib().sdsp_result_free(C.byref(self._outs[i]))
+            self._outs = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def analyze_batch_device(d_ptr, offsets, lens, sample_rate=44100, config=None, device=0, stream=None, raw=False):
+    """Tracks already resident in HBM (d_ptr: device address).  Returns a list of results
+    (dicts / AnalysisError), or with raw=True the native ResultBatch."""
     offs = np.ascontiguousarray(offsets, dtype=np.uint64)
     ln = np.ascontiguousarray(lens, dtype=np.uint64)
     n = ln.size
@@ -138,13 +169,11 @@ def analyze_batch_device(d_ptr, offsets, lens, sample_rate=44100, config=None, d
                                          device, C.c_void_p(stream or 0), outs)
     if st != 0:
         raise AnalysisError(st, "device batch failed")
-    res = []
-    for i in range(n):
-        if outs[i].status != 0:
-            res.append(AnalysisError(outs[i].status, outs[i].error_message.decode()))
-        else:
-            res.append(result_to_dict(outs[i]))
-        lib().sdsp_result_free(C.byref(outs[i]))
+    batch = ResultBatch(outs, n)
+    if raw:
+        return batch
+    res = [batch[i] for i in range(n)]
+    batch.free()
     return res
 
 
