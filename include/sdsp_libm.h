@@ -28,6 +28,8 @@
 #include <stdint.h>
 #include <stddef.h>
 
+#include "sdsp_logtab.h"
+
 #if defined(__HIPCC__) || defined(__HIP__)
 #define SD_HD __host__ __device__ inline
 #else
@@ -174,12 +176,62 @@ SD_HD double sd_cos_d(double x) {
 /* ---- f32 entry points (the Rust f32 method each one stands in for) ---- */
 
 /* f32::ln */
+/*
+ * f32::ln.  Table-driven (the hot transcendental: ln(1 + |X|) for every spectrogram bin):
+ * x = 2^e * m, m in [1, 2); the top 7 mantissa bits i pick a centre c (m in [c, c + 2^-7)
+ * for i < 53, else m/2 in (c - 2^-8, c] with e + 1, so that ln never cancels near x = 1);
+ * r = (m - c) * (1/c) with m - c exact, |r| < 2^-7; ln x = e ln2 + ln c + log1p(r), log1p by
+ * its degree-8 Taylor polynomial (truncation < 2^-66).  Double arithmetic with explicit
+ * fma (IEEE on both x86-64-v3 and gfx950); {c, 1/c, ln c} from include/sdsp_logtab.h
+ * (correctly rounded, tools/gen_logtab.py).  Exhaustive check (tools/check_logf.c, all
+ * 2^31 positive finite f32): bit-identical to the double atanh series (float)sd_log_d(x) on
+ * every input, and correctly rounded on all but 5 inputs that lie within ~1e-16 (relative)
+ * of a rounding midpoint (0x3c413d3a, 0x41178feb, 0x4c5d65a5, 0x65d890d3, 0x6f31a8ec).
+ */
+typedef struct {
+    double c, inv, lg;
+} sd_logtab_t;
+#if defined(__HIPCC__) || defined(__HIP__)
+static __constant__ const sd_logtab_t SD_LOGTAB_D[128] = SDSP_LOGTAB_INIT;
+#endif
+static const sd_logtab_t SD_LOGTAB_H[128] = SDSP_LOGTAB_INIT;
+
 SD_HD float sd_logf(float x) {
     if (x != x) return x;
     if (x < 0.0f) return SD_NAN_F;
     if (x == 0.0f) return -SD_INF_F;
     if (!sd_isfinite_f(x)) return x;
-    return (float)sd_log_d((double)x);
+    const uint32_t b = sd_bits_f(x);
+    uint32_t mant = b & 0x7fffffu;
+    int e = (int)(b >> 23) - 127;
+    if ((b >> 23) == 0) { /* subnormal: normalise the mantissa with integer shifts */
+        const int k = __builtin_clz(mant) - 8;
+        mant = (mant << k) & 0x7fffffu;
+        e = -126 - k;
+    }
+    const int i = (int)(mant >> 16);
+    double m = sd_from_bits_d(0x3ff0000000000000ull | ((uint64_t)mant << 29));
+    if (i >= 53) {
+        m = m * 0.5;
+        e = e + 1;
+    }
+#if defined(__HIP_DEVICE_COMPILE__)
+    const sd_logtab_t t = SD_LOGTAB_D[i];
+#else
+    const sd_logtab_t t = SD_LOGTAB_H[i];
+#endif
+    const double r = (m - t.c) * t.inv;
+    double p = -0.125;
+    p = __builtin_fma(p, r, 1.0 / 7.0);
+    p = __builtin_fma(p, r, -1.0 / 6.0);
+    p = __builtin_fma(p, r, 0.2);
+    p = __builtin_fma(p, r, -0.25);
+    p = __builtin_fma(p, r, 1.0 / 3.0);
+    p = __builtin_fma(p, r, -0.5);
+    p = __builtin_fma(p, r, 1.0);
+    p = p * r;
+    const double ed = (double)e;
+    return (float)__builtin_fma(ed, SD_LN2_HI, __builtin_fma(ed, SD_LN2_LO, t.lg + p));
 }
 
 /* f32::log10 */

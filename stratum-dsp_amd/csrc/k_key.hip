@@ -104,7 +104,7 @@ __global__ __launch_bounds__(MASK_T) void k_mask_r(float* __restrict__ mags, int
                                                     const int* __restrict__ tracks, int blocks_per_track,
                                                     float power) {
     constexpr int R = 2 * M + 2, RX = M + 1;
-    static_assert(M >= 1, "margin 0 uses k_mask");
+    static_assert(M >= 1 && (2 * M + 1) % 2 == 1 && 2 * M + 1 <= 25, "fast window division validated for 3..25");
     const int it = blockIdx.x / blocks_per_track;
     const int trk = tracks[it];
     const int b = (blockIdx.x % blocks_per_track) * MASK_T + threadIdx.x;
@@ -113,6 +113,7 @@ __global__ __launch_bounds__(MASK_T) void k_mask_r(float* __restrict__ mags, int
     float* col = mags + frame_pfx[trk] * (uint64_t)stride + b;
     const float p = sd_maxf(power, 1.0f);
     const float eps = 1e-12f;
+    const float inv_w = 1.0f / (float)(2 * M + 1);
     float P[R], X[RX];
 #pragma unroll
     for (int j = 0; j < R; j++) P[j] = 0.0f;
@@ -134,7 +135,17 @@ __global__ __launch_bounds__(MASK_T) void k_mask_r(float* __restrict__ mags, int
                 const int64_t st = t >= M ? t - M : 0;
                 const int64_t en = t + M + 1 < F ? t + M + 1 : F;
                 const float denom = (float)(en - st > 1 ? en - st : 1);
-                const float hm = (P[(u + 1) % R] - P[(u + R - 2 * M) % R]) / denom;
+                const float a = P[(u + 1) % R] - P[(u + R - 2 * M) % R];
+                float hm;
+                // interior window (2M+1 frames): a/(2M+1) by one product and one FMA correction,
+                // == the correctly rounded quotient for every f32 a in {0} U [2^-90, 2^120]
+                // (tools/check_div.c: exhaustive, every odd window 3..25); else the IEEE division
+                if (en - st == 2 * M + 1 && (a == 0.0f || (a >= 0x1p-90f && a <= 0x1p120f))) {
+                    const float q0 = a * inv_w;
+                    hm = __builtin_fmaf(__builtin_fmaf(-q0, (float)(2 * M + 1), a), inv_w, q0);
+                } else {
+                    hm = a / denom;
+                }
                 const float x = max_bnn(X[(u + 1) % RX], 0.0f);
                 const float h = max_bnn(hm, 0.0f);
                 const float r = max_bnn(x - h, 0.0f);

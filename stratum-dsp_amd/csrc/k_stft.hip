@@ -130,18 +130,26 @@ __global__ __launch_bounds__(256) void k_stft_mag(const float* __restrict__ samp
     // real-FFT post-processing, |X[k]|, k = 0..M
     float* out = mags + (mag_row0[trk] + f) * (uint64_t)stride;
     float mx = 0.0f;
-    for (int k = lt; k <= M; k += TPF) {
+    auto post = [&](int k, cx w) {
         const cx Zk = buf[lpad(k & (M - 1))];
         const cx Zr = buf[lpad((M - k) & (M - 1))];
         const cx Zc = {Zr.re, -Zr.im};
         const cx E = {(Zk.re + Zc.re) * 0.5f, (Zk.im + Zc.im) * 0.5f};
         const cx D = csub(Zk, Zc);
         const cx O = {D.im * 0.5f, -(D.re * 0.5f)};
-        const cx X = cadd(E, cmul(rt[k], O));
+        const cx X = cadd(E, cmul(w, O));
         const float mag = __builtin_sqrtf(X.re * X.re + X.im * X.im);
         if (live) out[k] = mag;
         if (FRAME_MAX) mx = sd_maxf(mx, mag);
-    }
+    };
+    // k = lt + TPF*j for j < M/TPF (post twiddles loaded up front), then k = M on lane 0
+    constexpr int NPOST = M / TPF;
+    cx wr[NPOST];
+#pragma unroll
+    for (int j = 0; j < NPOST; j++) wr[j] = rt[lt + TPF * j];
+#pragma unroll
+    for (int j = 0; j < NPOST; j++) post(lt + TPF * j, wr[j]);
+    if (lt == 0) post(M, rt[M]);
     if (FRAME_MAX) {
         if constexpr (TPF == 64) {
             mx = wave_max(mx);

@@ -410,8 +410,19 @@ void Pipeline::run(const float* d_samples, const std::vector<uint64_t>& in_off, 
             res[i].err = "Not implemented: " + why;
         }
     }
-    // sub-batches under an HBM budget (bytes per track estimated from its raw length)
-    const double budget = 64e9;
+    // Sub-batches under an HBM budget (bytes per track estimated from its raw length): what is
+    // free now plus what this context already holds (its buffers are reused), less headroom
+    // for the grow-only buffers' 1/8 slack.  SDSP_HBM_BUDGET_GB overrides.
+    double budget = 64e9;
+    {
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) == hipSuccess) {
+            double held = 0;
+            for (auto& kv : d_.bufs) held += (double)kv.second->bytes;
+            budget = std::max(4e9, ((double)fr + held) * 0.80 / 1.125);
+        }
+        if (const char* e = std::getenv("SDSP_HBM_BUDGET_GB")) budget = std::max(1.0, std::atof(e)) * 1e9;
+    }
     const uint64_t hop = cfg_.hop_size, khop = std::max<uint64_t>(cfg_.key_stft_hop_size, 1);
     std::vector<int> cur;
     double acc = 0;
