@@ -31,6 +31,73 @@ import sdsp  # noqa: E402  (loads libstratum_hip.so first)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
+class Engine:
+    """The HIP engine through its C ABI (libstratum_hip.so): tracks generated and kept in HBM."""
+
+    def __init__(self, dev):
+        sdsp.lib()
+        self.dev = dev
+
+    def generate(self, n, L, sr, seed0, bpm_mode):
+        buf = sdsp.DeviceBuffer(n * L, device=self.dev)
+        sdsp.generate_synthetic(buf.ptr, n, L, sr, seed0=seed0, bpm_mode=bpm_mode, device=self.dev)
+        return buf
+
+    def analyze(self, buf, offs, lens, sr):
+        return sdsp.analyze_batch_device(buf.ptr, offs, lens, sr, device=self.dev, raw=True)
+
+    def stage_times(self):
+        return sdsp.stage_times(self.dev)
+
+    def synchronize(self):
+        sdsp.synchronize(self.dev)
+
+
+class DryEngine:
+    """--dry-run: rehearses the launcher / sharding / timing / reporting logic on the CPU (the
+    multi-process tests drive it with gloo); it measures nothing."""
+
+    class _Res:
+        def __init__(self, n):
+            self.status = [0] * n
+
+        def free(self):
+            pass
+
+    def __init__(self, dev):
+        self.dev = dev
+
+    def generate(self, n, L, sr, seed0, bpm_mode):
+        return {"n": n, "seed0": seed0}
+
+    def analyze(self, buf, offs, lens, sr):
+        time.sleep(0.001 * len(lens))
+        return DryEngine._Res(len(lens))
+
+    def stage_times(self):
+        return {k: 0.0 for k in ("stft2048_ms", "stft8192_ms", "stft2048_bytes", "stft8192_bytes", "total_ms")} | {
+            "stft2048_launches": 0, "stft8192_launches": 0}
+
+    def synchronize(self):
+        pass
+
+
+def shard_seed0(rank, tracks_per_rank):
+    """First synthetic seed of this rank: ranks own disjoint, contiguous track ranges."""
+    return rank * tracks_per_rank
+
+
+def max_over_ranks(dt, tdist):
+    """The job's time = the slowest rank's (weak scaling, no data-path collective)."""
+    if tdist is None:
+        return dt
+    import torch
+
+    t = torch.tensor([dt], dtype=torch.float64)
+    tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -42,66 +109,57 @@ def main():
     ap.add_argument("--cpu-tracks", type=int, default=0, help="0 = 2 per thread")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--bpm-mode", type=int, default=0, help="1 = config-5 escalation-heavy BPM mix")
+    ap.add_argument("--dry-run", action="store_true", help="host-logic rehearsal without a GPU (tests)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dev = local
-    sdsp.lib()
-    dist = None
+    eng = (DryEngine if args.dry_run else Engine)(local)
+    tdist = None
     if world > 1:
-        import torch
         import torch.distributed as tdist
 
         tdist.init_process_group("gloo", rank=rank, world_size=world)
-        dist = (torch, tdist)
 
     def barrier():
-        if dist:
-            dist[1].barrier()
+        if tdist is not None:
+            tdist.barrier()
 
     sr = 44100
     n = args.tracks
     L = int(args.seconds * sr)
-    buf = sdsp.DeviceBuffer(n * L, device=dev)
-    sdsp.generate_synthetic(buf.ptr, n, L, sr, seed0=rank * n, bpm_mode=args.bpm_mode, device=dev)
+    buf = eng.generate(n, L, sr, shard_seed0(rank, n), args.bpm_mode)
     offs = np.arange(n, dtype=np.uint64) * np.uint64(L)
     lens = np.full(n, L, dtype=np.uint64)
 
     # results stay native (C-ABI structs, as a Rust/C caller receives them); the parity sample
     # below converts the tracks it checks
     for _ in range(args.warmup):
-        sdsp.analyze_batch_device(buf.ptr, offs, lens, sr, device=dev, raw=True).free()
+        eng.analyze(buf, offs, lens, sr).free()
     barrier()
-    sdsp.synchronize(dev)
+    eng.synchronize()
     t0 = time.perf_counter()
     stft = {"ms8": 0.0, "b8": 0.0, "l8": 0, "ms2": 0.0, "b2": 0.0, "l2": 0}
     res = None
     for _ in range(args.steps):
         if res is not None:
             res.free()
-        res = sdsp.analyze_batch_device(buf.ptr, offs, lens, sr, device=dev, raw=True)
-        st = sdsp.stage_times(dev)
+        res = eng.analyze(buf, offs, lens, sr)
+        st = eng.stage_times()
         stft["ms8"] += st["stft8192_ms"]
         stft["b8"] += st["stft8192_bytes"]
         stft["l8"] += st["stft8192_launches"]
         stft["ms2"] += st["stft2048_ms"]
         stft["b2"] += st["stft2048_bytes"]
         stft["l2"] += st["stft2048_launches"]
-    sdsp.synchronize(dev)
+    eng.synchronize()
     barrier()
-    dt = time.perf_counter() - t0
-    if dist:
-        torch, tdist = dist
-        t = torch.tensor([dt], dtype=torch.float64)
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        dt = float(t.item())
+    dt = max_over_ranks(time.perf_counter() - t0, tdist)
     n_err = sum(1 for st in res.status if st != 0)
     total_tracks = n * world * args.steps
     value = total_tracks / dt
-    stages = sdsp.stage_times(dev)
-
+    stages = eng.stage_times()
     # roofline of the dominant STFT kernel (k_stft_mag<8192>): algorithmic bytes per launch
     # (4*N_in + 4*F*(nfft/2+1)) / average launch time (HIP events on the engine stream)
     l8 = max(stft["l8"], 1)
@@ -134,7 +192,7 @@ def main():
 
     cpu = None
     parity = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.dry_run:
         cpu, parity = cpu_baseline(buf, res, n, L, sr, args)
 
     if rank == 0:
@@ -150,7 +208,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (seeded on-device generator: kick/hat/triad/diatonic line, 3-min 44.1 kHz mono)",
+            "data": "synthetic (seeded on-device generator: kick/hat/triad/diatonic line, 3-min 44.1 kHz mono)"
+            + (" [DRY RUN: no GPU, not a measurement]" if args.dry_run else ""),
             "config": {
                 "workload": f"batch of {n} synthetic {args.seconds:g}-s 44.1 kHz mono tracks per GPU, "
                             "AnalysisConfig::default(), full BPM + key + beat grid",
@@ -167,8 +226,8 @@ def main():
             "parity_sample": parity,
         }
         print(json.dumps(out), flush=True)
-    if dist:
-        dist[1].destroy_process_group()
+    if tdist is not None:
+        tdist.destroy_process_group()
 
 
 def cpu_baseline(buf, res, n, L, sr, args):

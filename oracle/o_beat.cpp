@@ -13,6 +13,26 @@ struct BeatPos {
     float t, conf;
 };
 
+// hmm.rs:165-174: tempo states 0.90 .. 1.10 x the estimate
+static void hmm_states(float bpm, float out[5]) {
+    const float mult[5] = {0.90f, 0.95f, 1.00f, 1.05f, 1.10f};
+    for (int i = 0; i < 5; i++) out[i] = bpm * mult[i];
+}
+
+// hmm.rs:184-219: transition matrix, rows normalized
+static void hmm_transition(float T[5][5]) {
+    for (int i = 0; i < 5; i++) {
+        float sum = 0.0f;
+        for (int j = 0; j < 5; j++) {
+            const int d = i > j ? i - j : j - i;
+            T[i][j] = d == 0 ? 0.7f : d == 1 ? 0.15f : 0.0f;
+            sum += T[i][j];
+        }
+        if (sum > EPS)
+            for (int j = 0; j < 5; j++) T[i][j] /= sum;
+    }
+}
+
 // hmm.rs:121-441.  The Viterbi pass is run faithfully, but note that the
 // emission is state-independent, so the extracted beats never depend on the path.
 static bool hmm_track(float bpm, const std::vector<float>& on, std::vector<BeatPos>* out) {
@@ -34,18 +54,8 @@ static bool hmm_track(float bpm, const std::vector<float>& on, std::vector<BeatP
         const float dsq = md * md;
         emis[t] = sd_expf(-dsq / (2.0f * sigma_sq));  // identical for all 5 states
     }
-    // transition matrix (hmm.rs:184-219), rows normalized
     float T[5][5];
-    for (int i = 0; i < 5; i++) {
-        float sum = 0.0f;
-        for (int j = 0; j < 5; j++) {
-            const int d = i > j ? i - j : j - i;
-            T[i][j] = d == 0 ? 0.7f : d == 1 ? 0.15f : 0.0f;
-            sum += T[i][j];
-        }
-        if (sum > EPS)
-            for (int j = 0; j < 5; j++) T[i][j] /= sum;
-    }
+    hmm_transition(T);
     // Viterbi (hmm.rs:308-375)
     std::vector<float> v(5), nv(5);
     std::vector<std::array<int, 5>> bp(nf);
@@ -318,3 +328,22 @@ bool generate_beat_grid(float bpm, float conf, const std::vector<float>& onsets_
 }
 
 }  // namespace orc
+
+// ---- KAT probes (tests only) ----
+extern "C" void sdsp_oracle_hmm_model(float bpm, float* states5, float* trans25) {
+    orc::hmm_states(bpm, states5);
+    float T[5][5];
+    orc::hmm_transition(T);
+    for (int i = 0; i < 25; i++) trans25[i] = T[i / 5][i % 5];
+}
+
+// HmmBeatTracker::track_beats on onset times (s); returns the beat count or -1 (Err)
+extern "C" int32_t sdsp_oracle_hmm_track(float bpm, const float* on, int32_t n, float* out, int32_t cap) {
+    std::vector<float> v(on, on + (n > 0 ? n : 0));
+    std::vector<orc::BeatPos> pos;
+    if (!orc::hmm_track(bpm, v, &pos)) return -1;
+    const int32_t m = (int32_t)pos.size();
+    for (int32_t i = 0; i < m && i < cap; i++) out[i] = pos[(size_t)i].t;
+    return m;
+}
+

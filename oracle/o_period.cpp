@@ -1043,3 +1043,18 @@ void multi_resolution(const std::vector<float>& samples, uint32_t sr, size_t fra
 }
 
 }  // namespace orc
+
+// find_best_bpm_fft / find_best_bpm_autocorr probe (tests only): tempogram already sorted by
+// value descending, as both tempogram builders return it.  Returns 0 for an empty tempogram.
+extern "C" int32_t sdsp_oracle_find_best(const float* bpm, const float* val, int32_t n, float* out_bpm,
+                                         float* out_val, float* out_conf) {
+    orc::Tg tg;
+    for (int32_t i = 0; i < n; i++) tg.push_back({bpm[i], val[i]});
+    float b = 0.0f, c = 0.0f;
+    if (!orc::find_best(tg, &b, &c)) return 0;
+    *out_bpm = b;
+    *out_val = tg[0].second;
+    *out_conf = c;
+    return 1;
+}
+

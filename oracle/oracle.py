@@ -51,6 +51,11 @@ def lib():
         L.sdsp_oracle_key_clarity.restype = C.c_float
         L.sdsp_oracle_key_templates.argtypes = [fp]
         L.sdsp_oracle_libm.argtypes = [C.c_int32, fp, fp, fp, C.c_uint64]
+        L.sdsp_oracle_find_best.argtypes = [fp, fp, C.c_int32, fp, fp, fp]
+        L.sdsp_oracle_find_best.restype = C.c_int32
+        L.sdsp_oracle_hmm_model.argtypes = [C.c_float, fp, fp]
+        L.sdsp_oracle_hmm_track.argtypes = [C.c_float, fp, C.c_int32, fp, C.c_int32]
+        L.sdsp_oracle_hmm_track.restype = C.c_int32
         _lib = L
     return _lib
 
@@ -147,3 +152,29 @@ def libm(op, x, y=None):
     out = np.empty_like(x)
     lib().sdsp_oracle_libm(ops[op], _fp(x), _fp(y), _fp(out), x.size)
     return out
+
+
+def find_best(tempogram):
+    """find_best_bpm_fft / find_best_bpm_autocorr on a (bpm, value) list sorted by value desc."""
+    b = np.ascontiguousarray([t[0] for t in tempogram], dtype=np.float32)
+    v = np.ascontiguousarray([t[1] for t in tempogram], dtype=np.float32)
+    ob, ov, oc = C.c_float(), C.c_float(), C.c_float()
+    ok = lib().sdsp_oracle_find_best(_fp(b), _fp(v), len(tempogram), C.byref(ob), C.byref(ov), C.byref(oc))
+    return (ob.value, ov.value, oc.value) if ok else None
+
+
+def hmm_model(bpm):
+    """(state BPMs, 5x5 transition matrix) of HmmBeatTracker (hmm.rs:165-219)."""
+    st = np.empty(5, np.float32)
+    tr = np.empty(25, np.float32)
+    lib().sdsp_oracle_hmm_model(C.c_float(bpm), _fp(st), _fp(tr))
+    return st, tr.reshape(5, 5)
+
+
+def hmm_track(bpm, onsets_s):
+    """HmmBeatTracker::track_beats beat times, or None on Err."""
+    on = np.ascontiguousarray(onsets_s, dtype=np.float32)
+    cap = 4 * on.size + 64
+    out = np.empty(cap, np.float32)
+    n = lib().sdsp_oracle_hmm_track(C.c_float(bpm), _fp(on), on.size, _fp(out), cap)
+    return None if n < 0 else out[:n].copy()

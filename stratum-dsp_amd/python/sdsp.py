@@ -103,6 +103,14 @@ def analyze_audio(samples, sample_rate=44100, config=None):
         lib().sdsp_result_free(C.byref(r))
 
 
+def _batch_error(outs, n, what):
+    """Whole-batch failure: the first per-track message, and free whatever was filled."""
+    msg = outs[0].error_message.decode() if n > 0 and outs[0].error_message[0:1] != b"\0" else ""
+    for i in range(n):
+        lib().sdsp_result_free(C.byref(outs[i]))
+    return f"{what}: {msg}" if msg else what
+
+
 def analyze_batch(tracks, sample_rate=44100, config=None, device_mask=0):
     """Batch form: list of per-track results; failed tracks come back as AnalysisError objects."""
     arrs = [np.ascontiguousarray(t, dtype=np.float32) for t in tracks]
@@ -114,7 +122,7 @@ def analyze_batch(tracks, sample_rate=44100, config=None, device_mask=0):
     st = lib().sdsp_analyze_batch(ptrs, lens.ctypes.data_as(C.POINTER(C.c_uint64)), n, sample_rate, C.byref(cfg),
                                   device_mask, outs)
     if st != 0:
-        raise AnalysisError(st, "batch failed")
+        raise AnalysisError(st, _batch_error(outs, n, "batch failed"))
     res = []
     for i in range(n):
         if outs[i].status != 0:
@@ -168,7 +176,7 @@ def analyze_batch_device(d_ptr, offsets, lens, sample_rate=44100, config=None, d
                                          ln.ctypes.data_as(C.POINTER(C.c_uint64)), n, sample_rate, C.byref(cfg),
                                          device, C.c_void_p(stream or 0), outs)
     if st != 0:
-        raise AnalysisError(st, "device batch failed")
+        raise AnalysisError(st, _batch_error(outs, n, "device batch failed"))
     batch = ResultBatch(outs, n)
     if raw:
         return batch

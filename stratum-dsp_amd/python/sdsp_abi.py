@@ -221,6 +221,27 @@ def key_numerical(mode, tonic):
     return f"{pos + 1}{'A' if mode == 0 else 'B'}"
 
 
+def key_from_numerical(notation):
+    """Key::from_numerical, result.rs:113-140 -> (mode, tonic) or None."""
+    import re
+
+    if len(notation.encode()) < 2:
+        return None
+    num_str, suffix = notation[:-1], notation[-1]
+    if not re.fullmatch(r"\+?[0-9]+", num_str):  # u32::from_str
+        return None
+    num = int(num_str)
+    if not 1 <= num <= 12:
+        return None
+    maj = [0, 7, 2, 9, 4, 11, 6, 1, 8, 3, 10, 5]
+    mnr = [9, 4, 11, 6, 1, 8, 3, 10, 5, 0, 7, 2]
+    if suffix == "A":
+        return (0, maj[num - 1])
+    if suffix == "B":
+        return (1, mnr[num - 1])
+    return None
+
+
 def _tri(v):
     return None if v < 0 else bool(v)
 

@@ -1,0 +1,98 @@
+"""The drop-in boundary (include/stratum_hip.h, libstratum_hip.so) without a GPU (CPU only).
+
+* the library loads and exports every function the header declares;
+* the Python binding's ctypes mirrors (sdsp_abi) have exactly the C layout (offset of every
+  field checked against a compiled probe of the header);
+* sdsp_config_default() == AnalysisConfig::default() (reference src/config.rs:594-744) as the
+  CPU restatement states it, field by field;
+* with no GPU the product path fails loudly (no CPU fallback).
+"""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle
+import sdsp
+import sdsp_abi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "stratum_hip.h")
+
+
+def _declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(sdsp_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_header_functions():
+    lib = sdsp.lib()
+    names = _declared_functions()
+    assert "sdsp_analyze_audio" in names and "sdsp_analyze_batch" in names and len(names) >= 14
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_version():
+    v = sdsp.version()
+    assert v.startswith("stratum-hip ") and v.endswith("gfx950")
+
+
+STRUCTS = {"sdsp_config": sdsp_abi.SdspConfig, "sdsp_result": sdsp_abi.SdspResult,
+           "sdsp_tempo_candidate": sdsp_abi.SdspTempoCandidate, "sdsp_stage_times": sdsp_abi.SdspStageTimes}
+
+
+def test_struct_layout_matches_header(tmp_path):
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void) {"]
+    for cname, py in STRUCTS.items():
+        lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
+        for f, _ in py._fields_:
+            lines.append(f'printf("{cname}.{f} %zu\\n", offsetof({cname}, {f}));')
+    lines.append("return 0; }")
+    src = tmp_path / "probe.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "probe"
+    subprocess.check_call(["gcc", "-std=c11", "-o", str(exe), str(src)])
+    out = subprocess.check_output([str(exe)]).decode().split("\n")
+    c = {}
+    for ln in out:
+        if ln:
+            k, v = ln.rsplit(" ", 1)
+            c[k] = int(v)
+    for cname, py in STRUCTS.items():
+        assert c[f"{cname} size"] == C.sizeof(py), cname
+        for f, _ in py._fields_:
+            assert c[f"{cname}.{f}"] == getattr(py, f).offset, f"{cname}.{f}"
+
+
+def _fields(cfg):
+    out = {}
+    for f, t in sdsp_abi.SdspConfig._fields_:
+        v = getattr(cfg, f)
+        if isinstance(v, C.Array):
+            v = list(v)
+        elif f.endswith("_ptr") or isinstance(v, (C._Pointer,)):
+            continue
+        out[f] = v
+    return out
+
+
+def test_config_default_matches_reference_defaults():
+    got, want = _fields(sdsp.default_config()), _fields(oracle.default_config())
+    diff = {k: (got[k], want[k]) for k in want if not (got[k] == want[k] or (got[k] != got[k] and want[k] != want[k]))}
+    assert not diff, diff
+
+
+def test_no_gpu_fails_loudly():
+    if sdsp.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(sdsp.AnalysisError) as e:
+        sdsp.analyze_audio(np.ones(44100, np.float32), 44100)
+    assert "no HIP device" in str(e.value)
+    with pytest.raises(sdsp.AnalysisError) as e:
+        sdsp.analyze_batch([np.ones(44100, np.float32)], 44100)
+    assert "no HIP device" in str(e.value)

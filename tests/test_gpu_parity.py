@@ -51,6 +51,7 @@ def test_reference_integration_ranges():
     assert len(b) >= 4 and abs((b[1] - b[0]) - 0.5) < 0.1
     x, sr = parity.load_wav(os.path.join(GOLDEN, "128bpm_4bar.wav"))
     r = sdsp.analyze_audio(x, sr)
+    assert 7.0 < r["metadata"]["duration_seconds"] < 8.0
     assert abs(r["bpm"] - 128.0) <= 2.0
     x, sr = parity.load_wav(os.path.join(GOLDEN, "cmajor_scale.wav"))
     r = sdsp.analyze_audio(x, sr)

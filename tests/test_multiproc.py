@@ -1,0 +1,66 @@
+"""The N>1 path on the CPU (gloo, world size 2, 127.0.0.1).  The path shards by track with no
+data-path collective: each rank owns a disjoint contiguous seed range, the job
+time is the slowest rank's, and rank 0 alone reports the whole-job throughput.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, ROOT)
+    import torch.distributed as tdist
+
+    import bench
+
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    seed0 = bench.shard_seed0(rank, 16)
+    dt = bench.max_over_ranks(0.5 + rank, tdist)  # rank 1 is the slow one
+    q.put((rank, seed0, dt))
+    tdist.destroy_process_group()
+
+
+def test_sharding_and_max_over_ranks():
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert [g[1] for g in got] == [0, 16]          # disjoint contiguous track ranges
+    assert all(abs(g[2] - 1.5) < 1e-12 for g in got)  # every rank sees the slowest time
+
+
+def test_bench_launcher_world2_dry_run():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--tracks", "4", "--seconds", "1", "--dry-run"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1  # rank 0 only
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["warmup"] == 2 - 1
+    assert d["scaling"] == "weak" and d["higher_is_better"] is True
+    assert abs(d["value"] - 4 * 2 * 2 / (d["ms_per_step"] * 2 / 1000.0)) / d["value"] < 1e-2
+    assert d["config"]["parallelism"].startswith("track-sharded x2")
