@@ -132,3 +132,36 @@ def test_emit_candidates_config():
     for a, b in zip(gc, rc):
         assert abs(a["bpm"] - b["bpm"]) <= 1e-4 and abs(a["score"] - b["score"]) <= 1e-4
         assert a["selected"] == b["selected"]
+
+
+def _golden():
+    import json
+
+    with open(os.path.join(GOLDEN, "oracle_results.json")) as f:
+        return json.load(f)
+
+
+def _strip(r):
+    import json
+
+    r = dict(r)
+    r["metadata"] = {k: v for k, v in r["metadata"].items() if k != "processing_time_ms"}
+    return json.loads(json.dumps(r, sort_keys=True))
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_golden_fixture_vectors(name):
+    """Bit-exact against the committed golden vectors (tests/golden/oracle_results.json)."""
+    x, sr = parity.load_wav(os.path.join(GOLDEN, name))
+    assert _strip(sdsp.analyze_audio(x, sr)) == _golden()["fixtures"][name]
+
+
+def test_golden_synthetic_vectors():
+    g = _golden()["synthetic"]
+    keys = sorted(g)
+    tracks = []
+    for k in keys:
+        seed, sec = k.split(":")
+        tracks.append(synth.make_track(int(seed), seconds=float(sec))[0])
+    for k, r in zip(keys, sdsp.analyze_batch(tracks, 44100)):
+        assert _strip(r) == g[k], k
