@@ -2,15 +2,16 @@
 // plus the C ABI entry points (sdsp_analyze_audio / _batch / _batch_device, synthetic tracks).
 //
 // Per sub-batch (sized to an HBM budget), the host plans ragged per-track frame ranges and
-// launches, in stream order:
+// launches:
 //   A  peak/gain, silence RMS, trim                      -> host reads trim bounds (sync 1)
+//   E  key, forked onto the key stream: STFT 8192/512 -> harmonic mask (in place) -> HPCP ->
+//      key vote (runs under B-D)
 //   B  energy RMS + energy-flux onsets; STFT 2048/512; frame features; spectral/HFC onsets;
 //      consensus; novelty (5 variants); FFT + ACF tempograms; candidate scoring + gate
 //                                                        -> host reads estimates (sync 2)
 //   C  escalation for ambiguous tracks: STFT 2048/256 and 2048/1024 of those tracks, the same
 //      feature/novelty/tempogram/scoring kernels, then multi-resolution fusion
-//   D  beat grid; E  key: STFT 8192/512 -> harmonic mask (in place) -> HPCP -> key vote
-//                                                        -> host reads results (sync 3)
+//   D  beat grid; join the key stream                    -> host reads results (sync 3)
 // No stage falls back to the CPU; host code only plans offsets and formats the result.
 #include <algorithm>
 #include <chrono>
