@@ -120,8 +120,41 @@ __global__ __launch_bounds__(MASK_T) void k_mask_r(float* __restrict__ mags, int
 #pragma unroll
     for (int j = 0; j < RX; j++) X[j] = 0.0f;
     float prev = 0.0f;
+    // one output element: window sum a over `den` frames -> masked value
+    auto emit = [&](float a, int64_t den, float xr, int64_t t) {
+        float hm;
+        // full window (2M+1 frames): a/(2M+1) by one product and one FMA correction, == the
+        // correctly rounded quotient for every f32 a in {0} U [2^-90, 2^120] (tools/check_div.c:
+        // exhaustive, every odd window 3..25); otherwise the IEEE division
+        if (den == 2 * M + 1 && (a == 0.0f || (a >= 0x1p-90f && a <= 0x1p120f))) {
+            const float q0 = a * inv_w;
+            hm = __builtin_fmaf(__builtin_fmaf(-q0, (float)(2 * M + 1), a), inv_w, q0);
+        } else {
+            hm = a / (float)(den > 1 ? den : 1);
+        }
+        const float x = max_bnn(xr, 0.0f);
+        const float h = max_bnn(hm, 0.0f);
+        const float r = max_bnn(x - h, 0.0f);
+        const float hp = mask_pow<PW>(h, p);
+        const float rp = mask_pow<PW>(r, p);
+        const float m = hp / (hp + rp + eps);
+        col[t * stride] = x * m;
+    };
     for (int64_t base = 0; base < F + M; base += R) {
         float xv[R];
+        if (base >= 2 * M && base + R <= F) {
+            // interior block: every step has a full window; no edge conditions
+#pragma unroll
+            for (int u = 0; u < R; u++) xv[u] = col[(base + u) * stride];
+#pragma unroll
+            for (int u = 0; u < R; u++) {
+                prev = prev + xv[u];
+                P[(u + 1) % R] = prev;
+                X[u % RX] = xv[u];
+                emit(P[(u + 1) % R] - P[(u + R - 2 * M) % R], 2 * M + 1, X[(u + 1) % RX], base + u - M);
+            }
+            continue;
+        }
 #pragma unroll
         for (int u = 0; u < R; u++) xv[u] = base + u < F ? col[(base + u) * stride] : 0.0f;
 #pragma unroll
@@ -134,25 +167,7 @@ __global__ __launch_bounds__(MASK_T) void k_mask_r(float* __restrict__ mags, int
             if (t >= 0 && t < F) {
                 const int64_t st = t >= M ? t - M : 0;
                 const int64_t en = t + M + 1 < F ? t + M + 1 : F;
-                const float denom = (float)(en - st > 1 ? en - st : 1);
-                const float a = P[(u + 1) % R] - P[(u + R - 2 * M) % R];
-                float hm;
-                // interior window (2M+1 frames): a/(2M+1) by one product and one FMA correction,
-                // == the correctly rounded quotient for every f32 a in {0} U [2^-90, 2^120]
-                // (tools/check_div.c: exhaustive, every odd window 3..25); else the IEEE division
-                if (en - st == 2 * M + 1 && (a == 0.0f || (a >= 0x1p-90f && a <= 0x1p120f))) {
-                    const float q0 = a * inv_w;
-                    hm = __builtin_fmaf(__builtin_fmaf(-q0, (float)(2 * M + 1), a), inv_w, q0);
-                } else {
-                    hm = a / denom;
-                }
-                const float x = max_bnn(X[(u + 1) % RX], 0.0f);
-                const float h = max_bnn(hm, 0.0f);
-                const float r = max_bnn(x - h, 0.0f);
-                const float hp = mask_pow<PW>(h, p);
-                const float rp = mask_pow<PW>(r, p);
-                const float m = hp / (hp + rp + eps);
-                col[t * stride] = x * m;
+                emit(P[(u + 1) % R] - P[(u + R - 2 * M) % R], en - st, X[(u + 1) % RX], t);
             }
         }
     }

@@ -12,144 +12,242 @@
 //   N = 2048 (M = 1024 = 16^2 * 4):   2 radix-16 passes + 1 radix-4 pass, 64 threads (one
 //                                     wave) per frame, 4 frames per workgroup
 //
-// The first pass reads the frame straight from HBM (x*gain*window, the reference's two f32
-// multiplies); the post-twiddle pass writes |X[k]|, k = 0..M, as coalesced row segments.
-// LDS index padding i + i/16 keeps the strided pass-1 stores near conflict-free.
+// Instruction economy (the kernel is VALU-bound):
+//  * complex values are 2-wide vectors, so every complex add / scale is one v_pk_* op and
+//    the -i rotation and conjugations fold into the packed ops' swizzle / negate modifiers;
+//  * the frame, the window and the per-thread twiddle tables are read with buffer loads
+//    whose per-element offsets are scalar (SGPR) constants, so no VALU address arithmetic;
+//  * every LDS index is (per-thread base) + (compile-time constant);
+//  * bins k and M-k share one LDS read and one E/O evaluation; |X| uses the exact fast sqrt.
+// The twiddle values are those of sdsp_fft_spec.h, re-laid out per thread on the host
+// (stft_tables below).  LDS index padding i + i/16 keeps the strided pass-1 stores
+// near conflict-free.
 //
 // Ragged batches: the flat frame index (frame_pfx prefix sums) picks the track.  Frames are
 // numbered XCD-contiguously (xcd_block) so the 16x (N=8192) / 4x (N=2048) overlap between
 // neighbouring frames is served from one L2.
+#include <vector>
+
 #include "kernels.hpp"
+#include "sdsp_runtime.hpp"
 
 namespace sdsp {
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2 ld_f2(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+    return __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+}
+// buffer resource over [p, p+bytes) for a wave-uniform pointer
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p, uint32_t bytes) {
+    const uint64_t a = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, bytes, 0x00020000);
+}
+
+// complex ops on (re, im) pairs; the same IEEE operations in the same order as cadd/csub/cmul
+__device__ __forceinline__ f2 vmul(f2 w, f2 z) {  // (w.re z.re - w.im z.im, w.re z.im + w.im z.re)
+    const f2 t1 = w.xx * z;
+    const f2 t2 = w.yy * z.yx;
+    return t1 + f2{-t2.x, t2.y};
+}
+
+// radix-4 butterfly of sdsp_fft_spec.h
+__device__ __forceinline__ void bfly4(f2 a, f2 b, f2 c, f2 d, f2 w1, f2 w2, f2 w3, f2& y0, f2& y1, f2& y2, f2& y3) {
+    const f2 apc = a + c, amc = a - c;
+    const f2 bpd = b + d, bmd = b - d;
+    const f2 jbmd = {bmd.y, -bmd.x};  // -i (b - d)
+    y0 = apc + bpd;
+    y1 = vmul(w1, amc + jbmd);
+    y2 = vmul(w2, apc - bpd);
+    y3 = vmul(w3, amc - jbmd);
+}
+
 __device__ __forceinline__ int lpad(int i) { return i + (i >> 4); }
 
-__device__ __forceinline__ void bfly4(cx a, cx b, cx c, cx d, cx w1, cx w2, cx w3, cx& y0, cx& y1, cx& y2, cx& y3) {
-    const cx apc = cadd(a, c), amc = csub(a, c);
-    const cx bpd = cadd(b, d), bmd = csub(b, d);
-    const cx jbmd = {bmd.im, -bmd.re};
-    y0 = cadd(apc, bpd);
-    y1 = cmul(w1, cadd(amc, jbmd));
-    y2 = cmul(w2, csub(apc, bpd));
-    y3 = cmul(w3, csub(amc, jbmd));
+// Correctly rounded f32 sqrt.  For x in [2^-96, inf) this is exactly the sequence hipcc emits
+// for sqrtf under -fhip-fp32-correctly-rounded-divide-sqrt (v_sqrt_f32, then the +-1 ulp
+// FMA-residual correction) without its small-input rescaling and special-value select; other
+// inputs (0, tiny, inf, NaN) take the compiler's full sqrtf.  tools/check_sqrt.hip: identical
+// to sqrtf on every non-negative f32.
+__device__ __forceinline__ float sqrt_cr(float x) {
+    if (__builtin_expect(x >= 0x1p-96f && x < __builtin_huge_valf(), 1)) {
+        float s = __builtin_amdgcn_sqrtf(x);
+        const float sm = __uint_as_float(__float_as_uint(s) - 1u);
+        const float sp = __uint_as_float(__float_as_uint(s) + 1u);
+        const float rm = __builtin_fmaf(-sm, s, x);
+        const float rp = __builtin_fmaf(-sp, s, x);
+        s = rm <= 0.0f ? sm : s;
+        s = rp > 0.0f ? sp : s;
+        return s;
+    }
+    return __builtin_sqrtf(x);
 }
 
 // Two radix-4 stages, (n, s) then (n/4, 4s), on v[j' + 4j] = x[q + s(p' + (n/16)(j' + 4j))].
-// On return v[jA + 4jB] = z[q + 16 s p' + s(jA + 4jB)].
-template <int M>
-__device__ __forceinline__ void radix16(cx v[16], const cx* __restrict__ tw, int n, int pp) {
-    const int m1 = n / 16;
-    const int tA = M / n, tB = 4 * (M / n);
-    cx u[16];
+// On return v[jA + 4jB] = z[q + 16 s p' + s(jA + 4jB)].  w[0..11] = stage-A twiddles
+// W^{jA (p' + j' n/16) M/n} at index 3 j' + jA - 1, w[12..14] = stage-B W^{jB p' 4M/n}.
+__device__ __forceinline__ void radix16(f2 v[16], const f2 w[15]) {
+    f2 u[16];
 #pragma unroll
-    for (int jp = 0; jp < 4; jp++) {
-        const int p = pp + jp * m1;
-        const cx w1 = tw[1 * p * tA], w2 = tw[2 * p * tA], w3 = tw[3 * p * tA];
-        bfly4(v[jp], v[jp + 4], v[jp + 8], v[jp + 12], w1, w2, w3, u[jp * 4 + 0], u[jp * 4 + 1], u[jp * 4 + 2],
-              u[jp * 4 + 3]);
-    }
-    const cx w1 = tw[1 * pp * tB], w2 = tw[2 * pp * tB], w3 = tw[3 * pp * tB];
+    for (int jp = 0; jp < 4; jp++)
+        bfly4(v[jp], v[jp + 4], v[jp + 8], v[jp + 12], w[3 * jp + 0], w[3 * jp + 1], w[3 * jp + 2], u[jp * 4 + 0],
+              u[jp * 4 + 1], u[jp * 4 + 2], u[jp * 4 + 3]);
 #pragma unroll
     for (int ja = 0; ja < 4; ja++)
-        bfly4(u[0 * 4 + ja], u[1 * 4 + ja], u[2 * 4 + ja], u[3 * 4 + ja], w1, w2, w3, v[ja + 0], v[ja + 4], v[ja + 8],
-              v[ja + 12]);
+        bfly4(u[0 * 4 + ja], u[1 * 4 + ja], u[2 * 4 + ja], u[3 * 4 + ja], w[12], w[13], w[14], v[ja + 0], v[ja + 4],
+              v[ja + 8], v[ja + 12]);
 }
+
+template <int M>
+struct StftShape {
+    static constexpr int TPF = M / 16;                                   // threads per frame
+    static constexpr int NPASS = (M == 4096) ? 3 : (M == 1024) ? 2 : 0;  // radix-16 passes
+    static constexpr int NPAIR = (M / 2 + TPF - 1) / TPF;               // post pairs per thread
+    static constexpr int RT_SPECIAL = NPAIR * 2 * TPF;                  // rt[0], rt[M], rt[M/2], tw[0]
+};
 
 template <int NFFT, bool FRAME_MAX>
 __global__ __launch_bounds__(256) void k_stft_mag(const float* __restrict__ samples,
                                                   const uint64_t* __restrict__ frame_pfx, int n_tracks,
                                                   uint64_t total_frames, const uint64_t* __restrict__ src_off,
                                                   const float* __restrict__ gain, int hop,
-                                                  const float* __restrict__ window, const cx* __restrict__ tw,
-                                                  const cx* __restrict__ rt, float* __restrict__ mags,
+                                                  const float* __restrict__ window, const cx* __restrict__ twp,
+                                                  const cx* __restrict__ rtp, float* __restrict__ mags,
                                                   const uint64_t* __restrict__ mag_row0, int stride,
                                                   float* __restrict__ frame_max) {
     constexpr int M = NFFT / 2;
-    constexpr int TPF = M / 16;          // threads per frame (one radix-16 group each)
-    constexpr int FPB = 256 / TPF;       // frames per workgroup
-    constexpr int PADM = M + M / 16;     // padded LDS slots per frame
-    static_assert(TPF == 64 || TPF == 256, "supported sizes: N = 2048, 8192");
-    __shared__ cx lds[FPB * PADM];
+    using S = StftShape<M>;
+    constexpr int TPF = S::TPF;
+    constexpr int FPB = 256 / TPF;    // frames per workgroup
+    constexpr int PADM = M + M / 16;  // padded LDS slots per frame
+    static_assert(S::NPASS > 0, "supported sizes: N = 2048, 8192");
+    __shared__ f2 lds[FPB * PADM];
     __shared__ float red[4];
 
-    const int lt = threadIdx.x % TPF;            // thread within frame
-    const int fl = threadIdx.x / TPF;            // frame within workgroup
+    const int lt = threadIdx.x % TPF;  // thread within frame
+    const int fl = threadIdx.x / TPF;  // frame within workgroup
     const uint64_t g = (uint64_t)xcd_block(blockIdx.x, gridDim.x) * FPB + fl;
     const bool live = g < total_frames;
     const uint64_t gg = live ? g : total_frames - 1;  // dead lanes recompute the last frame
     const int trk = find_track(frame_pfx, n_tracks, gg);
     const uint64_t f = gg - frame_pfx[trk];
-    const float* x = samples + src_off[trk] + f * (uint64_t)hop;
     const float gn = gain[trk];
-    cx* buf = lds + fl * PADM;
+    f2* buf = lds + fl * PADM;
+    const __amdgpu_buffer_rsrc_t rx = rsrc_of(samples + src_off[trk] + f * (uint64_t)hop, 4u * NFFT);
+    const __amdgpu_buffer_rsrc_t rw = rsrc_of(window, 4u * NFFT);
+    const __amdgpu_buffer_rsrc_t rtw = rsrc_of(twp, 8u * 15u * TPF * S::NPASS);
+    const __amdgpu_buffer_rsrc_t rrt = rsrc_of(rtp, 8u * (S::RT_SPECIAL + 4));
+    const int vo = 8 * lt;  // every table below is [item][lane] with 8-byte entries
 
-    cx v[16];
-    // pass 1 (n = M, s = 1, p' = lt): z[idx] = (x[2idx], x[2idx+1]) * gain * window
+    f2 v[16], w[15];
+    // pass 1 (n = M, s = 1, p' = lt): z[idx] = (x[2idx], x[2idx+1]) * gain * window, idx = lt + TPF k
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        const int idx = lt + TPF * k;
-        const float s0 = x[2 * idx] * gn;
-        const float s1 = x[2 * idx + 1] * gn;
-        v[k] = {s0 * window[2 * idx], s1 * window[2 * idx + 1]};
+        const f2 xs = ld_f2(rx, vo, 8 * TPF * k);
+        const f2 ws = ld_f2(rw, vo, 8 * TPF * k);
+        v[k] = (xs * gn) * ws;
     }
-    radix16<M>(v, tw, M, lt);
 #pragma unroll
-    for (int k = 0; k < 16; k++) buf[lpad(16 * lt + k)] = v[k];
+    for (int j = 0; j < 15; j++) w[j] = ld_f2(rtw, vo, 8 * TPF * j);
+    radix16(v, w);
+    {
+        const int b0 = 17 * lt;  // lpad(16 lt + k) = 17 lt + k
+#pragma unroll
+        for (int k = 0; k < 16; k++) buf[b0 + k] = v[k];
+    }
     __syncthreads();
-    // further radix-16 passes
+    // further radix-16 passes: (n, s) = (M/16, 16), (M/256, 256)
 #pragma unroll
-    for (int n = M / 16, s = 16; n >= 16; n /= 16, s *= 16) {
+    for (int pass = 1; pass < S::NPASS; pass++) {
+        const int s = pass == 1 ? 16 : 256;
+        const int m1 = (pass == 1 ? M / 16 : M / 256) / 16;  // n / 16
         const int q = lt % s, pp = lt / s;
-        const int m1 = n / 16;
+        // reads x[q + s pp + s m1 k]; s m1 is a multiple of 16, so lpad = lpad(q + s pp) + (17/16) s m1 k
+        const int rb = lpad(q + s * pp), rs = s * m1 + (s * m1) / 16;
 #pragma unroll
-        for (int k = 0; k < 16; k++) v[k] = buf[lpad(q + s * pp + s * m1 * k)];
+        for (int j = 0; j < 15; j++) w[j] = ld_f2(rtw, vo, 8 * TPF * (15 * pass + j));
+#pragma unroll
+        for (int k = 0; k < 16; k++) v[k] = buf[rb + rs * k];
         __syncthreads();
-        radix16<M>(v, tw, n, pp);
+        radix16(v, w);
+        // writes z[q + 16 s pp + s k]:  s = 16 -> (q + 272 pp) + 17 k;  s = 256 (pp = 0) -> lpad(q) + 272 k
+        if (s == 16) {
+            const int wb = q + 272 * pp;
 #pragma unroll
-        for (int k = 0; k < 16; k++) buf[lpad(q + 16 * s * pp + s * k)] = v[k];
-        __syncthreads();
-    }
-    // trailing radix-4 stage (M = 16^k * 4): n = 4, s = M/4, p = 0
-    if constexpr (M == 1024) {
-        constexpr int s = M / 4;
-        const cx w0 = tw[0];
+            for (int k = 0; k < 16; k++) buf[wb + 17 * k] = v[k];
+        } else {  // s = 256 only for M = 4096 (m1 = 1): z[q + 256 k], lpad = lpad(q) + 272 k
 #pragma unroll
-        for (int r = 0; r < s / TPF; r++) {
-            const int q = lt + TPF * r;
-            cx y0, y1, y2, y3;
-            bfly4(buf[lpad(q)], buf[lpad(q + s)], buf[lpad(q + 2 * s)], buf[lpad(q + 3 * s)], w0, w0, w0, y0, y1, y2,
-                  y3);
-            buf[lpad(q)] = y0;
-            buf[lpad(q + s)] = y1;
-            buf[lpad(q + 2 * s)] = y2;
-            buf[lpad(q + 3 * s)] = y3;
+            for (int k = 0; k < 16; k++) buf[rb + 272 * k] = v[k];
         }
         __syncthreads();
     }
-    // real-FFT post-processing, |X[k]|, k = 0..M
+    // trailing radix-4 stage (M = 16^2 * 4): n = 4, s = M/4, p = 0, twiddles tw[0]
+    if constexpr (M == 1024) {
+        constexpr int s = M / 4;
+        const f2 w0 = ld_f2(rrt, 0, 8 * (S::RT_SPECIAL + 3));
+#pragma unroll
+        for (int r = 0; r < s / TPF; r++) {
+            const int q = lt + TPF * r;
+            const int b = lpad(q);  // lpad(q + j s) = b + 272 j (s = 256)
+            f2 y0, y1, y2, y3;
+            bfly4(buf[b], buf[b + 272], buf[b + 544], buf[b + 816], w0, w0, w0, y0, y1, y2, y3);
+            buf[b] = y0;
+            buf[b + 272] = y1;
+            buf[b + 544] = y2;
+            buf[b + 816] = y3;
+        }
+        __syncthreads();
+    }
+    // real-FFT post-processing, |X[k]|, k = 0..M.  Bins k and M-k read the same pair
+    // (Z[k], Z[M-k]); the partner's E and O are the conjugates of this bin's (exactly, up to
+    // the sign of zero, which |X| cannot see), so each pair is read and combined once.
     float* out = mags + (mag_row0[trk] + f) * (uint64_t)stride;
     float mx = 0.0f;
-    auto post = [&](int k, cx w) {
-        const cx Zk = buf[lpad(k & (M - 1))];
-        const cx Zr = buf[lpad((M - k) & (M - 1))];
-        const cx Zc = {Zr.re, -Zr.im};
-        const cx E = {(Zk.re + Zc.re) * 0.5f, (Zk.im + Zc.im) * 0.5f};
-        const cx D = csub(Zk, Zc);
-        const cx O = {D.im * 0.5f, -(D.re * 0.5f)};
-        const cx X = cadd(E, cmul(w, O));
-        const float mag = __builtin_sqrtf(X.re * X.re + X.im * X.im);
+    auto mag_of = [&](f2 E, f2 O, f2 wt) {
+        const f2 X = E + vmul(wt, O);
+        const f2 sq = X * X;
+        return sqrt_cr(sq.x + sq.y);
+    };
+    auto put = [&](int k, float mag) {
         if (live) out[k] = mag;
         if (FRAME_MAX) mx = sd_maxf(mx, mag);
     };
-    // k = lt + TPF*j for j < M/TPF (post twiddles loaded up front), then k = M on lane 0
-    constexpr int NPOST = M / TPF;
-    cx wr[NPOST];
+    auto pair_eo = [&](int ik, int ir, f2& E, f2& O) {  // LDS indices of Z[k], Z[M-k]
+        const f2 Zk = buf[ik];
+        const f2 Zr = buf[ir];
+        const f2 Zc = {Zr.x, -Zr.y};
+        E = (Zk + Zc) * 0.5f;
+        const f2 D = Zk - Zc;
+        O = f2{D.y * 0.5f, -(D.x * 0.5f)};
+    };
+    f2 wk[S::NPAIR], wm[S::NPAIR];
 #pragma unroll
-    for (int j = 0; j < NPOST; j++) wr[j] = rt[lt + TPF * j];
+    for (int j = 0; j < S::NPAIR; j++) {
+        wk[j] = ld_f2(rrt, vo, 8 * TPF * (2 * j));
+        wm[j] = ld_f2(rrt, vo, 8 * TPF * (2 * j + 1));
+    }
 #pragma unroll
-    for (int j = 0; j < NPOST; j++) post(lt + TPF * j, wr[j]);
-    if (lt == 0) post(M, rt[M]);
+    for (int j = 0; j < S::NPAIR; j++) {
+        const int k = 1 + lt + TPF * j;  // k < M/2 except possibly on the last j
+        if (j + 1 < S::NPAIR || k < M / 2) {
+            f2 E, O;
+            pair_eo(lpad(k), lpad(M - k), E, O);
+            put(k, mag_of(E, O, wk[j]));
+            put(M - k, mag_of(f2{E.x, -E.y}, f2{O.x, -O.y}, wm[j]));
+        }
+    }
+    if (lt == 0) {  // k = 0 and k = M both read (Z[0], Z[0]); k = M/2 reads (Z[M/2], Z[M/2])
+        f2 E, O;
+        pair_eo(0, 0, E, O);
+        put(0, mag_of(E, O, ld_f2(rrt, 0, 8 * S::RT_SPECIAL)));
+        put(M, mag_of(E, O, ld_f2(rrt, 0, 8 * (S::RT_SPECIAL + 1))));
+    } else if (lt == 1) {
+        f2 E, O;
+        pair_eo(lpad(M / 2), lpad(M / 2), E, O);
+        put(M / 2, mag_of(E, O, ld_f2(rrt, 0, 8 * (S::RT_SPECIAL + 2))));
+    }
     if (FRAME_MAX) {
         if constexpr (TPF == 64) {
             mx = wave_max(mx);
@@ -167,10 +265,52 @@ __global__ __launch_bounds__(256) void k_stft_mag(const float* __restrict__ samp
     }
 }
 
+// Host: per-thread twiddle layouts for k_stft_mag, from the spec's tables (values unchanged).
+//   twp[(15 pass + j) TPF + lt]: pass (n, s) = (M / 16^pass, 16^pass), p' = lt / s,
+//       j = 3 j' + jA - 1 (< 12): tw[jA (p' + j' n/16) M/n];  j = 12 + jB - 1: tw[jB p' 4M/n]
+//   rtp[(2 j + side) TPF + lt]: k = 1 + lt + TPF j (< M/2): side 0 rt[k], side 1 rt[M-k];
+//   rtp[2 NPAIR TPF + {0,1,2,3}] = rt[0], rt[M], rt[M/2], tw[0]
+void stft_tables(int N, const std::vector<float>& tw, const std::vector<float>& rt, std::vector<float>* twp,
+                 std::vector<float>* rtp) {
+    const int M = N / 2, TPF = M / 16;
+    const int npass = M == 4096 ? 3 : M == 1024 ? 2 : 0;
+    if (!npass) throw HipError("stft_tables: unsupported size");
+    auto put = [](std::vector<float>* v, size_t i, const float* src) {
+        (*v)[2 * i] = src[0];
+        (*v)[2 * i + 1] = src[1];
+    };
+    twp->assign((size_t)2 * 15 * TPF * npass, 0.0f);
+    for (int pass = 0, n = M, s = 1; pass < npass; pass++, n /= 16, s *= 16) {
+        const int m1 = n / 16, tA = M / n, tB = 4 * (M / n);
+        for (int lt = 0; lt < TPF; lt++) {
+            const int pp = lt / s;
+            for (int jp = 0; jp < 4; jp++)
+                for (int ja = 1; ja <= 3; ja++)
+                    put(twp, (size_t)(15 * pass + 3 * jp + ja - 1) * TPF + lt,
+                        &tw[2 * (size_t)(ja * (pp + jp * m1) * tA)]);
+            for (int jb = 1; jb <= 3; jb++)
+                put(twp, (size_t)(15 * pass + 12 + jb - 1) * TPF + lt, &tw[2 * (size_t)(jb * pp * tB)]);
+        }
+    }
+    const int npair = (M / 2 + TPF - 1) / TPF, sp = npair * 2 * TPF;
+    rtp->assign((size_t)2 * (sp + 4), 0.0f);
+    for (int j = 0; j < npair; j++)
+        for (int lt = 0; lt < TPF; lt++) {
+            const int k = 1 + lt + TPF * j;
+            if (k >= M / 2) continue;
+            put(rtp, (size_t)(2 * j) * TPF + lt, &rt[2 * (size_t)k]);
+            put(rtp, (size_t)(2 * j + 1) * TPF + lt, &rt[2 * (size_t)(M - k)]);
+        }
+    put(rtp, (size_t)sp + 0, &rt[0]);
+    put(rtp, (size_t)sp + 1, &rt[2 * (size_t)M]);
+    put(rtp, (size_t)sp + 2, &rt[2 * (size_t)(M / 2)]);
+    put(rtp, (size_t)sp + 3, &tw[0]);
+}
+
 // host launcher (the runtime owns all buffers; see runtime.hip)
 void launch_stft(int nfft, bool frame_max, const float* samples, const uint64_t* frame_pfx, int n_tracks,
                  uint64_t total_frames, const uint64_t* src_off, const float* gain, int hop, const float* window,
-                 const cx* tw, const cx* rt, float* mags, const uint64_t* mag_row0, int stride, float* fmax,
+                 const cx* twp, const cx* rtp, float* mags, const uint64_t* mag_row0, int stride, float* fmax,
                  hipStream_t st) {
     if (total_frames == 0) return;
     const dim3 block(256);
@@ -178,13 +318,13 @@ void launch_stft(int nfft, bool frame_max, const float* samples, const uint64_t*
         const dim3 grid((unsigned)((total_frames + 3) / 4));
         if (frame_max)
             hipLaunchKernelGGL((k_stft_mag<2048, true>), grid, block, 0, st, samples, frame_pfx, n_tracks,
-                               total_frames, src_off, gain, hop, window, tw, rt, mags, mag_row0, stride, fmax);
+                               total_frames, src_off, gain, hop, window, twp, rtp, mags, mag_row0, stride, fmax);
         else
             hipLaunchKernelGGL((k_stft_mag<2048, false>), grid, block, 0, st, samples, frame_pfx, n_tracks,
-                               total_frames, src_off, gain, hop, window, tw, rt, mags, mag_row0, stride, fmax);
+                               total_frames, src_off, gain, hop, window, twp, rtp, mags, mag_row0, stride, fmax);
     } else if (nfft == 8192) {
         hipLaunchKernelGGL((k_stft_mag<8192, false>), dim3((unsigned)total_frames), block, 0, st, samples, frame_pfx,
-                           n_tracks, total_frames, src_off, gain, hop, window, tw, rt, mags, mag_row0, stride, fmax);
+                           n_tracks, total_frames, src_off, gain, hop, window, twp, rtp, mags, mag_row0, stride, fmax);
     }
 }
 

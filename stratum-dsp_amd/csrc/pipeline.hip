@@ -476,8 +476,8 @@ void Pipeline::tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPa
     Timers tm;
     tm.init(d_);
     tm.mark(0);
-    launch_stft(FS, true, in.samples, o.d_fpfx, P_T, total, d_src, d_gain, hop, tb.window.as<float>(), tb.tw.as<cx>(),
-                tb.rt.as<cx>(), o.mags, o.d_fpfx, STRIDE2, o.fmax, d_.stream);
+    launch_stft(FS, true, in.samples, o.d_fpfx, P_T, total, d_src, d_gain, hop, tb.window.as<float>(), tb.stft_tw.as<cx>(),
+                tb.stft_rt.as<cx>(), o.mags, o.d_fpfx, STRIDE2, o.fmax, d_.stream);
     SDSP_HIP_CHECK(hipGetLastError());
     tm.mark(1);
     o.stft_launch = total ? 1 : 0;
@@ -800,8 +800,8 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         kt.mark(7);
         SDSP_HIP_CHECK(hipStreamWaitEvent(st2, kt.ev[7], 0));
         kt.mark(0, st2);
-        launch_stft(KFS, false, d_samples, d_kpfx, NK, total8, d_ksrc, d_kgain, KHOP, t8.window.as<float>(), t8.tw.as<cx>(),
-                    t8.rt.as<cx>(), mags8, d_kpfx, STRIDE8, nullptr, st2);
+        launch_stft(KFS, false, d_samples, d_kpfx, NK, total8, d_ksrc, d_kgain, KHOP, t8.window.as<float>(), t8.stft_tw.as<cx>(),
+                    t8.stft_rt.as<cx>(), mags8, d_kpfx, STRIDE8, nullptr, st2);
         SDSP_HIP_CHECK(hipGetLastError());
         kt.mark(1, st2);
         const int B8 = KFS / 2 + 1;

@@ -43,6 +43,14 @@ FftTables& DeviceCtx::tables(int N, bool with_window) {
         for (int i = 0; i < N; i++) w[(size_t)i] = sdsp_hann_f32(i, N);  // extractor.rs:318-323
         t->window.ensure(w.size() * 4);
         SDSP_HIP_CHECK(hipMemcpy(t->window.p, w.data(), w.size() * 4, hipMemcpyHostToDevice));
+        std::vector<float> tw(2 * (size_t)(N / 2)), rt((size_t)N + 2), a, b;
+        sdsp_fft_twiddles(N / 2, tw.data());
+        sdsp_rfft_twiddles(N, rt.data());
+        stft_tables(N, tw, rt, &a, &b);
+        t->stft_tw.ensure(a.size() * 4);
+        t->stft_rt.ensure(b.size() * 4);
+        SDSP_HIP_CHECK(hipMemcpy(t->stft_tw.p, a.data(), a.size() * 4, hipMemcpyHostToDevice));
+        SDSP_HIP_CHECK(hipMemcpy(t->stft_rt.p, b.data(), b.size() * 4, hipMemcpyHostToDevice));
     }
     return *t;
 }
@@ -243,7 +251,7 @@ int32_t sdsp_debug_stft(const float* host_x, uint64_t n, uint64_t nfft, uint64_t
         SDSP_HIP_CHECK(hipMemcpy(g.p, &gain, 4, hipMemcpyHostToDevice));
         SDSP_HIP_CHECK(hipMemcpy(row0.p, &r0, 8, hipMemcpyHostToDevice));
         launch_stft((int)nfft, nfft == 2048, x.as<float>(), pfx.as<uint64_t>(), 1, frames, off.as<uint64_t>(),
-                    g.as<float>(), (int)hop, tb.window.as<float>(), tb.tw.as<cx>(), tb.rt.as<cx>(), mags.as<float>(),
+                    g.as<float>(), (int)hop, tb.window.as<float>(), tb.stft_tw.as<cx>(), tb.stft_rt.as<cx>(), mags.as<float>(),
                     row0.as<uint64_t>(), stride, fmax.as<float>(), c.stream);
         SDSP_HIP_CHECK(hipGetLastError());
         SDSP_HIP_CHECK(hipStreamSynchronize(c.stream));

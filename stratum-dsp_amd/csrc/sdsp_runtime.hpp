@@ -53,6 +53,8 @@ struct FftTables {
     DevBuf tw;      // M-point complex twiddles (M = N/2)
     DevBuf rt;      // N/2+1 real-FFT post twiddles
     DevBuf window;  // N-point symmetric Hann (STFT sizes only)
+    DevBuf stft_tw; // STFT sizes: the same twiddle values re-laid out per thread (k_stft.hip)
+    DevBuf stft_rt; // STFT sizes: post twiddles in the kernel's pair order + specials
 };
 
 struct StageTimer;
@@ -74,6 +76,11 @@ struct DeviceCtx {
 };
 
 DeviceCtx& device_ctx(int device);
+
+// Per-thread STFT twiddle tables (k_stft.hip), built from the sdsp_fft_spec.h tables (tw: N/2
+// complex, rt: N/2+1 complex, interleaved) so every value is bit-identical to the spec's.
+void stft_tables(int N, const std::vector<float>& tw, const std::vector<float>& rt, std::vector<float>* twp,
+                 std::vector<float>* rtp);
 
 // ---- kernel launchers (defined next to their kernels) ----
 void launch_stft(int nfft, bool frame_max, const float* samples, const uint64_t* frame_pfx, int n_tracks,
