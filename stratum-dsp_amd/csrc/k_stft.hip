@@ -137,7 +137,7 @@ __global__ __launch_bounds__(256) void k_stft_mag(const float* __restrict__ samp
     f2* buf = lds + fl * PADM;
     const __amdgpu_buffer_rsrc_t rx = rsrc_of(samples + src_off[trk] + f * (uint64_t)hop, 4u * NFFT);
     const __amdgpu_buffer_rsrc_t rw = rsrc_of(window, 4u * NFFT);
-    const __amdgpu_buffer_rsrc_t rtw = rsrc_of(twp, 8u * 15u * TPF * S::NPASS);
+    const __amdgpu_buffer_rsrc_t rtw = rsrc_of(twp, 8u * 15u * (TPF + TPF / 16 + 1));
     const __amdgpu_buffer_rsrc_t rrt = rsrc_of(rtp, 8u * (S::RT_SPECIAL + 4));
     const int vo = 8 * lt;  // every table below is [item][lane] with 8-byte entries
 
@@ -163,11 +163,20 @@ __global__ __launch_bounds__(256) void k_stft_mag(const float* __restrict__ samp
     for (int pass = 1; pass < S::NPASS; pass++) {
         const int s = pass == 1 ? 16 : 256;
         const int m1 = (pass == 1 ? M / 16 : M / 256) / 16;  // n / 16
-        const int q = lt % s, pp = lt / s;
+        const int q = lt % s, pp = pass == 2 ? 0 : lt / s;  // lt < TPF = 256 = s on pass 2
         // reads x[q + s pp + s m1 k]; s m1 is a multiple of 16, so lpad = lpad(q + s pp) + (17/16) s m1 k
         const int rb = lpad(q + s * pp), rs = s * m1 + (s * m1) / 16;
 #pragma unroll
-        for (int j = 0; j < 15; j++) w[j] = ld_f2(rtw, vo, 8 * TPF * (15 * pass + j));
+        for (int j = 0; j < 15; j++) {
+            // pass 1: one entry per p' (TPF/16 of them, shared by 16 lanes); pass 2: p' = 0 for
+            // every lane, so the 15 twiddles are wave-uniform scalar loads
+            if (pass == 1)
+                w[j] = ld_f2(rtw, 8 * pp, 8 * (15 * TPF + j * (TPF / 16)));
+            else {
+                const cx t = twp[15 * TPF + 15 * (TPF / 16) + j];
+                w[j] = f2{t.re, t.im};
+            }
+        }
 #pragma unroll
         for (int k = 0; k < 16; k++) v[k] = buf[rb + rs * k];
         __syncthreads();
@@ -266,7 +275,8 @@ __global__ __launch_bounds__(256) void k_stft_mag(const float* __restrict__ samp
 }
 
 // Host: per-thread twiddle layouts for k_stft_mag, from the spec's tables (values unchanged).
-//   twp[(15 pass + j) TPF + lt]: pass (n, s) = (M / 16^pass, 16^pass), p' = lt / s,
+//   twp[base(pass) + j (TPF/s) + p']: pass (n, s) = (M / 16^pass, 16^pass), p' = lt / s,
+//       base(pass) = 15 sum_{q < pass} TPF / 16^q,
 //       j = 3 j' + jA - 1 (< 12): tw[jA (p' + j' n/16) M/n];  j = 12 + jB - 1: tw[jB p' 4M/n]
 //   rtp[(2 j + side) TPF + lt]: k = 1 + lt + TPF j (< M/2): side 0 rt[k], side 1 rt[M-k];
 //   rtp[2 NPAIR TPF + {0,1,2,3}] = rt[0], rt[M], rt[M/2], tw[0]
@@ -279,18 +289,20 @@ void stft_tables(int N, const std::vector<float>& tw, const std::vector<float>& 
         (*v)[2 * i] = src[0];
         (*v)[2 * i + 1] = src[1];
     };
-    twp->assign((size_t)2 * 15 * TPF * npass, 0.0f);
+    size_t len = 0;
+    for (int pass = 0, s = 1; pass < npass; pass++, s *= 16) len += (size_t)15 * (TPF / s);
+    twp->assign(2 * len, 0.0f);
+    size_t base = 0;
     for (int pass = 0, n = M, s = 1; pass < npass; pass++, n /= 16, s *= 16) {
-        const int m1 = n / 16, tA = M / n, tB = 4 * (M / n);
-        for (int lt = 0; lt < TPF; lt++) {
-            const int pp = lt / s;
+        const int m1 = n / 16, tA = M / n, tB = 4 * (M / n), npp = TPF / s;
+        for (int pp = 0; pp < npp; pp++) {
             for (int jp = 0; jp < 4; jp++)
                 for (int ja = 1; ja <= 3; ja++)
-                    put(twp, (size_t)(15 * pass + 3 * jp + ja - 1) * TPF + lt,
-                        &tw[2 * (size_t)(ja * (pp + jp * m1) * tA)]);
+                    put(twp, base + (size_t)(3 * jp + ja - 1) * npp + pp, &tw[2 * (size_t)(ja * (pp + jp * m1) * tA)]);
             for (int jb = 1; jb <= 3; jb++)
-                put(twp, (size_t)(15 * pass + 12 + jb - 1) * TPF + lt, &tw[2 * (size_t)(jb * pp * tB)]);
+                put(twp, base + (size_t)(12 + jb - 1) * npp + pp, &tw[2 * (size_t)(jb * pp * tB)]);
         }
+        base += (size_t)15 * npp;
     }
     const int npair = (M / 2 + TPF - 1) / TPF, sp = npair * 2 * TPF;
     rtp->assign((size_t)2 * (sp + 4), 0.0f);
