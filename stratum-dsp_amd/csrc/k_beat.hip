@@ -526,4 +526,61 @@ void launch_beat(const int* tracks, int n_items, const uint32_t* onsets, const u
                        bpm, conf, scratch, beat_off, beat_cap, beats, downs, out);
 }
 
+// Gathers the tracks' beat and downbeat lists (capacity-strided in `beats` / `downs`) into
+// dense arrays so the host downloads only what was produced: one workgroup; pfx[0..n] and
+// pfx[n+1..2n+1] are the exclusive prefixes of the beat and downbeat counts (0 for failed
+// tracks).  Integer sums, so the scan order is immaterial.
+__global__ __launch_bounds__(1024) void k_beat_compact(int n, const BeatOut* __restrict__ out,
+                                                       const uint64_t* __restrict__ beat_off,
+                                                       const float* __restrict__ beats, const float* __restrict__ downs,
+                                                       uint64_t* __restrict__ pfx, float* __restrict__ cb,
+                                                       float* __restrict__ cd) {
+    __shared__ uint64_t sb[1024], sd[1024];
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const int per = (n + nt - 1) / nt, i0 = tid * per, i1 = min(n, i0 + per);
+    uint64_t ab = 0, ad = 0;
+    for (int i = i0; i < i1; i++) {
+        const BeatOut r = out[i];
+        ab += r.ok > 0 ? (uint64_t)r.n_beats : 0;
+        ad += r.ok > 0 ? (uint64_t)r.n_down : 0;
+    }
+    sb[tid] = ab;
+    sd[tid] = ad;
+    __syncthreads();
+    for (int o = 1; o < nt; o <<= 1) {  // inclusive Hillis-Steele scan
+        const uint64_t vb = tid >= o ? sb[tid - o] : 0, vd = tid >= o ? sd[tid - o] : 0;
+        __syncthreads();
+        sb[tid] += vb;
+        sd[tid] += vd;
+        __syncthreads();
+    }
+    uint64_t pb = sb[tid] - ab, pd = sd[tid] - ad;
+    for (int i = i0; i < i1; i++) {
+        const BeatOut r = out[i];
+        pfx[i] = pb;
+        pfx[n + 1 + i] = pd;
+        pb += r.ok > 0 ? (uint64_t)r.n_beats : 0;
+        pd += r.ok > 0 ? (uint64_t)r.n_down : 0;
+    }
+    if (tid == nt - 1) {
+        pfx[n] = sb[tid];
+        pfx[2 * n + 1] = sd[tid];
+    }
+    __syncthreads();
+    const int lane = tid & 63, w = tid >> 6, nw = nt >> 6;
+    for (int i = w; i < n; i += nw) {  // one wave per track
+        const BeatOut r = out[i];
+        if (r.ok <= 0) continue;
+        const uint64_t ob = pfx[i], od = pfx[n + 1 + i], src = beat_off[i];
+        for (int k = lane; k < r.n_beats; k += 64) cb[ob + k] = beats[src + k];
+        for (int k = lane; k < r.n_down; k += 64) cd[od + k] = downs[src + k];
+    }
+}
+
+void launch_beat_compact(int n, const BeatOut* out, const uint64_t* beat_off, const float* beats, const float* downs,
+                         uint64_t* pfx, float* cb, float* cd, hipStream_t st) {
+    if (n == 0) return;
+    hipLaunchKernelGGL(k_beat_compact, dim3(1), dim3(1024), 0, st, n, out, beat_off, beats, downs, pfx, cb, cd);
+}
+
 }  // namespace sdsp

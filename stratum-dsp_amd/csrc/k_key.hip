@@ -98,6 +98,29 @@ __global__ __launch_bounds__(MASK_T) void k_mask(float* __restrict__ mags, int s
 // contribute x = 0 (prefix + 0 == prefix, so P[min(t+M+1, F)] is read as P[t+M+1]), and
 // prefixes of negative index are the ring's initial zeros (== P[0]) because slot (t-M) mod R
 // is not written before t >= M.  R loads are issued ahead of each unrolled block.
+// One masked element: window sum a over `den` frames and the raw value xr -> xr * mask
+// (extractor.rs:1281-1285 then 1320-1340).  For the full window (2M+1 frames) a/(2M+1) is one
+// product and one FMA correction, == the correctly rounded quotient for every f32 a in
+// {0} U [2^-90, 2^120] (tools/check_div.c: exhaustive, every odd window 3..25); otherwise the
+// IEEE division.
+template <int M, int PW>
+__device__ __forceinline__ float mask_elem(float a, int64_t den, float xr, float p, float inv_w) {
+    float hm;
+    if (den == 2 * M + 1 && (a == 0.0f || (a >= 0x1p-90f && a <= 0x1p120f))) {
+        const float q0 = a * inv_w;
+        hm = __builtin_fmaf(__builtin_fmaf(-q0, (float)(2 * M + 1), a), inv_w, q0);
+    } else {
+        hm = a / (float)(den > 1 ? den : 1);
+    }
+    const float x = max_bnn(xr, 0.0f);
+    const float h = max_bnn(hm, 0.0f);
+    const float r = max_bnn(x - h, 0.0f);
+    const float hp = mask_pow<PW>(h, p);
+    const float rp = mask_pow<PW>(r, p);
+    const float m = hp / (hp + rp + 1e-12f);
+    return x * m;
+}
+
 template <int M, int PW>
 __global__ __launch_bounds__(MASK_T) void k_mask_r(float* __restrict__ mags, int stride, int B,
                                                     const uint64_t* __restrict__ frame_pfx,
@@ -112,7 +135,6 @@ __global__ __launch_bounds__(MASK_T) void k_mask_r(float* __restrict__ mags, int
     if (b >= B || F <= 0) return;
     float* col = mags + frame_pfx[trk] * (uint64_t)stride + b;
     const float p = sd_maxf(power, 1.0f);
-    const float eps = 1e-12f;
     const float inv_w = 1.0f / (float)(2 * M + 1);
     float P[R], X[RX];
 #pragma unroll
@@ -120,25 +142,8 @@ __global__ __launch_bounds__(MASK_T) void k_mask_r(float* __restrict__ mags, int
 #pragma unroll
     for (int j = 0; j < RX; j++) X[j] = 0.0f;
     float prev = 0.0f;
-    // one output element: window sum a over `den` frames -> masked value
     auto emit = [&](float a, int64_t den, float xr, int64_t t) {
-        float hm;
-        // full window (2M+1 frames): a/(2M+1) by one product and one FMA correction, == the
-        // correctly rounded quotient for every f32 a in {0} U [2^-90, 2^120] (tools/check_div.c:
-        // exhaustive, every odd window 3..25); otherwise the IEEE division
-        if (den == 2 * M + 1 && (a == 0.0f || (a >= 0x1p-90f && a <= 0x1p120f))) {
-            const float q0 = a * inv_w;
-            hm = __builtin_fmaf(__builtin_fmaf(-q0, (float)(2 * M + 1), a), inv_w, q0);
-        } else {
-            hm = a / (float)(den > 1 ? den : 1);
-        }
-        const float x = max_bnn(xr, 0.0f);
-        const float h = max_bnn(hm, 0.0f);
-        const float r = max_bnn(x - h, 0.0f);
-        const float hp = mask_pow<PW>(h, p);
-        const float rp = mask_pow<PW>(r, p);
-        const float m = hp / (hp + rp + eps);
-        col[t * stride] = x * m;
+        col[t * stride] = mask_elem<M, PW>(a, den, xr, p, inv_w);
     };
     for (int64_t base = 0; base < F + M; base += R) {
         float xv[R];
@@ -189,7 +194,6 @@ __global__ __launch_bounds__(HP_FRAMES) void k_hpcp(const float* __restrict__ ma
                                                     const HarmEntry* __restrict__ harm, float* __restrict__ chroma,
                                                     float* __restrict__ energy) {
     __shared__ float tile[HP_FRAMES][HP_CW + 1];
-    __shared__ float pc[12][HP_FRAMES];
     const uint64_t gb = blockIdx.x;
     const int it = find_track(tile_pfx, n_items, gb);
     const int trk = tracks[it];
@@ -262,6 +266,10 @@ __global__ __launch_bounds__(HP_FRAMES) void k_hpcp(const float* __restrict__ ma
             m1 = m;
         }
     }
+    // pitch-class accumulators reuse the staging tile (every read of it is done)
+    __syncthreads();
+    float(*pc)[HP_FRAMES] = reinterpret_cast<float(*)[HP_FRAMES]>(&tile[0][0]);
+    static_assert(sizeof(tile) >= sizeof(float) * 12 * HP_FRAMES, "pc fits the staging tile");
     if (!valid) return;
 #pragma unroll
     for (int q = 0; q < 12; q++) pc[q][i] = 0.0f;

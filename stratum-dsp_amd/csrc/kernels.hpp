@@ -154,6 +154,9 @@ void launch_multires(const int* tracks, int n_items, const float* c256, const in
 void launch_beat(const int* tracks, int n_items, const uint32_t* onsets, const uint64_t* on_off, const int* on_n,
                  uint32_t sr, const float* bpm, const float* conf, float* scratch, const uint64_t* beat_off,
                  const int* beat_cap, float* beats, float* downs, BeatOut* out, hipStream_t st);
+// dense beat/downbeat lists: pfx has 2 (n + 1) entries (beats, then downbeats)
+void launch_beat_compact(int n, const BeatOut* out, const uint64_t* beat_off, const float* beats, const float* downs,
+                         uint64_t* pfx, float* cb, float* cd, hipStream_t st);
 void launch_mask(float* mags, int stride, int B, const uint64_t* frame_pfx, const int* tracks, int n_items, int margin,
                  float power, hipStream_t st);
 void launch_hpcp(const float* mags, const uint64_t* frame_pfx, const uint64_t* tile_pfx, const int* tracks,

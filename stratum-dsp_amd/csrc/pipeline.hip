@@ -14,6 +14,7 @@
 //   D  beat grid; join the key stream                    -> host reads results (sync 3)
 // No stage falls back to the CPU; host code only plans offsets and formats the result.
 #include <algorithm>
+#include <cmath>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -31,8 +32,17 @@ namespace sdsp {
 
 namespace {
 
-constexpr int STRIDE2 = 1028;  // 1025 bins, 16-B rows
-constexpr int STRIDE8 = 4100;  // 4097 bins
+// Spectrogram row strides (floats; multiples of 4 for 16-B rows).  The key spectrogram's rows
+// are 16 KiB + 256 B apart: at 16 KiB + 16 B the mask's column streams (one 256-B row segment
+// per wave per frame) run 1.5x slower (profiles/README.md, stride sweep).  SDSP_STRIDE2 /
+// SDSP_STRIDE8 override them for layout experiments.
+static int env_stride(const char* name, int dflt, int min) {
+    const char* e = std::getenv(name);
+    const int v = e ? std::atoi(e) : dflt;
+    return v >= min && v % 4 == 0 ? v : dflt;
+}
+static const int STRIDE2 = env_stride("SDSP_STRIDE2", 1028, 1025);  // 1025 bins
+static const int STRIDE8 = env_stride("SDSP_STRIDE8", 4160, 4097);  // 4097 bins
 constexpr int SUPPORT_HMAX = 8;
 
 uint64_t next_pow2(uint64_t n) {
@@ -434,14 +444,30 @@ void Pipeline::run(const float* d_samples, const std::vector<uint64_t>& in_off, 
     };
     times_ = sdsp_stage_times{};
     auto t0 = std::chrono::steady_clock::now();
+    // equal shares: the fewest sub-batches that fit the budget, each near total / count (a
+    // short last sub-batch runs at a fraction of the chip)
+    std::vector<double> need(T, 0.0);
+    double total_need = 0;
     for (size_t i = 0; i < T; i++) {
         if (res[i].status != SDSP_OK) continue;
         const double n = (double)n_raw[i];
-        const double need = n / hop * (STRIDE2 * 4.0 * 1.3 + 4 * 70.0) + n / khop * STRIDE8 * 4.0 +
-                            (n / 256 + n / 1024) * STRIDE2 * 4.0 + 1e6;
-        if (!cur.empty() && acc + need > budget) flush();
+        need[i] = n / hop * (STRIDE2 * 4.0 * 1.3 + 4 * 70.0) + n / khop * STRIDE8 * 4.0 +
+                  (n / 256 + n / 1024) * STRIDE2 * 4.0 + 1e6;
+        total_need += need[i];
+    }
+    const double parts = std::max(1.0, std::ceil(total_need / budget));
+    const double share = total_need / parts;
+    double cum = 0;
+    int part = 0;
+    for (size_t i = 0; i < T; i++) {
+        if (res[i].status != SDSP_OK) continue;
+        // a track belongs to the share its midpoint falls in
+        const int p = (int)std::min(parts - 1.0, std::floor((cum + 0.5 * need[i]) / share));
+        if (!cur.empty() && (p != part || acc + need[i] > budget)) flush();
+        part = p;
         cur.push_back((int)i);
-        acc += need;
+        acc += need[i];
+        cum += need[i];
     }
     flush();
     times_.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -679,12 +705,27 @@ void Pipeline::tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPa
 
 namespace sdsp {
 
+// SDSP_HOST_TRACE=1: host wall time between the sub-batch's synchronisation points (stderr)
+struct HostTrace {
+    bool on = std::getenv("SDSP_HOST_TRACE") != nullptr;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now(), tp = t0;
+    void operator()(const char* tag) {
+        if (!on) return;
+        const auto t = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[sdsp host] %-12s +%8.3f ms  (%8.3f)\n", tag,
+                     std::chrono::duration<double, std::milli>(t - tp).count(),
+                     std::chrono::duration<double, std::milli>(t - t0).count());
+        tp = t;
+    }
+};
+
 void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in_off, const std::vector<uint64_t>& n_raw,
                          const std::vector<int>& idx, std::vector<TrackRes>& res) {
     const int T = (int)idx.size();
     const int FS = 2048;
     const int HOP = (int)cfg_.hop_size;
     hipStream_t st = d_.stream;
+    HostTrace htr;
     Timers tm;
     tm.init(d_);
     tm.mark(0);
@@ -717,6 +758,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     SDSP_HIP_CHECK(hipGetLastError());
     std::vector<float> gain_h = c_.down(d_gain, (size_t)T);
     std::vector<uint64_t> ts = c_.down(d_ts, (size_t)T), te = c_.down(d_te, (size_t)T);
+    htr("A");
     tm.mark(1);
     // remaining tracks (non-empty after trimming)
     std::vector<int> R;  // positions in idx
@@ -907,6 +949,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     SDSP_HIP_CHECK(hipGetLastError());
     std::vector<TempoEst> best = c_.down(bo.est, (size_t)NR);
     std::vector<int> en_h = c_.down(d_en, (size_t)NR);
+    htr("B");
     tm.mark(3);
     // final tempo per track (tempogram -> legacy -> 0; legacy is never consulted on the default path,
     // see DESIGN.md "legacy estimator")
@@ -1000,6 +1043,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         }
     }
     std::vector<float> fbpm_h = c_.down(d_fbpm, (size_t)NR), fconf_h = c_.down(d_fconf, (size_t)NR);
+    htr("C");
     tm.mark(4);
     // ---------------- D: beat grid ----------------
     std::vector<int> ident((size_t)NR);
@@ -1029,14 +1073,23 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     if (NK > 0) {  // join the key stream
         SDSP_HIP_CHECK(hipStreamWaitEvent(st, kt.ev[2], 0));
         kout = c_.down(d_kout, (size_t)NK);
+        htr("E join");
         times_.stft8192_ms += kt.ms(0, 1);
         times_.key_ms += kt.ms(1, 2);
     }
     // ---------------- results ----------------
+    uint64_t* d_bpfx = c_.dev<uint64_t>("D.bpfx", 2 * ((size_t)NR + 1));
+    float* d_cbeats = c_.dev<float>("D.cbeats", boff[(size_t)NR]);
+    float* d_cdowns = c_.dev<float>("D.cdowns", boff[(size_t)NR]);
+    launch_beat_compact(NR, d_bout, d_boff, d_beats, d_downs, d_bpfx, d_cbeats, d_cdowns, st);
+    SDSP_HIP_CHECK(hipGetLastError());
     std::vector<BeatOut> bout = c_.down(d_bout, (size_t)NR);
-    std::vector<float> beats_h = c_.down(d_beats, boff[(size_t)NR]), downs_h = c_.down(d_downs, boff[(size_t)NR]);
+    std::vector<uint64_t> bpfx = c_.down(d_bpfx, 2 * ((size_t)NR + 1));
+    std::vector<float> beats_h = c_.down(d_cbeats, bpfx[(size_t)NR]);
+    std::vector<float> downs_h = c_.down(d_cdowns, bpfx[2 * (size_t)NR + 1]);
     std::vector<float> cand_h;
     if (cfg_.emit_tempogram_candidates) cand_h = c_.down(bo.cand, (size_t)NR * (size_t)bin.cand_cap * 4);
+    htr("D down");
     times_.beat_ms += tm.ms(4, 5);
     for (int i = 0; i < NR; i++) {
         TrackRes& r = res[(size_t)idx[(size_t)R[(size_t)i]]];
@@ -1049,8 +1102,9 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
             continue;
         }
         if (b.ok > 0) {
-            r.beats.assign(beats_h.begin() + (long)boff[(size_t)i], beats_h.begin() + (long)(boff[(size_t)i] + b.n_beats));
-            r.downs.assign(downs_h.begin() + (long)boff[(size_t)i], downs_h.begin() + (long)(boff[(size_t)i] + b.n_down));
+            const uint64_t ob = bpfx[(size_t)i], od = bpfx[(size_t)NR + 1 + (size_t)i];
+            r.beats.assign(beats_h.begin() + (long)ob, beats_h.begin() + (long)(ob + b.n_beats));
+            r.downs.assign(downs_h.begin() + (long)od, downs_h.begin() + (long)(od + b.n_down));
             r.stability = b.stability;
         }
         if (cfg_.emit_tempogram_candidates && best[(size_t)i].ok) {
@@ -1073,6 +1127,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         r.key_conf = ko.conf;
         r.key_clarity = ko.clarity;
     }
+    htr("results");
 }
 
 namespace {

@@ -104,6 +104,19 @@ def test_ragged_batch_matches_single():
         assert not parity.diff_results(r, ref), (i, parity.diff_results(r, ref))
 
 
+def test_sub_batches_match_one_batch(monkeypatch):
+    """A 1 GB HBM budget splits the batch into several sub-batches (equal shares, ragged
+    lengths); every result must equal the single-sub-batch run's."""
+    tracks = [synth.make_track(300 + s, seconds=20.0 + 3.0 * (s % 7))[0] for s in range(40)]
+    whole = sdsp.analyze_batch(tracks, 44100)
+    monkeypatch.setenv("SDSP_HBM_BUDGET_GB", "1")
+    split = sdsp.analyze_batch(tracks, 44100)
+    for i, (a, b) in enumerate(zip(whole, split)):
+        a = {k: v for k, v in a.items() if k != "metadata"} | {"d": a["metadata"]["duration_seconds"]}
+        b = {k: v for k, v in b.items() if k != "metadata"} | {"d": b["metadata"]["duration_seconds"]}
+        assert a == b, i
+
+
 def test_device_generated_3min_tracks():
     """Device-resident batch (the bench path) on two 3-min synthetic tracks, checked on the host."""
     n, L = 2, 44100 * 180
