@@ -196,6 +196,30 @@ static __constant__ const sd_logtab_t SD_LOGTAB_D[128] = SDSP_LOGTAB_INIT;
 #endif
 static const sd_logtab_t SD_LOGTAB_H[128] = SDSP_LOGTAB_INIT;
 
+/* Shared core for a finite normal or subnormal x > 0 given its exponent and 23-bit mantissa
+ * (subnormals already normalised) and a {c, 1/c, ln c} table (sdsp_logtab.h contents). */
+SD_HD float sd_logf_core(uint32_t mant, int e, const sd_logtab_t* tab) {
+    const int i = (int)(mant >> 16);
+    double m = sd_from_bits_d(0x3ff0000000000000ull | ((uint64_t)mant << 29));
+    if (i >= 53) {
+        m = m * 0.5;
+        e = e + 1;
+    }
+    const sd_logtab_t t = tab[i];
+    const double r = (m - t.c) * t.inv;
+    double p = -0.125;
+    p = __builtin_fma(p, r, 1.0 / 7.0);
+    p = __builtin_fma(p, r, -1.0 / 6.0);
+    p = __builtin_fma(p, r, 0.2);
+    p = __builtin_fma(p, r, -0.25);
+    p = __builtin_fma(p, r, 1.0 / 3.0);
+    p = __builtin_fma(p, r, -0.5);
+    p = __builtin_fma(p, r, 1.0);
+    p = p * r;
+    const double ed = (double)e;
+    return (float)__builtin_fma(ed, SD_LN2_HI, __builtin_fma(ed, SD_LN2_LO, t.lg + p));
+}
+
 SD_HD float sd_logf(float x) {
     if (x != x) return x;
     if (x < 0.0f) return SD_NAN_F;
@@ -209,29 +233,19 @@ SD_HD float sd_logf(float x) {
         mant = (mant << k) & 0x7fffffu;
         e = -126 - k;
     }
-    const int i = (int)(mant >> 16);
-    double m = sd_from_bits_d(0x3ff0000000000000ull | ((uint64_t)mant << 29));
-    if (i >= 53) {
-        m = m * 0.5;
-        e = e + 1;
-    }
 #if defined(__HIP_DEVICE_COMPILE__)
-    const sd_logtab_t t = SD_LOGTAB_D[i];
+    return sd_logf_core(mant, e, SD_LOGTAB_D);
 #else
-    const sd_logtab_t t = SD_LOGTAB_H[i];
+    return sd_logf_core(mant, e, SD_LOGTAB_H);
 #endif
-    const double r = (m - t.c) * t.inv;
-    double p = -0.125;
-    p = __builtin_fma(p, r, 1.0 / 7.0);
-    p = __builtin_fma(p, r, -1.0 / 6.0);
-    p = __builtin_fma(p, r, 0.2);
-    p = __builtin_fma(p, r, -0.25);
-    p = __builtin_fma(p, r, 1.0 / 3.0);
-    p = __builtin_fma(p, r, -0.5);
-    p = __builtin_fma(p, r, 1.0);
-    p = p * r;
-    const double ed = (double)e;
-    return (float)__builtin_fma(ed, SD_LN2_HI, __builtin_fma(ed, SD_LN2_LO, t.lg + p));
+}
+
+/* sd_logf for x >= 1, +inf or NaN (e.g. ln(1 + max(v, 0))), with the table at `tab` (a copy in
+ * LDS on the device): the same arithmetic, without the branches for x <= 0 and subnormals. */
+SD_HD float sd_logf_ge1(float x, const sd_logtab_t* tab) {
+    if (!(x < SD_INF_F)) return x; /* +inf -> +inf, NaN -> NaN, as sd_logf */
+    const uint32_t b = sd_bits_f(x);
+    return sd_logf_core(b & 0x7fffffu, (int)(b >> 23) - 127, tab);
 }
 
 /* f32::log10 */

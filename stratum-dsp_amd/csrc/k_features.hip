@@ -27,7 +27,10 @@
 
 namespace sdsp {
 
-template <int CW, int W>
+// KK > 0: compile-time SuperFlux half width (the default 4) -- the previous frame's logs for
+// the chunk's windows are read once into registers and every bin's window max is taken from
+// them; KK = 0: runtime P.K with the per-bin window loop.
+template <int CW, int W, int KK>
 __global__ __launch_bounds__(FT_FRAMES) void k_features(const float* __restrict__ mags,
                                                         const float* __restrict__ fmax,
                                                         const uint64_t* __restrict__ frame_pfx,
@@ -41,6 +44,9 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const float* __restrict_
     constexpr int LS = W + 1;
     __shared__ float Mt[ROWS][LS];
     __shared__ float Lt[ROWS][LS];
+    __shared__ sd_logtab_t ltab[128];  // sd_logf's table, read per element by the staging
+    static_assert(KK == 0 || CW + 2 * KK <= W, "window halo must fit the ring");
+    for (int q = threadIdx.x; q < 128; q += FT_FRAMES) ltab[q] = SD_LOGTAB_D[q];
 
     const uint64_t gb = blockIdx.x;
     const int trk = find_track(tile_pfx, T, gb);
@@ -51,7 +57,7 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const float* __restrict_
     const int64_t f = f0 + i;
     const bool valid = f < F;
     const bool has_prev = valid && f >= 1;
-    const int K = P.K, B = P.B;
+    const int K = KK > 0 ? KK : P.K, B = P.B;
     const uint64_t g = g0 + (uint64_t)f;
 
     float e[4] = {0, 0, 0, 0}, h[4] = {0, 0, 0, 0}, sx[4] = {0, 0, 0, 0}, so = 0.0f;
@@ -88,15 +94,18 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const float* __restrict_
             const int r = sub + u * RSTEP;
             if (r < ROWS) {
                 Mt[r][slot] = nx[u];
-                Lt[r][slot] = sd_logf(1.0f + sd_maxf(nx[u], 0.0f));
+                Lt[r][slot] = sd_logf_ge1(1.0f + sd_maxf(nx[u], 0.0f), ltab);
             }
         }
     };
-    // prologue: bins [0, K) (K <= CW)
+    __syncthreads();  // ltab
+    // prologue: bins [0, K) (K <= CW); the ring slots of bins [-K, 0) read as L = 0
     if (jj < K) {
         load(0);
         commit(0);
     }
+    if (KK > 0)
+        for (int q = threadIdx.x; q < ROWS * KK; q += FT_FRAMES) Lt[q / KK][W - KK + q % KK] = 0.0f;
     load(K);
     for (int c0 = 0; c0 < B; c0 += CW) {
         __syncthreads();  // previous step's readers are done with the slots overwritten here
@@ -105,7 +114,15 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const float* __restrict_
         if (c0 + CW < B) load(c0 + CW + K);
         const int nb = B - c0 < CW ? B - c0 : CW;
         if (!valid) continue;
-        for (int j = 0; j < nb; j++) {
+        // KK > 0: previous frame's L for bins [c0 - KK, c0 + CW + KK) (0 outside [0, B))
+        float Rw[KK > 0 ? CW + 2 * KK : 1];
+        if (KK > 0 && has_prev) {
+#pragma unroll
+            for (int q = 0; q < (KK > 0 ? CW + 2 * KK : 1); q++) Rw[q] = Lt[i][(c0 - KK + q) & (W - 1)];
+        }
+#pragma unroll
+        for (int j = 0; j < CW; j++) {
+            if (j >= nb) break;
             const int b = c0 + j;
             const int s = b & (W - 1);
             const float m = Mt[i + 1][s];
@@ -146,11 +163,19 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const float* __restrict_
                 const float cv = cn ? m / mx_c : 0.0f;
                 const float d = max_bnn(cv - pv, 0.0f);
                 so += d * d;
-                // SuperFlux, full band window [b-K, b+K] clipped to [0, B)
+                // SuperFlux, full band window [b-K, b+K] clipped to [0, B).  Every L >= +0 and
+                // max is an exact selection, so the max over the register window (entries
+                // outside [0, B) are +0) equals the reference's max from 0 over the clipped range.
                 const int lo = b - K < 0 ? 0 : b - K;
                 const int hi = b + K + 1 < B ? b + K + 1 : B;
                 float pm = 0.0f;
-                for (int q = lo; q < hi; q++) pm = max_bnn(pm, Lt[i][q & (W - 1)]);  // L is never NaN
+                if constexpr (KK > 0) {
+                    pm = Rw[j];
+#pragma unroll
+                    for (int q = 1; q <= 2 * KK; q++) pm = max_bnn(pm, Rw[j + q]);
+                } else {
+                    for (int q = lo; q < hi; q++) pm = max_bnn(pm, Lt[i][q & (W - 1)]);  // L is never NaN
+                }
                 const float df = max_bnn(lc - pm, 0.0f);
                 sx[0] += df * df;
 #pragma unroll
@@ -161,7 +186,13 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const float* __restrict_
                             const int lb = lo < P.bs[v] ? P.bs[v] : lo;
                             const int hb = hi > P.be[v] ? P.be[v] : hi;
                             pmb = 0.0f;
-                            for (int q = lb; q < hb; q++) pmb = max_bnn(pmb, Lt[i][q & (W - 1)]);
+                            if constexpr (KK > 0) {
+#pragma unroll
+                                for (int q = 0; q <= 2 * KK; q++)
+                                    if (b - KK + q >= lb && b - KK + q < hb) pmb = max_bnn(pmb, Rw[j + q]);
+                            } else {
+                                for (int q = lb; q < hb; q++) pmb = max_bnn(pmb, Lt[i][q & (W - 1)]);
+                            }
                         }
                         const float db = max_bnn(lc - pmb, 0.0f);
                         sx[v] += db * db;
@@ -194,11 +225,14 @@ void launch_features(const float* mags, const float* fmax, const uint64_t* frame
                      float* SFO, float* MEL, uint64_t total, hipStream_t st) {
     if (n_tiles == 0) return;
     // window must hold [c0-K, c0+CW+K): CW + 2K <= W
-    if (P.K <= 4)
-        hipLaunchKernelGGL((k_features<8, 16>), dim3((unsigned)n_tiles), dim3(FT_FRAMES), 0, st, mags, fmax,
+    if (P.K == 4)
+        hipLaunchKernelGGL((k_features<8, 16, 4>), dim3((unsigned)n_tiles), dim3(FT_FRAMES), 0, st, mags, fmax,
+                           frame_pfx, tile_pfx, T, P, mel, E, H, SFX, SFO, MEL, total);
+    else if (P.K <= 4)
+        hipLaunchKernelGGL((k_features<8, 16, 0>), dim3((unsigned)n_tiles), dim3(FT_FRAMES), 0, st, mags, fmax,
                            frame_pfx, tile_pfx, T, P, mel, E, H, SFX, SFO, MEL, total);
     else
-        hipLaunchKernelGGL((k_features<16, 32>), dim3((unsigned)n_tiles), dim3(FT_FRAMES), 0, st, mags, fmax,
+        hipLaunchKernelGGL((k_features<16, 32, 0>), dim3((unsigned)n_tiles), dim3(FT_FRAMES), 0, st, mags, fmax,
                            frame_pfx, tile_pfx, T, P, mel, E, H, SFX, SFO, MEL, total);
 }
 

@@ -16,7 +16,7 @@ import numpy as np
 from sdsp_abi import ERROR_NAMES, SdspConfig, SdspResult, SdspStageTimes, result_to_dict
 
 PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG, "lib", "libstratum_hip.so")
+LIB_PATH = os.environ.get("SDSP_LIB_PATH") or os.path.join(PKG, "lib", "libstratum_hip.so")  # override: layout/ablation builds
 _lib = None
 
 
