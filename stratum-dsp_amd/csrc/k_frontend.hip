@@ -53,69 +53,6 @@ __global__ void k_gain(const unsigned int* __restrict__ peak_bits, int T, float 
     gain[t] = g;
 }
 
-// ---- frame RMS: sqrt(sum_{k in frame} (x_k*gain)^2 / len), the sum folded in sample order ----
-// One thread per frame, RMS_ROWS frames per workgroup.  The frames' samples are staged through
-// LDS in RMS_KC-sample column chunks (row-contiguous, coalesced loads, RMS_KC loads in flight
-// per thread), then each thread folds its own row in order.  Overlapping frames re-read their
-// shared samples from L2 / Infinity Cache, not HBM.
-constexpr int RMS_ROWS = 256;
-constexpr int RMS_KC = 32;
-__global__ __launch_bounds__(RMS_ROWS) void k_frame_rms(const float* __restrict__ x,
-                                                        const uint64_t* __restrict__ src_off,
-                                                        const float* __restrict__ gain,
-                                                        const uint64_t* __restrict__ n_len,
-                                                        const uint64_t* __restrict__ frame_pfx, int T,
-                                                        uint64_t total, int fs, int hop, float* __restrict__ rms) {
-    __shared__ float tile[RMS_ROWS][RMS_KC + 1];
-    __shared__ uint64_t r_beg[RMS_ROWS];
-    __shared__ uint32_t r_len[RMS_ROWS];
-    __shared__ float r_gain[RMS_ROWS];
-    const int tid = threadIdx.x;
-    const uint64_t g = (uint64_t)blockIdx.x * RMS_ROWS + tid;
-    uint32_t len = 0;
-    if (g < total) {
-        const int trk = find_track(frame_pfx, T, g);
-        const uint64_t f = g - frame_pfx[trk];
-        const uint64_t n = n_len[trk];
-        const uint64_t s = f * (uint64_t)hop;
-        const uint64_t e = s + (uint64_t)fs < n ? s + (uint64_t)fs : n;
-        len = e > s ? (uint32_t)(e - s) : 0u;
-        r_beg[tid] = src_off[trk] + s;
-        r_gain[tid] = gain[trk];
-    } else {
-        r_beg[tid] = 0;
-        r_gain[tid] = 0.0f;
-    }
-    r_len[tid] = len;
-    float sum = 0.0f;
-    const int sub = tid / RMS_KC, j = tid % RMS_KC;
-    constexpr int RSTEP = RMS_ROWS / RMS_KC, NLD = RMS_ROWS / RSTEP;
-    __syncthreads();
-    float nx[NLD];
-    auto load = [&](int c0) {
-        const uint32_t k = (uint32_t)(c0 + j);
-#pragma unroll
-        for (int u = 0; u < NLD; u++) {
-            const int r = sub + u * RSTEP;
-            nx[u] = k < r_len[r] ? x[r_beg[r] + k] : 0.0f;
-        }
-    };
-    load(0);
-    for (int c0 = 0; c0 < fs; c0 += RMS_KC) {
-        __syncthreads();
-#pragma unroll
-        for (int u = 0; u < NLD; u++) tile[sub + u * RSTEP][j] = nx[u] * r_gain[sub + u * RSTEP];
-        __syncthreads();
-        if (c0 + RMS_KC < fs) load(c0 + RMS_KC);
-        const int lim = (int)len - c0 < RMS_KC ? (int)len - c0 : RMS_KC;
-        for (int q = 0; q < lim; q++) {
-            const float v = tile[tid][q];
-            sum += v * v;
-        }
-    }
-    if (g < total) rms[g] = len > 0 ? __builtin_sqrtf(sum / (float)len) : 0.0f;
-}
-
 // Silence regions and trim bounds (silence.rs:171-279), one workgroup per track.  Only two
 // regions can move the trim: the run of silent frames starting at frame 0 (always kept, its
 // end becomes the trim start) and the run reaching the last frame (kept when at least
@@ -435,6 +372,71 @@ void launch_peak_gain(const float* x, const uint64_t* in_off, const uint64_t* n_
     if (n_chunks) hipLaunchKernelGGL(k_peak_abs, dim3((unsigned)n_chunks), dim3(256), 0, st, x, in_off, n_raw, chunk_pfx, T, peak_bits);
     hipLaunchKernelGGL(k_gain, dim3((T + 255) / 256), dim3(256), 0, st, peak_bits, T, target, enable, gain);
 }
+// ---- frame RMS: sqrt(sum_{k in frame} (x_k*gain)^2 / len), the sum folded in sample order ----
+// Each thread streams its own frame from global memory in 16-B aligned blocks (lanes read
+// rows `hop` apart, so every wave-instruction touches 64 lines; 16-B rather than 4-B loads cut
+// the instruction count 4x).  hop is a multiple of 4, so a frame's misalignment d is its
+// track's; the first block skips its d leading floats and a scalar tail finishes the frame.
+constexpr int RMS_U = 8;  // 16-B blocks per step (two steps in flight per thread)
+__global__ __launch_bounds__(256) void k_frame_rms(const float* __restrict__ x,
+                                                          const uint64_t* __restrict__ src_off,
+                                                          const float* __restrict__ gain,
+                                                          const uint64_t* __restrict__ n_len,
+                                                          const uint64_t* __restrict__ frame_pfx, int T,
+                                                          uint64_t total, int fs, int hop, float* __restrict__ rms) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (g >= total) return;
+    const int trk = find_track(frame_pfx, T, g);
+    const uint64_t f = g - frame_pfx[trk];
+    const uint64_t n = n_len[trk];
+    const uint64_t s = f * (uint64_t)hop;
+    const uint64_t e = s + (uint64_t)fs < n ? s + (uint64_t)fs : n;
+    const int64_t len = e > s ? (int64_t)(e - s) : 0;
+    const uint64_t a = src_off[trk] + s;  // float index of the frame's first sample
+    const int d = (int)(a & 3u);
+    const f4* q = reinterpret_cast<const f4*>(x + (a - (uint64_t)d));
+    const float gn = gain[trk];
+    float sum = 0.0f;
+    auto acc = [&](float v) {
+        const float y = v * gn;
+        sum += y * y;
+    };
+    // block j holds samples k = 4j - d .. 4j - d + 3
+    int64_t j = 0;
+    if (d != 0 && len > 0) {
+        const f4 h = q[0];
+        for (int i = d; i < 4 && i - d < len; i++) acc(h[i]);
+        j = 1;
+    }
+    // RMS_U whole blocks per step, the next step's blocks in flight while this one is folded
+    if (4 * (j + RMS_U) - d <= len) {
+        f4 cur[RMS_U], nxt[RMS_U];
+#pragma unroll
+        for (int u = 0; u < RMS_U; u++) cur[u] = q[j + u];
+        for (;;) {
+            const bool more = 4 * (j + 2 * RMS_U) - d <= len;
+            if (more) {
+#pragma unroll
+                for (int u = 0; u < RMS_U; u++) nxt[u] = q[j + RMS_U + u];
+            }
+#pragma unroll
+            for (int u = 0; u < RMS_U; u++) {
+                acc(cur[u].x);
+                acc(cur[u].y);
+                acc(cur[u].z);
+                acc(cur[u].w);
+            }
+            j += RMS_U;
+            if (!more) break;
+#pragma unroll
+            for (int u = 0; u < RMS_U; u++) cur[u] = nxt[u];
+        }
+    }
+    for (int64_t k = j == 0 ? 0 : 4 * j - d; k < len; k++) acc(x[a + (uint64_t)k]);  // j == 0: d == 0 or empty
+    rms[g] = len > 0 ? __builtin_sqrtf(sum / (float)len) : 0.0f;
+}
+
 void launch_frame_rms(const float* x, const uint64_t* src_off, const float* gain, const uint64_t* n_len,
                       const uint64_t* frame_pfx, int T, uint64_t total, int fs, int hop, float* rms, hipStream_t st) {
     if (total == 0) return;

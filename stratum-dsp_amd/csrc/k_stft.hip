@@ -66,6 +66,20 @@ __device__ __forceinline__ void bfly4(f2 a, f2 b, f2 c, f2 d, f2 w1, f2 w2, f2 w
 
 __device__ __forceinline__ int lpad(int i) { return i + (i >> 4); }
 
+// Barrier over the threads of one frame: a frame of TPF = 64 threads is one wave, whose LDS
+// operations complete in order, so a wave-scope fence + wave barrier replaces the workgroup
+// barrier and the frames of a workgroup run independently.
+template <int TPF>
+__device__ __forceinline__ void frame_sync() {
+    if constexpr (TPF == 64) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+        __syncthreads();
+    }
+}
+
 // Correctly rounded f32 sqrt.  For x in [2^-96, inf) this is exactly the sequence hipcc emits
 // for sqrtf under -fhip-fp32-correctly-rounded-divide-sqrt (v_sqrt_f32, then the +-1 ulp
 // FMA-residual correction) without its small-input rescaling and special-value select; other
@@ -157,7 +171,7 @@ __global__ __launch_bounds__(256) void k_stft_mag(const float* __restrict__ samp
 #pragma unroll
         for (int k = 0; k < 16; k++) buf[b0 + k] = v[k];
     }
-    __syncthreads();
+    frame_sync<TPF>();
     // further radix-16 passes: (n, s) = (M/16, 16), (M/256, 256)
 #pragma unroll
     for (int pass = 1; pass < S::NPASS; pass++) {
@@ -179,7 +193,7 @@ __global__ __launch_bounds__(256) void k_stft_mag(const float* __restrict__ samp
         }
 #pragma unroll
         for (int k = 0; k < 16; k++) v[k] = buf[rb + rs * k];
-        __syncthreads();
+        frame_sync<TPF>();
         radix16(v, w);
         // writes z[q + 16 s pp + s k]:  s = 16 -> (q + 272 pp) + 17 k;  s = 256 (pp = 0) -> lpad(q) + 272 k
         if (s == 16) {
@@ -190,7 +204,7 @@ __global__ __launch_bounds__(256) void k_stft_mag(const float* __restrict__ samp
 #pragma unroll
             for (int k = 0; k < 16; k++) buf[rb + 272 * k] = v[k];
         }
-        __syncthreads();
+        frame_sync<TPF>();
     }
     // trailing radix-4 stage (M = 16^2 * 4): n = 4, s = M/4, p = 0, twiddles tw[0]
     if constexpr (M == 1024) {
@@ -207,7 +221,7 @@ __global__ __launch_bounds__(256) void k_stft_mag(const float* __restrict__ samp
             buf[b + 544] = y2;
             buf[b + 816] = y3;
         }
-        __syncthreads();
+        frame_sync<TPF>();
     }
     // real-FFT post-processing, |X[k]|, k = 0..M.  Bins k and M-k read the same pair
     // (Z[k], Z[M-k]); the partner's E and O are the conjugates of this bin's (exactly, up to
