@@ -336,6 +336,7 @@ __global__ __launch_bounds__(64) void k_beat(const int* __restrict__ tracks, int
                                              float* __restrict__ scratch, const uint64_t* __restrict__ beat_off,
                                              const int* __restrict__ beat_cap, float* __restrict__ beats,
                                              float* __restrict__ downs, BeatOut* __restrict__ out) {
+    SDSP_LATENCY_CRITICAL();
     __shared__ float s_on[BEAT_LDS_ON];
     __shared__ float s_kv[BEAT_SORT_MAX];
     __shared__ int s_ki[BEAT_SORT_MAX];

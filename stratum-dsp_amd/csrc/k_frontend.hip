@@ -62,6 +62,7 @@ __global__ __launch_bounds__(256) void k_trim(const float* __restrict__ rms, con
                                               int T, const uint64_t* __restrict__ n_raw, int hop, float thr,
                                               uint64_t min_frames, int enable, uint64_t* __restrict__ trim_start,
                                               uint64_t* __restrict__ trim_end) {
+    SDSP_LATENCY_CRITICAL();
     __shared__ long long red_lo[4], red_hi[4];
     const int t = blockIdx.x;
     const uint64_t n = n_raw[t];
@@ -119,6 +120,7 @@ __global__ __launch_bounds__(256) void k_energy_onsets(const float* __restrict__
                                                        const uint64_t* __restrict__ n_trim, int hop, float factor,
                                                        uint32_t* __restrict__ out, const uint64_t* __restrict__ out_off,
                                                        int* __restrict__ out_n) {
+    SDSP_LATENCY_CRITICAL();
     __shared__ float redf[8];
     __shared__ int redi[9];
     const int trk = blockIdx.x;
@@ -171,6 +173,7 @@ __global__ __launch_bounds__(256) void k_flux_onsets(const float* __restrict__ s
                                                      const uint64_t* __restrict__ n_trim, int hop, float pct,
                                                      uint32_t* __restrict__ out, const uint64_t* __restrict__ out_off,
                                                      int* __restrict__ out_n, int T) {
+    SDSP_LATENCY_CRITICAL();
     __shared__ int hist[256];
     __shared__ int misc[4];
     __shared__ int redi[9];
@@ -257,6 +260,7 @@ __global__ __launch_bounds__(256) void k_consensus(const uint32_t* __restrict__ 
                                                    const int* __restrict__ has_mags, uint32_t* __restrict__ chosen,
                                                    const uint64_t* __restrict__ c_off, int* __restrict__ c_n,
                                                    uint32_t* __restrict__ scr) {
+    SDSP_LATENCY_CRITICAL();
     __shared__ int red[8];
     const int t = blockIdx.x;
     const int tid = threadIdx.x;

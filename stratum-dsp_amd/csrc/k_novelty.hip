@@ -21,6 +21,7 @@ __global__ __launch_bounds__(1024) void k_novelty(const float* __restrict__ E, c
                                                    const float* __restrict__ SFX, const uint64_t* __restrict__ frame_pfx,
                                                    int T, uint64_t total, NovParams P, float* __restrict__ scratch,
                                                    float* __restrict__ nov, float* __restrict__ nov_sum) {
+    SDSP_LATENCY_CRITICAL();
     __shared__ float red[16];
     const int trk = blockIdx.x % T, v = blockIdx.x / T;
     if (!P.band_on[v]) return;
@@ -120,6 +121,7 @@ __device__ inline float mel_flux_frame(const float* mtile, int RW, int i, int n_
 __global__ __launch_bounds__(256) void k_mel_flux(const float* __restrict__ MEL, int n_mels, int K,
                                                   const uint64_t* __restrict__ frame_pfx, int T, uint64_t total,
                                                   float* __restrict__ nov, unsigned int* __restrict__ mx_bits) {
+    SDSP_LATENCY_CRITICAL();
     extern __shared__ float mtile[];  // [n_mels][257]: frames gb .. gb+256
     constexpr int RW = 257;
     const uint64_t gb = (uint64_t)blockIdx.x * 256;
@@ -150,6 +152,7 @@ __global__ __launch_bounds__(256) void k_mel_flux(const float* __restrict__ MEL,
 __global__ __launch_bounds__(256) void k_mel_norm(const uint64_t* __restrict__ frame_pfx, int T, uint64_t total,
                                                   const unsigned int* __restrict__ mx_bits, float* __restrict__ nov,
                                                   float* __restrict__ nov_sum) {
+    SDSP_LATENCY_CRITICAL();
     __shared__ float sbuf[SEQ_CH];
     const int trk = blockIdx.x;
     const int64_t F = (int64_t)(frame_pfx[trk + 1] - frame_pfx[trk]);

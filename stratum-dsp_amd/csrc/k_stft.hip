@@ -64,7 +64,19 @@ __device__ __forceinline__ void bfly4(f2 a, f2 b, f2 c, f2 d, f2 w1, f2 w2, f2 w
     y3 = vmul(w3, amc - jbmd);
 }
 
+#ifdef SDSP_EXP_NOPAD
+__device__ __forceinline__ int lpad(int i) { return i; }
+#define P17 16
+#define P272 256
+#define PADSHIFT 0
+#define STFT_ATTR __attribute__((amdgpu_waves_per_eu(5, 8)))
+#else
 __device__ __forceinline__ int lpad(int i) { return i + (i >> 4); }
+#define P17 17
+#define P272 272
+#define PADSHIFT 1
+#define STFT_ATTR
+#endif
 
 // Barrier over the threads of one frame: a frame of TPF = 64 threads is one wave, whose LDS
 // operations complete in order, so a wave-scope fence + wave barrier replaces the workgroup
@@ -123,7 +135,7 @@ struct StftShape {
 };
 
 template <int NFFT, bool FRAME_MAX>
-__global__ __launch_bounds__(256) void k_stft_mag(const float* __restrict__ samples,
+__global__ __launch_bounds__(256) STFT_ATTR void k_stft_mag(const float* __restrict__ samples,
                                                   const uint64_t* __restrict__ frame_pfx, int n_tracks,
                                                   uint64_t total_frames, const uint64_t* __restrict__ src_off,
                                                   const float* __restrict__ gain, int hop,
@@ -135,7 +147,7 @@ __global__ __launch_bounds__(256) void k_stft_mag(const float* __restrict__ samp
     using S = StftShape<M>;
     constexpr int TPF = S::TPF;
     constexpr int FPB = 256 / TPF;    // frames per workgroup
-    constexpr int PADM = M + M / 16;  // padded LDS slots per frame
+    constexpr int PADM = M + PADSHIFT * M / 16;  // padded LDS slots per frame
     static_assert(S::NPASS > 0, "supported sizes: N = 2048, 8192");
     __shared__ f2 lds[FPB * PADM];
     __shared__ float red[4];
@@ -167,7 +179,7 @@ __global__ __launch_bounds__(256) void k_stft_mag(const float* __restrict__ samp
     for (int j = 0; j < 15; j++) w[j] = ld_f2(rtw, vo, 8 * TPF * j);
     radix16(v, w);
     {
-        const int b0 = 17 * lt;  // lpad(16 lt + k) = 17 lt + k
+        const int b0 = P17 * lt;  // lpad(16 lt + k) = 17 lt + k
 #pragma unroll
         for (int k = 0; k < 16; k++) buf[b0 + k] = v[k];
     }
@@ -179,7 +191,7 @@ __global__ __launch_bounds__(256) void k_stft_mag(const float* __restrict__ samp
         const int m1 = (pass == 1 ? M / 16 : M / 256) / 16;  // n / 16
         const int q = lt % s, pp = pass == 2 ? 0 : lt / s;  // lt < TPF = 256 = s on pass 2
         // reads x[q + s pp + s m1 k]; s m1 is a multiple of 16, so lpad = lpad(q + s pp) + (17/16) s m1 k
-        const int rb = lpad(q + s * pp), rs = s * m1 + (s * m1) / 16;
+        const int rb = lpad(q + s * pp), rs = s * m1 + PADSHIFT * (s * m1) / 16;
 #pragma unroll
         for (int j = 0; j < 15; j++) {
             // pass 1: one entry per p' (TPF/16 of them, shared by 16 lanes); pass 2: p' = 0 for
@@ -197,12 +209,12 @@ __global__ __launch_bounds__(256) void k_stft_mag(const float* __restrict__ samp
         radix16(v, w);
         // writes z[q + 16 s pp + s k]:  s = 16 -> (q + 272 pp) + 17 k;  s = 256 (pp = 0) -> lpad(q) + 272 k
         if (s == 16) {
-            const int wb = q + 272 * pp;
+            const int wb = q + P272 * pp;
 #pragma unroll
-            for (int k = 0; k < 16; k++) buf[wb + 17 * k] = v[k];
+            for (int k = 0; k < 16; k++) buf[wb + P17 * k] = v[k];
         } else {  // s = 256 only for M = 4096 (m1 = 1): z[q + 256 k], lpad = lpad(q) + 272 k
 #pragma unroll
-            for (int k = 0; k < 16; k++) buf[rb + 272 * k] = v[k];
+            for (int k = 0; k < 16; k++) buf[rb + P272 * k] = v[k];
         }
         frame_sync<TPF>();
     }
@@ -215,11 +227,11 @@ __global__ __launch_bounds__(256) void k_stft_mag(const float* __restrict__ samp
             const int q = lt + TPF * r;
             const int b = lpad(q);  // lpad(q + j s) = b + 272 j (s = 256)
             f2 y0, y1, y2, y3;
-            bfly4(buf[b], buf[b + 272], buf[b + 544], buf[b + 816], w0, w0, w0, y0, y1, y2, y3);
+            bfly4(buf[b], buf[b + P272], buf[b + 2 * P272], buf[b + 3 * P272], w0, w0, w0, y0, y1, y2, y3);
             buf[b] = y0;
-            buf[b + 272] = y1;
-            buf[b + 544] = y2;
-            buf[b + 816] = y3;
+            buf[b + P272] = y1;
+            buf[b + 2 * P272] = y2;
+            buf[b + 3 * P272] = y3;
         }
         frame_sync<TPF>();
     }

@@ -59,6 +59,62 @@ __device__ cx* fft_block(cx* A, cx* B, int M, const cx* __restrict__ tw) {
     return src;
 }
 
+// In-place variant for a single LDS buffer (M <= 4 * 256 * RMAX): each radix-4 pass reads
+// its butterflies' inputs into registers, barriers, then writes the outputs -- the same
+// arithmetic and output positions as fft_block with half the LDS, so an FFT tempogram block
+// fits on a CU beside the STFT blocks of the other stream.
+template <int RMAX>
+__device__ cx* fft_block_inplace(cx* A, int M, const cx* __restrict__ tw) {
+    int n = M, s = 1, ls = 0;
+    const int nb = M >> 2;
+    while (n >= 4) {
+        const int m = n >> 2, tstep = M / n;
+        cx o[RMAX][4];
+        int ob[RMAX];
+#pragma unroll
+        for (int r = 0; r < RMAX; r++) {
+            const int beta = threadIdx.x + r * blockDim.x;
+            ob[r] = -1;
+            if (beta < nb) {
+                const int p = beta >> ls, q = beta & (s - 1);
+                const cx a = A[q + s * p], b = A[q + s * (p + m)], c = A[q + s * (p + 2 * m)],
+                         d = A[q + s * (p + 3 * m)];
+                const cx w1 = tw[1 * p * tstep], w2 = tw[2 * p * tstep], w3 = tw[3 * p * tstep];
+                const cx apc = cadd(a, c), amc = csub(a, c), bpd = cadd(b, d), bmd = csub(b, d);
+                const cx jbmd = {bmd.im, -bmd.re};
+                o[r][0] = cadd(apc, bpd);
+                o[r][1] = cmul(w1, cadd(amc, jbmd));
+                o[r][2] = cmul(w2, csub(apc, bpd));
+                o[r][3] = cmul(w3, csub(amc, jbmd));
+                ob[r] = q + s * 4 * p;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < RMAX; r++)
+            if (ob[r] >= 0) {
+                A[ob[r]] = o[r][0];
+                A[ob[r] + s] = o[r][1];
+                A[ob[r] + 2 * s] = o[r][2];
+                A[ob[r] + 3 * s] = o[r][3];
+            }
+        __syncthreads();
+        n = m;
+        s <<= 2;
+        ls += 2;
+    }
+    if (n == 2) {  // each thread reads and writes the same two slots
+        for (int q = threadIdx.x; q < s; q += blockDim.x) {
+            const cx a = A[q], b = A[q + s];
+            A[q] = cadd(a, b);
+            A[q + s] = csub(a, b);
+        }
+        __syncthreads();
+    }
+    return A;
+}
+constexpr int FFT_TG_RMAX = 8;  // in-place LDS FFT up to M = 8192 (P = 16384)
+
 // ----------------------------------------------------------------------------------------
 // FFT tempogram.  items[i] = trk*NVAR + v.  Output entries for item i at out_off[i], count K.
 __global__ __launch_bounds__(256) void k_fft_tempogram(const int* __restrict__ items, int n_items, int T,
@@ -68,6 +124,7 @@ __global__ __launch_bounds__(256) void k_fft_tempogram(const int* __restrict__ i
                                                        const cx* __restrict__ rt, cx* __restrict__ gscratch,
                                                        const uint64_t* __restrict__ out_off, float* __restrict__ out_bpm,
                                                        float* __restrict__ out_pow) {
+    SDSP_LATENCY_CRITICAL();
     extern __shared__ cx dyn[];
     const int it = items[blockIdx.x];
     const int trk = it / NVAR, v = it % NVAR;
@@ -93,9 +150,15 @@ __global__ __launch_bounds__(256) void k_fft_tempogram(const int* __restrict__ i
         A[j] = {r0, r1};
     }
     __syncthreads();
-    cx* Z = (M >= 2) ? fft_block(A, Bb, M, tw) : A;
-    cx* freebuf = (Z == A) ? Bb : A;
-    uint64_t* keys = reinterpret_cast<uint64_t*>(freebuf);
+    cx* Z;
+    uint64_t* keys;
+    if (P.lds) {  // one M-slot buffer + the key buffer (dyn[M ..])
+        Z = (M >= 2) ? fft_block_inplace<FFT_TG_RMAX>(A, M, tw) : A;
+        keys = reinterpret_cast<uint64_t*>(dyn + M);
+    } else {
+        Z = (M >= 2) ? fft_block(A, Bb, M, tw) : A;
+        keys = reinterpret_cast<uint64_t*>((Z == A) ? Bb : A);
+    }
     int K2 = 1;
     while (K2 < P.K) K2 <<= 1;
     for (int i = threadIdx.x; i < K2; i += blockDim.x) {
@@ -141,6 +204,7 @@ __global__ __launch_bounds__(256) void k_acf_tempogram(const int* __restrict__ i
                                                        const float* __restrict__ bpm_grid,
                                                        const int* __restrict__ lag_grid, int NB,
                                                        float* __restrict__ out_bpm, float* __restrict__ out_str) {
+    SDSP_LATENCY_CRITICAL();
     __shared__ uint64_t keys[NACF_MAX];
     __shared__ float vals[NACF_MAX];
     const int it = items[blockIdx.x];
@@ -201,6 +265,7 @@ __global__ __launch_bounds__(256) void k_tempo_select(const int* __restrict__ ac
                                                       const uint64_t* __restrict__ acf_off,  // per item*NVAR+v
                                                       SelParams P, TempoEst* __restrict__ est,
                                                       float* __restrict__ cand, int cand_cap) {
+    SDSP_LATENCY_CRITICAL();
     __shared__ uint64_t keys[SEL_MAXC];
     __shared__ float cvals[SEL_MAXC];
     __shared__ float sc[SEL_MAXC][3];  // score, fft_norm, ac_norm (indexed by uniq position)
@@ -461,6 +526,7 @@ __global__ __launch_bounds__(64) void k_multires(const int* __restrict__ tracks,
                                                  const float* __restrict__ nov512, const uint64_t* __restrict__ fpfx512,
                                                  MrParams P, TempoEst* __restrict__ mr_est, int* __restrict__ used,
                                                  float* __restrict__ final_bpm, float* __restrict__ final_conf) {
+    SDSP_LATENCY_CRITICAL();
     __shared__ float fam_bpm[5], fam_sup[5], fam_align[5];
     __shared__ int n_fam_s, do_fam_s;
     __shared__ float best_bpm_s, best_score_s, second_s;
@@ -714,7 +780,9 @@ void launch_fft_tempogram(const int* items, int n_items, int T, const float* nov
                           const uint64_t* frame_pfx, uint64_t total, const FftTgParams& P, const cx* tw, const cx* rt,
                           cx* gscratch, const uint64_t* out_off, float* out_bpm, float* out_pow, hipStream_t st) {
     if (n_items == 0) return;
-    const size_t lds = P.lds ? (size_t)P.P * sizeof(cx) : 0;  // two M = P/2 buffers
+    int K2 = 1;
+    while (K2 < P.K) K2 <<= 1;
+    const size_t lds = P.lds ? (size_t)(P.P / 2 + K2) * sizeof(cx) : 0;  // M = P/2 slots + keys
     hipLaunchKernelGGL(k_fft_tempogram, dim3(n_items), dim3(256), lds, st, items, n_items, T, nov, nov_sum, frame_pfx,
                        total, P, tw, rt, gscratch, out_off, out_bpm, out_pow);
 }

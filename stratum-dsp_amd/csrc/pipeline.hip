@@ -628,7 +628,7 @@ void Pipeline::tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPa
         pc.prm.b_lo = b_lo;
         pc.prm.K = K;
         pc.prm.fres = fr;
-        pc.prm.lds = kv.first <= 16384 ? 1 : 0;
+        pc.prm.lds = kv.first <= 16384 ? 1 : 0;  // k_fft_tempogram's in-place LDS FFT: M <= 8192
         uint64_t K2 = 1;
         while (K2 < (uint64_t)K) K2 <<= 1;
         if (K > 0 && K2 > kv.first / 2) throw HipError("FFT tempogram: too many in-range bins for the key buffer");

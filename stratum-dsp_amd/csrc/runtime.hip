@@ -3,6 +3,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "../../include/sdsp_fft_spec.h"
 #include "sdsp_runtime.hpp"
@@ -19,8 +20,37 @@ DeviceCtx& device_ctx(int device) {
         c.reset(new DeviceCtx());
         c->device = device;
         SDSP_HIP_CHECK(hipSetDevice(device));
-        SDSP_HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-        SDSP_HIP_CHECK(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+        // The tempo path (main stream) is the critical path and is made of short, latency-bound
+        // kernels; the key path (stream2) is long bandwidth-bound kernels.  The main stream gets
+        // the higher priority so its workgroups are dispatched ahead of the key stream's
+        // (SDSP_EQUAL_PRIORITY=1 disables).
+        if (const char* sk = std::getenv("SDSP_ALLOC_SKEW_MB")) {  // placement experiment
+            void* dummy = nullptr;
+            SDSP_HIP_CHECK(hipMalloc(&dummy, (size_t)std::atol(sk) << 20));
+        }
+        int lo = 0, hi = 0;
+        SDSP_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        if (std::getenv("SDSP_EQUAL_PRIORITY")) lo = hi = 0;
+        SDSP_HIP_CHECK(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi));
+        // SDSP_KEY_CU_FRAC=f (experiment): the key stream runs on a fixed fraction f of the CUs,
+        // spread evenly over CU ids, and the main stream on the rest
+        const char* kf = std::getenv("SDSP_KEY_CU_FRAC");
+        if (kf && std::atof(kf) > 0.0 && std::atof(kf) < 1.0) {
+            SDSP_HIP_CHECK(hipStreamDestroy(c->stream));
+            hipDeviceProp_t prop;
+            SDSP_HIP_CHECK(hipGetDeviceProperties(&prop, device));
+            const int ncu = prop.multiProcessorCount;
+            const double f = std::atof(kf);
+            std::vector<uint32_t> mk((size_t)(ncu + 31) / 32, 0u), mm((size_t)(ncu + 31) / 32, 0u);
+            for (int i = 0; i < ncu; i++) {
+                const bool key = (int)((i + 1) * f) != (int)(i * f);  // even spread
+                (key ? mk : mm)[(size_t)i / 32] |= 1u << (i % 32);
+            }
+            SDSP_HIP_CHECK(hipExtStreamCreateWithCUMask(&c->stream, (uint32_t)mm.size(), mm.data()));
+            SDSP_HIP_CHECK(hipExtStreamCreateWithCUMask(&c->stream2, (uint32_t)mk.size(), mk.data()));
+        } else {
+            SDSP_HIP_CHECK(hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, lo));
+        }
     }
     return *c;
 }

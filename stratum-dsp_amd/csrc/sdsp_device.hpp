@@ -15,6 +15,15 @@ namespace sdsp {
 constexpr float EPS = 1e-10f;
 constexpr int WAVE = 64;
 
+// Raises the issuing wave's priority on its SIMD.  Used at the top of the short, latency-bound
+// tempo-path kernels so that, running beside the key stream's VALU-heavy STFT waves, they are
+// not starved of issue slots (the main stream is the pipeline's critical path).
+#ifdef SDSP_NO_SETPRIO
+#define SDSP_LATENCY_CRITICAL() ((void)0)
+#else
+#define SDSP_LATENCY_CRITICAL() __builtin_amdgcn_s_setprio(2)
+#endif
+
 struct cx {
     float re, im;
 };
