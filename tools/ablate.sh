@@ -1,6 +1,6 @@
 #!/bin/bash
 # kernel-time ablations: per-kernel stats for alternative library builds (serial streams)
-# usage: tools_ablate.sh name1 name2 ...   (stratum-dsp_amd/lib_exp/lib_<name>.so; "base" = the normal build)
+# usage: tools/ablate.sh name1 name2 ...   (stratum-dsp_amd/lib_exp/lib_<name>.so; "base" = the normal build)
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 for v in "$@"; do

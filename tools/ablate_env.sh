@@ -1,5 +1,5 @@
 #!/bin/bash
-# kernel-time A/B by environment: tools_ablate_env.sh tag "VAR=val VAR2=val" ...
+# kernel-time A/B by environment: tools/ablate_env.sh tag "VAR=val VAR2=val" ...
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 tag=$1; shift

@@ -1,6 +1,6 @@
 #!/bin/bash
 # layout experiment: per-kernel stats for several spectrogram row strides (serial streams)
-# usage: tools_stride_sweep.sh "S8 S2" ...
+# usage: tools/stride_sweep.sh "S8 S2" ...
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 for cfg in "$@"; do

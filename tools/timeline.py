@@ -1,11 +1,16 @@
+"""GPU busy fraction and largest idle gaps from a rocprofv3 kernel trace (csv).
+usage: tools_timeline.py run_kernel_trace.csv [from_ms]   (from_ms: skip kernels starting earlier)"""
 import csv, sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 iv = sorted((int(r['Start_Timestamp']), int(r['End_Timestamp']), r['Kernel_Name'][:40]) for r in rows)
+t00 = iv[0][0]
+if len(sys.argv) > 2:
+    iv = [x for x in iv if x[0] - t00 >= float(sys.argv[2]) * 1e6]
 t0 = iv[0][0]; t1 = max(e for _, e, _ in iv)
 busy = 0; cur_s, cur_e = iv[0][0], iv[0][1]; gaps = []
 for s, e, n in iv[1:]:
     if s > cur_e:
-        busy += cur_e - cur_s; gaps.append((s - cur_e, cur_e - t0, n)); cur_s, cur_e = s, e
+        busy += cur_e - cur_s; gaps.append((s - cur_e, cur_e - t00, n)); cur_s, cur_e = s, e
     else:
         cur_e = max(cur_e, e)
 busy += cur_e - cur_s
