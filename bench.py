@@ -192,8 +192,14 @@ def main():
 
     cpu = None
     parity = None
+    extras = {}
+    if not args.dry_run:
+        # fraction of this rank's tracks whose base estimate escalated to multi-resolution
+        # (src/lib.rs:410-459; BASELINE.md asks for the escalation rate beside the throughput)
+        extras["escalation_rate"] = round(res.count("tempogram_multi_res_triggered") / max(n, 1), 4)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.dry_run:
         cpu, parity = cpu_baseline(buf, res, n, L, sr, args)
+        extras["sine_30s"] = sine_30s(sr)
 
     if rank == 0:
         out = {
@@ -224,6 +230,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "parity_sample": parity,
+            **extras,
         }
         print(json.dumps(out), flush=True)
     if tdist is not None:
@@ -259,8 +266,38 @@ def cpu_baseline(buf, res, n, L, sr, args):
         "sample": f"{k} of the benchmark's own {args.seconds:g}-s tracks, one track per thread, "
                   f"{dt:.1f} s wall ({dt * threads:.0f} thread-s); C++ restatement -O3, FFT per sdsp_fft_spec.h",
     }
+    # one thread, the same tracks (report 1 thread and all cores)
+    k1 = min(k, 2)
+    t0 = time.perf_counter()
+    for x in xs[:k1]:
+        one(x)
+    cpu["value_1thread"] = round(k1 / (time.perf_counter() - t0), 4)
     par = {"checked": k, "within_tolerance": match, "bit_exact": exact}
     return cpu, par
+
+
+def sine_30s(sr):
+    """The reference's own Criterion workload (benches/audio_analysis_bench.rs:25-29,410-423):
+    one 30-s 440 Hz sine at amplitude 0.5, one analyze_audio call.  GPU: host buffer in, results
+    out (H2D included), median of 5 calls after one warmup; CPU: the oracle on one thread.  The
+    reference publishes ~203-208 ms for it on its author's machine."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+
+    i = np.arange(sr * 30, dtype=np.float32)
+    f32 = np.float32
+    x = (np.sin(i * f32(440.0) * f32(2.0) * f32(np.pi) / f32(sr)) * f32(0.5)).astype(np.float32)  # f32 ops, Rust order
+    sdsp.analyze_audio(x, sr)
+    ts = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        sdsp.analyze_audio(x, sr)
+        ts.append((time.perf_counter() - t0) * 1e3)
+    t0 = time.perf_counter()
+    oracle.analyze(x, sr)
+    cpu_ms = (time.perf_counter() - t0) * 1e3
+    return {"gpu_ms": round(sorted(ts)[2], 3), "cpu_port_1thread_ms": round(cpu_ms, 1),
+            "reference_published_ms": "203-208 (author's machine, Criterion)"}
 
 
 if __name__ == "__main__":

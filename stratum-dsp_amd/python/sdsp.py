@@ -151,6 +151,11 @@ class ResultBatch:
             return AnalysisError(o.status, o.error_message.decode())
         return result_to_dict(o)
 
+    def count(self, field, value=1):
+        """How many successful tracks have the native result field == value (e.g.
+        tempogram_multi_res_triggered), without building result dicts."""
+        return sum(1 for i in range(self.n) if self.status[i] == 0 and getattr(self._outs[i], field) == value)
+
     def free(self):
         if self._outs is not None:
             for i in range(self.n):
