@@ -130,6 +130,56 @@ def test_device_generated_3min_tracks():
         assert not parity.diff_results(res[i], ref), (i, parity.diff_results(res[i], ref))
 
 
+def test_config4_mixed_lengths():
+    """BASELINE config 4 shape: device-generated tracks of 30 s to 10 min in one ragged batch
+    (frames 2,580 -> 51,676 at 2048/512; FFT-tempogram sizes from 4,096 up to the global-memory
+    path), each checked against the oracle."""
+    secs = [30, 75, 240, 600]
+    xs = []
+    for k, sec in enumerate(secs):
+        L = 44100 * sec
+        buf = sdsp.DeviceBuffer(L)
+        sdsp.generate_synthetic(buf.ptr, 1, L, seed0=400 + k)
+        xs.append(buf.to_host())
+    res = sdsp.analyze_batch(xs, 44100)
+    for sec, x, r in zip(secs, xs, res):
+        st, ref = oracle.analyze(x, 44100)
+        assert st == 0 and not isinstance(r, sdsp.AnalysisError), (sec, r)
+        assert not parity.diff_results(r, ref), (sec, parity.diff_results(r, ref))
+        assert parity.exact_fraction(r, ref) == 1.0, sec
+
+
+def test_config5_escalation_heavy():
+    """BASELINE config 5 mix (BPMs 1/3 in [55,80], 1/3 in [170,200], 1/3 in [80,170]): the
+    multi-resolution escalation runs for most tracks; bpm, confidence and the escalation flags
+    must equal the oracle's."""
+    n, L = 9, 44100 * 60
+    buf = sdsp.DeviceBuffer(n * L)
+    sdsp.generate_synthetic(buf.ptr, n, L, seed0=500, bpm_mode=1)
+    res = sdsp.analyze_batch_device(buf.ptr, np.arange(n) * L, np.full(n, L))
+    host = buf.to_host()
+    trig = 0
+    for i in range(n):
+        st, ref = oracle.analyze(host[i * L:(i + 1) * L], 44100)
+        assert st == 0
+        assert not parity.diff_results(res[i], ref), (i, parity.diff_results(res[i], ref))
+        m = res[i]["metadata"]
+        assert m["tempogram_multi_res_triggered"] == ref["metadata"]["tempogram_multi_res_triggered"]
+        assert m["tempogram_multi_res_used"] == ref["metadata"]["tempogram_multi_res_used"]
+        trig += m["tempogram_multi_res_triggered"] is True
+    assert trig >= n // 3, trig  # the trap-range thirds escalate
+
+
+def test_reference_bench_sine():
+    """The reference's Criterion workload (benches/audio_analysis_bench.rs:25-29): 30 s of a
+    440 Hz sine at 0.5, f32 arithmetic in the bench's order."""
+    f32 = np.float32
+    i = np.arange(44100 * 30, dtype=np.float32)
+    x = (np.sin(i * f32(440.0) * f32(2.0) * f32(np.pi) / f32(44100)) * f32(0.5)).astype(np.float32)
+    got, ref = _check(x, 44100, "sine30")
+    assert parity.exact_fraction(got, ref) == 1.0
+
+
 def test_emit_candidates_config():
     x, *_ = synth.make_track(5, seconds=25.0)
     cfg = sdsp.default_config()
