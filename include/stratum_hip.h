@@ -297,6 +297,38 @@ int32_t sdsp_memcpy_h2d(int32_t device, void* dst, const void* src, uint64_t byt
 int32_t sdsp_memcpy_d2h(int32_t device, void* dst, const void* src, uint64_t bytes);
 int32_t sdsp_device_synchronize(int32_t device);
 
+/*
+ * compute_confidence (src/analysis/confidence.rs:121-297): host-side scores of one result.
+ * flag_list holds AnalysisFlag indices (0 MultimodalBpm, 1 WeakTonality, 2 TempoVariation,
+ * 3 OnsetDetectionAmbiguous) in the reference's push order, duplicates kept (the result's own
+ * flags first, then MultimodalBpm / WeakTonality / TempoVariation as their thresholds fire).
+ */
+typedef struct sdsp_confidence {
+    float bpm_confidence;
+    float key_confidence;
+    float grid_stability;
+    float overall_confidence;
+    uint32_t n_flags;
+    int32_t flag_list[8];
+} sdsp_confidence;
+int32_t sdsp_compute_confidence(const sdsp_result* result, sdsp_confidence* out);
+
+/* Key::name (src/analysis/result.rs:31-39): "C", "F#", "Am", "C#m"; returns the length. */
+int32_t sdsp_key_name(int32_t key_mode, uint32_t key_tonic, char* buf, uint64_t buflen);
+
+/*
+ * Audio decode front-end (examples/analyze_file.rs:25-180, analyze_batch.rs:30-177): RIFF/WAVE
+ * files -- PCM u8 / s16 / s24 / s32, IEEE float f32 / f64, WAVE_FORMAT_EXTENSIBLE with those
+ * sub-formats -- decoded to mono f32 exactly as the reference's symphonia path converts them
+ * (s16 / 32768, s24 / 8388608, s32 / 2147483648, (u8 - 128) / 128, f64 -> f32; channels summed
+ * in order and divided by the channel count).  *samples is malloc'ed (free with
+ * sdsp_free_samples).  Returns 0, or SDSP_ERR_DECODING with the reason in err for anything else
+ * (other containers and codecs are outside this front-end).
+ */
+int32_t sdsp_decode_audio_file(const char* path, float** samples, uint64_t* n_samples, uint32_t* sample_rate,
+                               char* err, uint64_t errlen);
+void sdsp_free_samples(float* samples);
+
 /* Library identification: "stratum-hip <abi> gfx950" */
 const char* sdsp_version(void);
 

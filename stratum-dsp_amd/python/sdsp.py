@@ -13,7 +13,7 @@ import subprocess
 
 import numpy as np
 
-from sdsp_abi import ERROR_NAMES, SdspConfig, SdspResult, SdspStageTimes, result_to_dict
+from sdsp_abi import ERROR_NAMES, FLAG_NAMES, SdspConfidence, SdspConfig, SdspResult, SdspStageTimes, result_to_dict
 
 PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("SDSP_LIB_PATH") or os.path.join(PKG, "lib", "libstratum_hip.so")  # override: layout/ablation builds
@@ -66,8 +66,14 @@ def lib():
         L.sdsp_memcpy_h2d.argtypes = [C.c_int32, C.c_void_p, C.c_void_p, C.c_uint64]
         L.sdsp_memcpy_d2h.argtypes = [C.c_int32, C.c_void_p, C.c_void_p, C.c_uint64]
         L.sdsp_device_synchronize.argtypes = [C.c_int32]
+        L.sdsp_compute_confidence.argtypes = [C.POINTER(SdspResult), C.POINTER(SdspConfidence)]
+        L.sdsp_key_name.argtypes = [C.c_int32, C.c_uint32, C.c_char_p, C.c_uint64]
+        L.sdsp_decode_audio_file.argtypes = [C.c_char_p, C.POINTER(fp), u64p, C.POINTER(C.c_uint32), C.c_char_p,
+                                             C.c_uint64]
+        L.sdsp_free_samples.argtypes = [fp]
+        L.sdsp_free_samples.restype = None
         for f in ("sdsp_device_malloc", "sdsp_device_free", "sdsp_memcpy_h2d", "sdsp_memcpy_d2h",
-                  "sdsp_device_synchronize"):
+                  "sdsp_device_synchronize", "sdsp_compute_confidence", "sdsp_key_name", "sdsp_decode_audio_file"):
             getattr(L, f).restype = C.c_int32
         _lib = L
     return _lib
@@ -131,6 +137,49 @@ def analyze_batch(tracks, sample_rate=44100, config=None, device_mask=0):
             res.append(result_to_dict(outs[i]))
         lib().sdsp_result_free(C.byref(outs[i]))
     return res
+
+
+def compute_confidence(result):
+    """compute_confidence (src/analysis/confidence.rs:121) through the C ABI, on an
+    AnalysisResult dict (as analyze_audio returns).  Returns the AnalysisConfidence fields plus
+    the confidence_level() string (confidence.rs:218-228)."""
+    r = SdspResult()
+    r.bpm = result["bpm"]
+    r.bpm_confidence = result["bpm_confidence"]
+    r.key_confidence = result["key_confidence"]
+    r.key_clarity = result["key_clarity"]
+    r.grid_stability = result["grid_stability"]
+    md = result.get("metadata", {})
+    r.flags = sum(1 << FLAG_NAMES.index(f) for f in set(md.get("flags", [])))
+    warns = [w.encode() for w in md.get("confidence_warnings", [])]
+    arr = (C.c_char_p * max(len(warns), 1))(*warns)
+    r.warnings = C.cast(arr, C.POINTER(C.c_char_p))
+    r.n_warnings = len(warns)
+    out = SdspConfidence()
+    if lib().sdsp_compute_confidence(C.byref(r), C.byref(out)) != 0:
+        raise AnalysisError(1, "Invalid input: compute_confidence")
+    overall = out.overall_confidence
+    level = "High" if overall >= 0.7 else "Low" if overall < 0.5 else "Medium"
+    return {"bpm_confidence": out.bpm_confidence, "key_confidence": out.key_confidence,
+            "grid_stability": out.grid_stability, "overall_confidence": overall,
+            "flags": [FLAG_NAMES[out.flag_list[i]] for i in range(out.n_flags)], "confidence_level": level}
+
+
+def decode_audio_file(path):
+    """The decode front-end (sdsp_decode_audio_file): RIFF/WAVE -> (mono float32 array, sample_rate),
+    converted as examples/analyze_file.rs:25-180 does.  Raises AnalysisError(DecodingError)."""
+    p = C.POINTER(C.c_float)()
+    n = C.c_uint64()
+    sr = C.c_uint32()
+    err = C.create_string_buffer(512)
+    st = lib().sdsp_decode_audio_file(os.fsencode(path), C.byref(p), C.byref(n), C.byref(sr), err, 512)
+    if st != 0:
+        raise AnalysisError(st, "Decoding error: " + err.value.decode(errors="replace"))
+    try:
+        x = np.ctypeslib.as_array(p, shape=(n.value,)).copy() if n.value else np.zeros(0, np.float32)
+    finally:
+        lib().sdsp_free_samples(p)
+    return x, sr.value
 
 
 class ResultBatch:

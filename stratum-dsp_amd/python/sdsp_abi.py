@@ -202,6 +202,17 @@ class SdspStageTimes(C.Structure):
     ]
 
 
+class SdspConfidence(C.Structure):
+    _fields_ = [
+        ("bpm_confidence", f32),
+        ("key_confidence", f32),
+        ("grid_stability", f32),
+        ("overall_confidence", f32),
+        ("n_flags", u32),
+        ("flag_list", C.c_int32 * 8),
+    ]
+
+
 NOTE_NAMES = ["C", "C#", "D", "D#", "E", "F", "F#", "G", "G#", "A", "A#", "B"]
 FLAG_NAMES = ["MultimodalBpm", "WeakTonality", "TempoVariation", "OnsetDetectionAmbiguous"]
 ERROR_NAMES = {1: "InvalidInput", 2: "DecodingError", 3: "ProcessingError", 4: "NotImplemented", 5: "NumericalError"}

@@ -43,7 +43,8 @@ def test_version():
 
 
 STRUCTS = {"sdsp_config": sdsp_abi.SdspConfig, "sdsp_result": sdsp_abi.SdspResult,
-           "sdsp_tempo_candidate": sdsp_abi.SdspTempoCandidate, "sdsp_stage_times": sdsp_abi.SdspStageTimes}
+           "sdsp_tempo_candidate": sdsp_abi.SdspTempoCandidate, "sdsp_stage_times": sdsp_abi.SdspStageTimes,
+           "sdsp_confidence": sdsp_abi.SdspConfidence}
 
 
 def test_struct_layout_matches_header(tmp_path):
