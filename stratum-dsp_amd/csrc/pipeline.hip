@@ -14,6 +14,9 @@
 //   D  beat grid; join the key stream                    -> host reads results (sync 3)
 // No stage falls back to the CPU; host code only plans offsets and formats the result.
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <mutex>
 #include <cmath>
 #include <chrono>
 #include <cstdio>
@@ -1245,7 +1248,18 @@ int32_t sdsp_analyze_batch_device(const float* d_samples, const uint64_t* offset
     }
 }
 
-// Host buffers: tracks are copied to HBM (one contiguous shard per device) and analysed there.
+// Host buffers: the batch is cut into chunks of whole tracks (up to
+// SDSP_BATCH_CHUNK_TRACKS tracks, default 512, and about 8 GB) that one host thread per device
+// pulls from a shared counter, so escalation-heavy chunks do not leave the other GPUs idle.  Per
+// device a copier thread stages the next chunk into the second of two HBM slots while the
+// device analyses the current one, so PCIe transfers overlap the kernels.
+namespace {
+struct Slot {
+    float* d = nullptr;
+    uint64_t cap = 0;  // floats
+};
+}  // namespace
+
 int32_t sdsp_analyze_batch(const float* const* tracks, const uint64_t* lens, uint64_t n_tracks, uint32_t sample_rate,
                            const sdsp_config* cfg, uint32_t device_mask, sdsp_result* outs) {
     std::vector<int> devs;
@@ -1261,13 +1275,98 @@ int32_t sdsp_analyze_batch(const float* const* tracks, const uint64_t* lens, uin
     for (int d = 0; d < ndev && d < 32; d++)
         if (device_mask == 0 ? d == 0 : ((device_mask >> d) & 1u)) devs.push_back(d);
     if (devs.empty()) devs.push_back(0);
-    const size_t nd = devs.size();
-    std::vector<int32_t> rc(nd, SDSP_OK);
-    auto work = [&](size_t k) {
-        const uint64_t a = n_tracks * k / nd, b = n_tracks * (k + 1) / nd;
-        if (a >= b) return;
-        try {
-            SDSP_HIP_CHECK(hipSetDevice(devs[k]));
+    // chunk boundaries: whole tracks, bounded in count and bytes
+    uint64_t max_tracks = 512;
+    if (const char* e = std::getenv("SDSP_BATCH_CHUNK_TRACKS")) max_tracks = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
+    const uint64_t max_floats = (uint64_t)2 << 30;  // 8 GB
+    std::vector<uint64_t> cb(1, 0);
+    uint64_t acc = 0;
+    for (uint64_t i = 0; i < n_tracks; i++) {
+        if (i > cb.back() && (i - cb.back() >= max_tracks || acc + lens[i] > max_floats)) {
+            cb.push_back(i);
+            acc = 0;
+        }
+        acc += lens[i];
+    }
+    cb.push_back(n_tracks);
+    const size_t n_chunks = n_tracks ? cb.size() - 1 : 0;
+    // every result starts as an error; run_device overwrites the tracks it analyses
+    for (uint64_t i = 0; i < n_tracks; i++) {
+        std::memset(&outs[i], 0, sizeof(outs[i]));
+        outs[i].status = SDSP_ERR_PROCESSING;
+        std::snprintf(outs[i].error_message, sizeof outs[i].error_message, "Processing error: track not analysed");
+    }
+    std::atomic<size_t> next{0};
+    std::vector<int32_t> rc(devs.size(), SDSP_OK);
+    auto fail_chunk = [&](size_t c, const char* what) {
+        for (uint64_t i = cb[c]; i < cb[c + 1]; i++) {
+            std::memset(&outs[i], 0, sizeof(outs[i]));
+            outs[i].status = SDSP_ERR_PROCESSING;
+            std::snprintf(outs[i].error_message, sizeof outs[i].error_message, "Processing error: %s", what);
+        }
+    };
+    auto device_worker = [&](size_t k) {
+        const int dev = devs[k];
+        Slot slot[2];
+        std::mutex mu;
+        std::condition_variable cv;
+        // ready[s]: chunk index staged in slot s (-1 = free); done: the copier has finished
+        long ready[2] = {-1, -1};
+        bool done = false;
+        std::string copy_err;
+        auto copier = [&]() {
+            int s = 0;
+            try {
+                SDSP_HIP_CHECK(hipSetDevice(dev));
+                for (;;) {
+                    const size_t c = next++;
+                    if (c >= n_chunks) break;
+                    {
+                        std::unique_lock<std::mutex> lk(mu);
+                        cv.wait(lk, [&] { return ready[s] < 0; });
+                    }
+                    uint64_t tot = 0;
+                    for (uint64_t i = cb[c]; i < cb[c + 1]; i++) tot += lens[i];
+                    if (slot[s].cap < tot) {
+                        if (slot[s].d) SDSP_HIP_CHECK(hipFree(slot[s].d));
+                        slot[s].d = nullptr;
+                        slot[s].cap = std::max<uint64_t>(tot, 1);
+                        SDSP_HIP_CHECK(hipMalloc(&slot[s].d, slot[s].cap * sizeof(float)));
+                    }
+                    uint64_t o = 0;
+                    for (uint64_t i = cb[c]; i < cb[c + 1]; i++) {
+                        if (lens[i])
+                            SDSP_HIP_CHECK(hipMemcpy(slot[s].d + o, tracks[i], lens[i] * sizeof(float), hipMemcpyHostToDevice));
+                        o += lens[i];
+                    }
+                    {
+                        std::lock_guard<std::mutex> lk(mu);
+                        ready[s] = (long)c;
+                    }
+                    cv.notify_all();
+                    s ^= 1;
+                }
+            } catch (const std::exception& e) {
+                std::lock_guard<std::mutex> lk(mu);
+                copy_err = e.what();
+            }
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                done = true;
+            }
+            cv.notify_all();
+        };
+        std::thread cp(copier);
+        int s = 0;
+        for (;;) {
+            long c;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return ready[s] >= 0 || (done && ready[0] < 0 && ready[1] < 0); });
+                if (ready[s] < 0) break;  // copier finished and nothing staged
+                c = ready[s];
+            }
+            const uint64_t a = cb[(size_t)c], b = cb[(size_t)c + 1];
             std::vector<uint64_t> off(b - a), ln(b - a);
             uint64_t tot = 0;
             for (uint64_t i = a; i < b; i++) {
@@ -1275,22 +1374,34 @@ int32_t sdsp_analyze_batch(const float* const* tracks, const uint64_t* lens, uin
                 ln[i - a] = lens[i];
                 tot += lens[i];
             }
-            float* d = nullptr;
-            SDSP_HIP_CHECK(hipMalloc(&d, std::max<uint64_t>(tot, 1) * sizeof(float)));
-            for (uint64_t i = a; i < b; i++)
-                if (lens[i]) SDSP_HIP_CHECK(hipMemcpy(d + off[i - a], tracks[i], lens[i] * sizeof(float), hipMemcpyHostToDevice));
-            rc[k] = run_device(devs[k], d, off.data(), ln.data(), b - a, sample_rate, cfg, nullptr, outs + a);
-            SDSP_HIP_CHECK(hipFree(d));
-        } catch (const std::exception& e) {
-            std::fprintf(stderr, "sdsp_analyze_batch: %s\n", e.what());
+            try {
+                const int32_t r = run_device(dev, slot[s].d, off.data(), ln.data(), b - a, sample_rate, cfg, nullptr, outs + a);
+                if (r != SDSP_OK) rc[k] = r;
+            } catch (const std::exception& e) {
+                std::fprintf(stderr, "sdsp_analyze_batch: %s\n", e.what());
+                fail_chunk((size_t)c, e.what());
+                rc[k] = SDSP_ERR_PROCESSING;
+            }
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                ready[s] = -1;
+            }
+            cv.notify_all();
+            s ^= 1;
+        }
+        cp.join();
+        if (!copy_err.empty()) {
+            std::fprintf(stderr, "sdsp_analyze_batch: %s\n", copy_err.c_str());
             rc[k] = SDSP_ERR_PROCESSING;
         }
+        for (auto& sl : slot)
+            if (sl.d) (void)hipFree(sl.d);
     };
-    if (nd == 1) {
-        work(0);
+    if (devs.size() == 1) {
+        device_worker(0);
     } else {
         std::vector<std::thread> th;
-        for (size_t k = 0; k < nd; k++) th.emplace_back(work, k);
+        for (size_t k = 0; k < devs.size(); k++) th.emplace_back(device_worker, k);
         for (auto& t : th) t.join();
     }
     for (auto v : rc)

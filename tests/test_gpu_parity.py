@@ -117,6 +117,23 @@ def test_sub_batches_match_one_batch(monkeypatch):
         assert a == b, i
 
 
+def test_host_batch_chunks_match_one_chunk(monkeypatch):
+    """sdsp_analyze_batch's chunked work queue (copy of chunk k+1 overlapping the analysis of
+    chunk k): 3-track chunks give the same results as one chunk, empty tracks included."""
+    tracks = [synth.make_track(700 + s, seconds=8.0 + 2.0 * (s % 5))[0] for s in range(11)]
+    tracks.insert(4, np.zeros(0, np.float32))
+    whole = sdsp.analyze_batch(tracks, 44100)
+    monkeypatch.setenv("SDSP_BATCH_CHUNK_TRACKS", "3")
+    split = sdsp.analyze_batch(tracks, 44100)
+    for i, (a, b) in enumerate(zip(whole, split)):
+        if isinstance(a, sdsp.AnalysisError):
+            assert isinstance(b, sdsp.AnalysisError) and a.code == b.code, i
+            continue
+        a = {k: v for k, v in a.items() if k != "metadata"} | {"d": a["metadata"]["duration_seconds"]}
+        b = {k: v for k, v in b.items() if k != "metadata"} | {"d": b["metadata"]["duration_seconds"]}
+        assert a == b, i
+
+
 def test_device_generated_3min_tracks():
     """Device-resident batch (the bench path) on two 3-min synthetic tracks, checked on the host."""
     n, L = 2, 44100 * 180
