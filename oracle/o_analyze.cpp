@@ -442,12 +442,29 @@ void analyze(const float* samples, size_t n, uint32_t sr, const sdsp_config& c, 
         hpcp_frames(ks, sr, kfft, c.soft_mapping_sigma, (size_t)c.key_hpcp_peaks_per_frame,
                     (size_t)c.key_hpcp_num_harmonics, c.key_hpcp_harmonic_decay, c.key_hpcp_mag_power, &chroma,
                     &energies);
-        const size_t F = ks.frames;
-        if (c.chroma_sharpening_power > 1.0f) not_impl("chroma sharpening");
-        if (F > 5) smooth_chroma_inplace(chroma, F, 5);  // :1211-1213
-        if (c.enable_key_edge_trim) not_impl("key edge trim");
+        const size_t F_all = ks.frames;
+        if (c.chroma_sharpening_power > 1.0f)  // :1200-1208
+            for (size_t f = 0; f < F_all; f++) sharpen_chroma_inplace(chroma.data() + f * 12, c.chroma_sharpening_power);
+        if (F_all > 5) smooth_chroma_inplace(chroma, F_all, 5);  // :1211-1213
         tr.chroma = chroma;
         tr.energies = energies;
+        // optional edge trim (:1215-1232): the middle of the frames
+        size_t t0 = 0, F = F_all;
+        if (c.enable_key_edge_trim && energies.size() == F_all && F_all >= 200) {
+            const float frac = sd_clampf(c.key_edge_trim_fraction, 0.0f, 0.49f);
+            const size_t st = (size_t)sd_roundf((float)F_all * frac);
+            const size_t en = (size_t)sd_roundf((float)F_all * (1.0f - frac));
+            if (en > st + 50 && en <= F_all) {
+                t0 = st;
+                F = en - st;
+            }
+        }
+        if (t0 > 0 || F != F_all) {
+            chroma.erase(chroma.begin(), chroma.begin() + (long)(t0 * 12));
+            chroma.resize(F * 12);
+            energies.erase(energies.begin(), energies.begin() + (long)t0);
+            energies.resize(F);
+        }
         // frame weights (:1236-1287)
         std::vector<float> weights;
         bool use_w = false;
@@ -487,18 +504,39 @@ void analyze(const float* samples, size_t n, uint32_t sr, const sdsp_config& c, 
         }
         tr.weights = weights;
         tr.weights_used = use_w;
-        if (c.enable_key_ensemble) not_impl("key ensemble");
-        if (c.key_template_set != SDSP_TEMPLATES_KRUMHANSL_KESSLER) not_impl("Temperley templates");
         float maj[12][12], mnr[12][12];
-        key_templates(maj, mnr);
-        if (c.enable_key_multi_scale && c.key_multi_scale_lengths_len > 0) not_impl("multi-scale key");
-        if (c.enable_key_mode_heuristic || c.enable_key_minor_harmonic_bonus) not_impl("key mode heuristic");
+        key_templates(maj, mnr, c.key_template_set == SDSP_TEMPLATES_TEMPERLEY ? 1 : 0);
+        ModeHeuristic mh;
+        mh.on = c.enable_key_mode_heuristic || c.enable_key_minor_harmonic_bonus;
+        mh.third_margin = c.key_mode_third_ratio_margin;
+        mh.flip_ratio = c.enable_key_mode_heuristic ? c.key_mode_flip_min_score_ratio : 0.0f;
+        mh.bonus = c.enable_key_minor_harmonic_bonus;
+        mh.bonus_w = c.key_minor_leading_tone_bonus_weight;
+        std::vector<size_t> ms_len;
+        for (uint64_t i = 0; i < c.key_multi_scale_lengths_len; i++) ms_len.push_back((size_t)c.key_multi_scale_lengths[i]);
+        std::vector<float> ms_w(c.key_multi_scale_weights, c.key_multi_scale_weights + c.key_multi_scale_weights_len);
         const float* wp = use_w ? weights.data() : nullptr;
+        auto detect_full = [&]() {
+            return mh.on ? detect_key_weighted_mode_heuristic(chroma.data(), F, wp, maj, mnr, mh)
+                         : detect_key_weighted(chroma.data(), F, wp, maj, mnr);
+        };
         try {
             KeyResult kr;
             float clarity;
             const size_t seg_len_cfg = (size_t)c.key_segment_len_frames;
-            if (c.enable_key_segment_voting && F >= std::max<size_t>(seg_len_cfg, 1) && seg_len_cfg >= 120 &&
+            const size_t ms_min = ms_len.empty() ? 1 : *std::min_element(ms_len.begin(), ms_len.end());
+            if (c.enable_key_ensemble) {  // :1289-1299
+                kr = detect_key_ensemble(chroma.data(), F, wp, c.key_ensemble_kk_weight, c.key_ensemble_temperley_weight);
+                clarity = key_clarity(kr.scores, 24);
+            } else if (c.enable_key_multi_scale && !ms_len.empty() && F >= ms_min) {  // :1304-1330
+                int used = 0;
+                if (!detect_key_multi_scale(chroma.data(), F, wp, maj, mnr, ms_len, (size_t)c.key_multi_scale_hop,
+                                            sd_clampf(c.key_multi_scale_min_clarity, 0.0f, 1.0f),
+                                            ms_w.empty() ? nullptr : &ms_w, mh, &kr, &used))
+                    kr = detect_full();
+                tr.used_segments = used;
+                clarity = key_clarity(kr.scores, 24);
+            } else if (c.enable_key_segment_voting && F >= std::max<size_t>(seg_len_cfg, 1) && seg_len_cfg >= 120 &&
                 c.key_segment_hop_frames >= 1) {
                 const size_t seg_len = std::min(seg_len_cfg, F);
                 const size_t hop = std::max<size_t>(std::min<size_t>((size_t)c.key_segment_hop_frames, seg_len), 1);
@@ -506,7 +544,10 @@ void analyze(const float* samples, size_t n, uint32_t sr, const sdsp_config& c, 
                 float acc[24] = {0};
                 int used = 0;
                 for (size_t st = 0; st + seg_len <= F; st += hop) {
-                    KeyResult sr_ = detect_key_weighted(chroma.data() + st * 12, seg_len, wp ? wp + st : nullptr, maj, mnr);
+                    KeyResult sr_ = mh.on ? detect_key_weighted_mode_heuristic(chroma.data() + st * 12, seg_len,
+                                                                               wp ? wp + st : nullptr, maj, mnr, mh)
+                                          : detect_key_weighted(chroma.data() + st * 12, seg_len, wp ? wp + st : nullptr,
+                                                                maj, mnr);
                     const float cl = key_clarity(sr_.scores, 24);
                     if (cl >= min_cl) {
                         used++;
@@ -515,7 +556,7 @@ void analyze(const float* samples, size_t n, uint32_t sr, const sdsp_config& c, 
                 }
                 tr.used_segments = used;
                 if (used == 0) {
-                    kr = detect_key_weighted(chroma.data(), F, wp, maj, mnr);
+                    kr = detect_full();
                     clarity = key_clarity(kr.scores, 24);
                 } else {
                     int idx[24];
@@ -530,7 +571,7 @@ void analyze(const float* samples, size_t n, uint32_t sr, const sdsp_config& c, 
                     clarity = key_clarity(sorted, 24);
                 }
             } else {
-                kr = detect_key_weighted(chroma.data(), F, wp, maj, mnr);
+                kr = detect_full();
                 clarity = key_clarity(kr.scores, 24);
             }
             o.key_mode = kr.mode;

@@ -163,10 +163,15 @@ void smooth_chroma_inplace(std::vector<float>& ch, size_t frames, size_t window)
     ch.swap(out);
 }
 
-// templates.rs:64-145 (K-K profiles rotated, then L2-normalised per key in rotated order)
-void key_templates(float maj[12][12], float min_[12][12]) {
-    const float cM[12] = {6.35f, 2.23f, 3.48f, 2.33f, 4.38f, 4.09f, 2.52f, 5.19f, 2.39f, 3.66f, 2.29f, 2.88f};
-    const float cm[12] = {6.33f, 2.68f, 3.52f, 5.38f, 2.60f, 3.53f, 2.54f, 4.75f, 3.98f, 2.69f, 3.34f, 3.17f};
+// templates.rs:64-145 (K-K) and :147-235 (Temperley): profiles rotated, then L2-normalised per
+// key in rotated order
+void key_templates(float maj[12][12], float min_[12][12], int template_set) {
+    const float kM[12] = {6.35f, 2.23f, 3.48f, 2.33f, 4.38f, 4.09f, 2.52f, 5.19f, 2.39f, 3.66f, 2.29f, 2.88f};
+    const float km[12] = {6.33f, 2.68f, 3.52f, 5.38f, 2.60f, 3.53f, 2.54f, 4.75f, 3.98f, 2.69f, 3.34f, 3.17f};
+    const float tM[12] = {5.0f, 2.0f, 3.5f, 2.0f, 4.5f, 4.0f, 2.0f, 4.5f, 2.0f, 3.5f, 1.5f, 4.0f};
+    const float tm[12] = {5.0f, 2.0f, 3.5f, 5.0f, 2.0f, 3.5f, 2.0f, 4.5f, 3.5f, 2.0f, 4.0f, 3.5f};
+    const float* cM = template_set == 1 ? tM : kM;
+    const float* cm = template_set == 1 ? tm : km;
     for (int k = 0; k < 12; k++)
         for (int s = 0; s < 12; s++) {
             maj[k][s] = cM[(s + 12 - k) % 12];
@@ -266,6 +271,202 @@ KeyResult detect_key_weighted(const float* ch, size_t frames, const float* w, co
     const float bo = r.scores[1];  // first entry whose key != final key
     r.confidence = fs > 0.0f ? sd_clampf((fs - bo) / fs, 0.0f, 1.0f) : 0.0f;
     return r;
+}
+
+// chroma/normalization.rs:41-65: x^p, L2-normalise (EPSILON 1e-10), else uniform 1/sqrt(12)
+void sharpen_chroma_inplace(float* ch, float power) {
+    float sq = 0.0f;
+    for (int i = 0; i < 12; i++) {
+        ch[i] = sd_powf(ch[i], power);
+        sq += ch[i] * ch[i];
+    }
+    const float norm = __builtin_sqrtf(sq);
+    if (norm > 1e-10f) {
+        for (int i = 0; i < 12; i++) ch[i] /= norm;
+    } else {
+        const float u = 1.0f / __builtin_sqrtf(12.0f);
+        for (int i = 0; i < 12; i++) ch[i] = u;
+    }
+}
+
+// detector.rs:326-506.  `scores`/`order` of the result are the post-bonus table, stably re-sorted
+// from the base result's order; mode/tonic/confidence are the (possibly mode-flipped) choice.
+KeyResult detect_key_weighted_mode_heuristic(const float* ch, size_t frames, const float* w, const float maj[12][12],
+                                             const float mnr[12][12], const ModeHeuristic& mh) {
+    const KeyResult base = detect_key_weighted(ch, frames, w, maj, mnr);
+    const float flip_ratio = sd_clampf(mh.flip_ratio, 0.0f, 1.0f);
+    const bool mode_flip = flip_ratio > 0.0f;
+    if (!mh.bonus && !mode_flip) return base;
+    float avg[12] = {0};
+    float wsum = 0.0f;
+    if (!w) {
+        for (size_t f = 0; f < frames; f++)
+            for (int i = 0; i < 12; i++) avg[i] += ch[f * 12 + i];
+        wsum = (float)frames;
+    } else {
+        for (size_t f = 0; f < frames; f++) {
+            const float wt = w[f];
+            if (wt <= 0.0f) continue;
+            for (int i = 0; i < 12; i++) avg[i] += wt * ch[f * 12 + i];
+            wsum += wt;
+        }
+    }
+    if (wsum <= 1e-9f) return base;
+    float sum = -0.0f;
+    for (int i = 0; i < 12; i++) sum += avg[i];
+    if (sum > 1e-9f)
+        for (int i = 0; i < 12; i++) avg[i] /= sum;
+    float sc[24];
+    int ord[24];
+    for (int i = 0; i < 24; i++) {
+        sc[i] = base.scores[i];
+        ord[i] = base.order[i];
+    }
+    if (mh.bonus) {
+        const float bw = sd_maxf(mh.bonus_w, 0.0f);
+        if (bw > 0.0f)
+            for (int i = 0; i < 24; i++)
+                if (ord[i] >= 12) {
+                    const int tonic = ord[i] - 12;
+                    const int lt = (tonic + 11) % 12, b7 = (tonic + 10) % 12;
+                    sc[i] += wsum * bw * (avg[lt] - avg[b7]);
+                }
+    }
+    {  // stable sort desc of the base-ordered table
+        int idx[24];
+        for (int i = 0; i < 24; i++) idx[i] = i;
+        std::stable_sort(idx, idx + 24, [&](int a, int b) { return sc[b] < sc[a]; });
+        float s2[24];
+        int o2[24];
+        for (int i = 0; i < 24; i++) {
+            s2[i] = sc[idx[i]];
+            o2[i] = ord[idx[i]];
+        }
+        for (int i = 0; i < 24; i++) {
+            sc[i] = s2[i];
+            ord[i] = o2[i];
+        }
+    }
+    float major_s[12] = {0}, minor_s[12] = {0};
+    for (int i = 0; i < 24; i++) (ord[i] < 12 ? major_s[ord[i]] : minor_s[ord[i] - 12]) = sc[i];
+    const int best = ord[0];
+    const int tonic = best % 12;
+    const bool best_major = best < 12;
+    const float p_min3 = avg[(tonic + 3) % 12], p_maj3 = avg[(tonic + 4) % 12];
+    const float p_min6 = avg[(tonic + 8) % 12], p_maj6 = avg[(tonic + 9) % 12];
+    const float p_min7 = avg[(tonic + 10) % 12], p_maj7 = avg[(tonic + 11) % 12];
+    const float margin = sd_maxf(mh.third_margin, 0.0f);
+    float minor_score = 0.0f, major_score = 0.0f;
+    const float third = sd_absf(p_min3 - p_maj3);
+    if (p_min3 > p_maj3 * (1.0f + margin))
+        minor_score += third * 2.0f;
+    else if (p_maj3 > p_min3 * (1.0f + margin))
+        major_score += third * 2.0f;
+    const float sixth = sd_absf(p_min6 - p_maj6);
+    if (p_min6 > p_maj6 * (1.0f + margin))
+        minor_score += sixth * 1.0f;
+    else if (p_maj6 > p_min6 * (1.0f + margin))
+        major_score += sixth * 1.0f;
+    const float seventh = sd_absf(p_min7 - p_maj7);
+    if (p_min7 > p_maj7 * (1.0f + margin))
+        minor_score += seventh * 1.0f;
+    else if (p_maj7 > p_min7 * (1.0f + margin))
+        major_score += seventh * 1.0f;
+    const float total = minor_score + major_score;
+    const bool minor_pref = total > 1e-9f ? minor_score > major_score * (1.0f + margin * 0.5f) : false;
+    const bool major_pref = total > 1e-9f ? major_score > minor_score * (1.0f + margin * 0.5f) : false;
+    int chosen = best;
+    if (mode_flip) {
+        if (best_major && minor_pref) {
+            const float sb = major_s[tonic], sa = minor_s[tonic];
+            if (sb > 0.0f && sa >= sb * flip_ratio) chosen = 12 + tonic;
+        } else if (!best_major && major_pref) {
+            const float sb = minor_s[tonic], sa = major_s[tonic];
+            if (sb > 0.0f && sa >= sb * flip_ratio) chosen = tonic;
+        }
+    }
+    const float chosen_s = chosen < 12 ? major_s[chosen] : minor_s[chosen - 12];
+    float best_other = 0.0f;
+    for (int i = 0; i < 24; i++)
+        if (ord[i] != chosen) best_other = sd_maxf(best_other, sc[i]);
+    KeyResult r{};
+    for (int i = 0; i < 24; i++) {
+        r.scores[i] = sc[i];
+        r.order[i] = ord[i];
+    }
+    r.mode = chosen < 12 ? 0 : 1;
+    r.tonic = (uint32_t)(chosen % 12);
+    r.confidence = chosen_s > 0.0f ? sd_clampf((chosen_s - best_other) / chosen_s, 0.0f, 1.0f) : 0.0f;
+    return r;
+}
+
+static KeyResult from_table(const float acc[24]) {  // stable sort desc + (best - second) / best
+    int idx[24];
+    for (int i = 0; i < 24; i++) idx[i] = i;
+    std::stable_sort(idx, idx + 24, [&](int a, int b) { return acc[b] < acc[a]; });
+    KeyResult r{};
+    for (int i = 0; i < 24; i++) {
+        r.order[i] = idx[i];
+        r.scores[i] = acc[idx[i]];
+    }
+    r.mode = idx[0] < 12 ? 0 : 1;
+    r.tonic = (uint32_t)(idx[0] % 12);
+    const float bs = r.scores[0], ss = r.scores[1];
+    r.confidence = bs > 0.0f ? sd_clampf((bs - ss) / bs, 0.0f, 1.0f) : 0.0f;
+    return r;
+}
+
+// detector.rs:881-978
+KeyResult detect_key_ensemble(const float* ch, size_t frames, const float* w, float kk_weight, float temp_weight) {
+    const float total = kk_weight + temp_weight;
+    const float kk_norm = total > 1e-9f ? kk_weight / total : 0.5f;
+    const float tp_norm = total > 1e-9f ? temp_weight / total : 0.5f;
+    float km[12][12], kn[12][12], tm[12][12], tn[12][12];
+    key_templates(km, kn, 0);
+    key_templates(tm, tn, 1);
+    const KeyResult a = detect_key_weighted(ch, frames, w, km, kn);
+    const KeyResult b = detect_key_weighted(ch, frames, w, tm, tn);
+    float sa[24], sb[24], comb[24];
+    for (int i = 0; i < 24; i++) {
+        sa[a.order[i]] = a.scores[i];
+        sb[b.order[i]] = b.scores[i];
+    }
+    for (int k = 0; k < 24; k++) comb[k] = kk_norm * sa[k] + tp_norm * sb[k];
+    return from_table(comb);
+}
+
+// detector.rs:546-719 (the fallback to full-track detection is the caller's)
+bool detect_key_multi_scale(const float* ch, size_t frames, const float* w, const float maj[12][12],
+                            const float mnr[12][12], const std::vector<size_t>& lengths, size_t hop_in, float min_cl,
+                            const std::vector<float>* scale_w, const ModeHeuristic& mh, KeyResult* out,
+                            int* used_segments) {
+    float acc[24] = {0};
+    float total_w = 0.0f;
+    int used = 0;
+    const size_t hop = std::max<size_t>(hop_in, 1);
+    for (size_t si = 0; si < lengths.size(); si++) {
+        const size_t len = lengths[si];
+        if (len == 0 || len > frames) continue;
+        const float sw = (scale_w && si < scale_w->size()) ? (*scale_w)[si] : 1.0f;
+        if (sw <= 0.0f) continue;
+        for (size_t st = 0; st + len <= frames; st += hop) {
+            const KeyResult r = mh.on ? detect_key_weighted_mode_heuristic(ch + st * 12, len, w ? w + st : nullptr, maj,
+                                                                           mnr, mh)
+                                      : detect_key_weighted(ch + st * 12, len, w ? w + st : nullptr, maj, mnr);
+            const float cl = key_clarity(r.scores, 24);
+            if (cl >= min_cl) {
+                used++;
+                const float cw = cl * sw;
+                total_w += cw;
+                for (int i = 0; i < 24; i++) acc[r.order[i]] += r.scores[i] * cw;
+            }
+        }
+    }
+    *used_segments = used;
+    if (used == 0 || total_w <= 1e-12f) return false;
+    for (int k = 0; k < 24; k++) acc[k] /= total_w;
+    *out = from_table(acc);
+    return true;
 }
 
 // key_clarity.rs:51-93 (scores in the given order)

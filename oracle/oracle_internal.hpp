@@ -123,10 +123,26 @@ struct KeyResult {
     float scores[24];
     int order[24];  // key index (mode*12+tonic) of scores[i]
 };
-void key_templates(float major[12][12], float minor[12][12]);
+void key_templates(float major[12][12], float minor[12][12], int template_set = 0);
 KeyResult detect_key_weighted(const float* chroma, size_t frames, const float* weights,
                               const float maj[12][12], const float min[12][12]);
 float key_clarity(const float* sorted_scores, int n);
+void sharpen_chroma_inplace(float* ch12, float power);
+struct ModeHeuristic {
+    bool on = false;  // enable_key_mode_heuristic || enable_key_minor_harmonic_bonus
+    float third_margin = 0.0f, flip_ratio = 0.0f, bonus_w = 0.0f;
+    bool bonus = false;
+};
+KeyResult detect_key_weighted_mode_heuristic(const float* chroma, size_t frames, const float* weights,
+                                             const float maj[12][12], const float min[12][12],
+                                             const ModeHeuristic& mh);
+KeyResult detect_key_ensemble(const float* chroma, size_t frames, const float* weights, float kk_weight,
+                              float temperley_weight);
+// detect_key_multi_scale; returns false when no segment qualified (the caller falls back)
+bool detect_key_multi_scale(const float* chroma, size_t frames, const float* weights, const float maj[12][12],
+                            const float min[12][12], const std::vector<size_t>& lengths, size_t hop, float min_clarity,
+                            const std::vector<float>* scale_weights, const ModeHeuristic& mh, KeyResult* out,
+                            int* used_segments);
 
 // ---------- trace (test probes) ----------
 struct Trace {

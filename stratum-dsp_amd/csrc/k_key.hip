@@ -363,9 +363,116 @@ __device__ float clarity_of(const float* s) {
 // circle_of_fifths = [0,7,2,9,4,11,6,1,8,3,10,5] for the tonic (detector.rs:214-224); that
 // array is its own inverse, so position(t) = circle_of_fifths[t].
 
+// stable sort desc of a 24-entry score table by key index, (best - second) / best
+__device__ void from_table(const float* acc, float sorted[24], int order[24], float* conf) {
+    for (int k = 0; k < 24; k++) order[k] = k;
+    for (int a = 1; a < 24; a++) {
+        const int o = order[a];
+        int b = a;
+        while (b > 0 && acc[order[b - 1]] < acc[o]) {
+            order[b] = order[b - 1];
+            b--;
+        }
+        order[b] = o;
+    }
+    for (int k = 0; k < 24; k++) sorted[k] = acc[order[k]];
+    *conf = sorted[0] > 0.0f ? sd_clampf((sorted[0] - sorted[1]) / sorted[0], 0.0f, 1.0f) : 0.0f;
+}
+
+// detect_key_weighted_mode_heuristic on a base result (detector.rs:326-506): sorted/order become
+// the post-bonus table (stable re-sort of the base order), *chosen the possibly mode-flipped key
+// index (mode * 12 + tonic) and *conf its confidence.  avg_in: the raw weighted chroma sums,
+// wsum: their weight total.
+__device__ void mode_heuristic(float sorted[24], int order[24], const float* avg_in, float wsum, const KeyParams& P,
+                               int* chosen, float* conf) {
+    *chosen = order[0];
+    *conf = sorted[0] > 0.0f ? sd_clampf((sorted[0] - sorted[1]) / sorted[0], 0.0f, 1.0f) : 0.0f;
+    const float flip_ratio = sd_clampf(P.mh_flip, 0.0f, 1.0f);
+    const bool mode_flip = flip_ratio > 0.0f;
+    if (!P.mh_bonus && !mode_flip) return;
+    if (wsum <= 1e-9f) return;
+    float avg[12];
+    float sum = -0.0f;
+    for (int i = 0; i < 12; i++) {
+        avg[i] = avg_in[i];
+        sum += avg[i];
+    }
+    if (sum > 1e-9f)
+        for (int i = 0; i < 12; i++) avg[i] /= sum;
+    if (P.mh_bonus) {
+        const float bw = sd_maxf(P.mh_bonus_w, 0.0f);
+        if (bw > 0.0f)
+            for (int i = 0; i < 24; i++)
+                if (order[i] >= 12) {
+                    const int tonic = order[i] - 12;
+                    sorted[i] += wsum * bw * (avg[(tonic + 11) % 12] - avg[(tonic + 10) % 12]);
+                }
+    }
+    for (int a = 1; a < 24; a++) {  // stable insertion sort of the base-ordered table, desc
+        const float v = sorted[a];
+        const int o = order[a];
+        int b = a;
+        while (b > 0 && sorted[b - 1] < v) {
+            sorted[b] = sorted[b - 1];
+            order[b] = order[b - 1];
+            b--;
+        }
+        sorted[b] = v;
+        order[b] = o;
+    }
+    float maj_s[12], min_s[12];
+    for (int i = 0; i < 24; i++) {
+        if (order[i] < 12)
+            maj_s[order[i]] = sorted[i];
+        else
+            min_s[order[i] - 12] = sorted[i];
+    }
+    const int best = order[0], tonic = best % 12;
+    const bool best_major = best < 12;
+    const float p_min3 = avg[(tonic + 3) % 12], p_maj3 = avg[(tonic + 4) % 12];
+    const float p_min6 = avg[(tonic + 8) % 12], p_maj6 = avg[(tonic + 9) % 12];
+    const float p_min7 = avg[(tonic + 10) % 12], p_maj7 = avg[(tonic + 11) % 12];
+    const float margin = sd_maxf(P.mh_margin, 0.0f);
+    float minor_score = 0.0f, major_score = 0.0f;
+    const float third = sd_absf(p_min3 - p_maj3);
+    if (p_min3 > p_maj3 * (1.0f + margin))
+        minor_score += third * 2.0f;
+    else if (p_maj3 > p_min3 * (1.0f + margin))
+        major_score += third * 2.0f;
+    const float sixth = sd_absf(p_min6 - p_maj6);
+    if (p_min6 > p_maj6 * (1.0f + margin))
+        minor_score += sixth * 1.0f;
+    else if (p_maj6 > p_min6 * (1.0f + margin))
+        major_score += sixth * 1.0f;
+    const float seventh = sd_absf(p_min7 - p_maj7);
+    if (p_min7 > p_maj7 * (1.0f + margin))
+        minor_score += seventh * 1.0f;
+    else if (p_maj7 > p_min7 * (1.0f + margin))
+        major_score += seventh * 1.0f;
+    const float total = minor_score + major_score;
+    const bool minor_pref = total > 1e-9f ? minor_score > major_score * (1.0f + margin * 0.5f) : false;
+    const bool major_pref = total > 1e-9f ? major_score > minor_score * (1.0f + margin * 0.5f) : false;
+    int ch = best;
+    if (mode_flip) {
+        if (best_major && minor_pref) {
+            if (maj_s[tonic] > 0.0f && min_s[tonic] >= maj_s[tonic] * flip_ratio) ch = 12 + tonic;
+        } else if (!best_major && major_pref) {
+            if (min_s[tonic] > 0.0f && maj_s[tonic] >= min_s[tonic] * flip_ratio) ch = tonic;
+        }
+    }
+    const float cs = ch < 12 ? maj_s[ch] : min_s[ch - 12];
+    float other = 0.0f;
+    for (int i = 0; i < 24; i++)
+        if (order[i] != ch) other = sd_maxf(other, sorted[i]);
+    *chosen = ch;
+    *conf = cs > 0.0f ? sd_clampf((cs - other) / cs, 0.0f, 1.0f) : 0.0f;
+}
+
+constexpr int KV_ROW = 64;  // segment scratch row: 24 sorted, 24 order, clarity, used, cw, wsum, avg[12]
+constexpr int KV_MAXSCALE = 8;
+
 __global__ __launch_bounds__(256) void k_key_vote(const int* __restrict__ tracks, int n_items,
-                                                  const uint64_t* __restrict__ frame_pfx,
-                                                  const float* __restrict__ chroma_raw,
+                                                  const uint64_t* __restrict__ frame_pfx, float* __restrict__ chroma_raw,
                                                   const float* __restrict__ energy, float* __restrict__ chroma_s,
                                                   float* __restrict__ weights, float* __restrict__ seg_scratch,
                                                   const uint64_t* __restrict__ seg_off, const float* __restrict__ tmpl,
@@ -373,32 +480,52 @@ __global__ __launch_bounds__(256) void k_key_vote(const int* __restrict__ tracks
     __shared__ int hist[256];
     __shared__ int misc[4];
     __shared__ int redi[8];
-    __shared__ float acc[24];
+    __shared__ float acc[48];
     __shared__ int use_w_s, used_s;
-    __shared__ float tpl[24][12];
+    __shared__ float totw_s;
+    __shared__ float tpl[48][12];
+    __shared__ int sc_len[KV_MAXSCALE], sc_pfx[KV_MAXSCALE + 1];
+    __shared__ float sc_w[KV_MAXSCALE];
     const int it = blockIdx.x;
     const int trk = tracks[it];
-    const int64_t F = (int64_t)(frame_pfx[trk + 1] - frame_pfx[trk]);
+    const int64_t F_all = (int64_t)(frame_pfx[trk + 1] - frame_pfx[trk]);
     const uint64_t g0 = frame_pfx[trk];
-    const float* cr = chroma_raw + g0 * 12;
-    float* cs = chroma_s + g0 * 12;
-    float* w = weights + g0;
-    const float* en = energy + g0;
-    for (int k = threadIdx.x; k < 288; k += blockDim.x) tpl[k / 12][k % 12] = tmpl[k];
-    if (F <= 0) {
+    float* cr = chroma_raw + g0 * 12;
+    for (int k = threadIdx.x; k < 576; k += blockDim.x) tpl[k / 12][k % 12] = tmpl[k];
+    if (F_all <= 0) {
         if (threadIdx.x == 0) out[trk] = KeyOut{0, 0, 0.0f, 0.0f, 0, 0, 0};
         return;
     }
+    // chroma sharpening (src/lib.rs:1200-1208 -> chroma/normalization.rs:41-65), in place
+    if (P.sharpen > 1.0f) {
+        for (int64_t f = threadIdx.x; f < F_all; f += blockDim.x) {
+            float* c = cr + f * 12;
+            float sq = 0.0f;
+            for (int i = 0; i < 12; i++) {
+                c[i] = sd_powf(c[i], P.sharpen);
+                sq += c[i] * c[i];
+            }
+            const float nrm = __builtin_sqrtf(sq);
+            if (nrm > 1e-10f) {
+                for (int i = 0; i < 12; i++) c[i] /= nrm;
+            } else {
+                const float u = 1.0f / __builtin_sqrtf(12.0f);
+                for (int i = 0; i < 12; i++) c[i] = u;
+            }
+        }
+        __syncthreads();
+    }
     // median smoothing, window 5 (src/lib.rs:1211-1213 -> smoothing.rs:37-94)
-    for (int64_t q = threadIdx.x; q < F * 12; q += blockDim.x) {
+    float* cs_all = chroma_s + g0 * 12;
+    for (int64_t q = threadIdx.x; q < F_all * 12; q += blockDim.x) {
         const int64_t f = q / 12;
         const int s = (int)(q % 12);
-        if (F > 5) {
+        if (F_all > 5) {
             float v[5];
             int n = 0;
             for (int o = -2; o <= 2; o++) {
                 const int64_t fi = f + o;
-                if (fi >= 0 && fi < F) v[n++] = cr[fi * 12 + s];
+                if (fi >= 0 && fi < F_all) v[n++] = cr[fi * 12 + s];
             }
             for (int a = 1; a < n; a++) {
                 const float x = v[a];
@@ -409,13 +536,27 @@ __global__ __launch_bounds__(256) void k_key_vote(const int* __restrict__ tracks
                 }
                 v[b] = x;
             }
-            cs[q] = v[n / 2];
+            cs_all[q] = v[n / 2];
         } else {
-            cs[q] = cr[q];
+            cs_all[q] = cr[q];
         }
     }
     __syncthreads();
-    // frame weights (src/lib.rs:1236-1287)
+    // optional edge trim (src/lib.rs:1215-1232): keep the middle frames
+    int64_t t0 = 0, F = F_all;
+    if (P.edge_trim && F_all >= 200) {
+        const float frac = sd_clampf(P.edge_frac, 0.0f, 0.49f);
+        const int64_t st = (int64_t)sd_roundf((float)F_all * frac);
+        const int64_t en_ = (int64_t)sd_roundf((float)F_all * (1.0f - frac));
+        if (en_ > st + 50 && en_ <= F_all) {
+            t0 = st;
+            F = en_ - st;
+        }
+    }
+    const float* cs = cs_all + t0 * 12;
+    const float* en = energy + g0 + t0;
+    float* w = weights + g0 + t0;
+    // frame weights over the slice (src/lib.rs:1236-1287)
     if (P.weighting) {
         const float med = sd_maxf(block_select_kth(en, (int)F, (int)(F / 2), hist, misc), 1e-12f);
         const float ln12 = sd_logf(12.0f);
@@ -451,9 +592,10 @@ __global__ __launch_bounds__(256) void k_key_vote(const int* __restrict__ tracks
     }
     __syncthreads();
     const bool use_w = use_w_s;
-    auto wsd = [&](int64_t f0, int64_t n, int key) {  // weighted_sum_dot, detector.rs:984-1001
+    const int toff = P.tset == 1 ? 24 : 0;  // template rows of the selected set
+    auto wsd = [&](int64_t f0, int64_t n, int row) {  // weighted_sum_dot, detector.rs:984-1001
         float a = 0.0f;
-        const float* t = tpl[key];
+        const float* t = tpl[row];
         for (int64_t f = f0; f < f0 + n; f++) {
             const float* c = cs + f * 12;
             if (use_w) {
@@ -471,98 +613,188 @@ __global__ __launch_bounds__(256) void k_key_vote(const int* __restrict__ tracks
         }
         return a;
     };
-    int nseg = 0;
-    if (P.seg_voting && F >= P.seg_len) nseg = (int)((F - P.seg_len) / P.seg_hop) + 1;
-    float* S = seg_scratch + seg_off[it];  // nseg x (24 sorted scores + 24 order + clarity + used)
-    if (nseg > 0) {
-        for (int q = threadIdx.x; q < nseg * 24; q += blockDim.x) {
-            const int sg = q / 24, k = q % 24;
-            S[(size_t)sg * 50 + k] = wsd((int64_t)sg * P.seg_hop, P.seg_len, k);  // raw score
+    // the heuristic's weighted chroma sums (detector.rs:344-368): i < 12 -> avg[i], 12 -> wsum
+    auto avg_sum = [&](int64_t f0, int64_t n, int i) {
+        if (!use_w && i == 12) return (float)n;
+        float a = 0.0f;
+        for (int64_t f = f0; f < f0 + n; f++) {
+            const float wt = use_w ? w[f] : 1.0f;
+            if (use_w && wt <= 0.0f) continue;
+            if (i == 12)
+                a += wt;
+            else
+                a += use_w ? wt * cs[f * 12 + i] : cs[f * 12 + i];
         }
+        return a;
+    };
+    auto write_out = [&](int key, float conf, float clarity, int used) {
+        KeyOut r{};
+        r.mode = key < 12 ? 0 : 1;
+        r.tonic = key % 12;
+        r.conf = conf;
+        r.clarity = clarity;
+        r.ok = 1;
+        r.used_segments = used;
+        r.weights_used = use_w;
+        out[trk] = r;
+    };
+    // full-slice detection: detect_key_weighted (+ the mode heuristic)
+    auto detect_full = [&](int used_segments) {
         __syncthreads();
-        for (int sg = threadIdx.x; sg < nseg; sg += blockDim.x) {
-            float raw[24], sorted[24];
-            int order[24];
-            for (int k = 0; k < 24; k++) raw[k] = S[(size_t)sg * 50 + k];
-            key_from_raw(raw, sorted, order);
-            const float cl = clarity_of(sorted);
-            for (int k = 0; k < 24; k++) {
-                S[(size_t)sg * 50 + k] = sorted[k];
-                S[(size_t)sg * 50 + 24 + k] = (float)order[k];
-            }
-            S[(size_t)sg * 50 + 48] = cl;
-            S[(size_t)sg * 50 + 49] = cl >= P.min_clarity ? 1.0f : 0.0f;
-        }
-        __syncthreads();
-        if (threadIdx.x < 24) {
-            const int key = threadIdx.x;
-            float a = 0.0f;
-            for (int sg = 0; sg < nseg; sg++) {
-                const float* row = S + (size_t)sg * 50;
-                if (row[49] == 0.0f) continue;
-                for (int k = 0; k < 24; k++)
-                    if ((int)row[24 + k] == key) {
-                        a += row[k] * row[48];
-                        break;
-                    }
-            }
-            acc[key] = a;
-        }
-        if (threadIdx.x == 0) {
-            int u = 0;
-            for (int sg = 0; sg < nseg; sg++) u += S[(size_t)sg * 50 + 49] != 0.0f;
-            used_s = u;
-        }
-        __syncthreads();
-    } else if (threadIdx.x == 0) {
-        used_s = 0;
-    }
-    __syncthreads();
-    const int used = used_s;
-    if (used == 0) {  // whole-slice detect_key_weighted
-        if (threadIdx.x < 24) acc[threadIdx.x] = wsd(0, F, threadIdx.x);
+        if (threadIdx.x < 24) acc[threadIdx.x] = wsd(0, F, toff + threadIdx.x);
+        if (P.mh_on && threadIdx.x >= 24 && threadIdx.x < 37) acc[threadIdx.x] = avg_sum(0, F, threadIdx.x - 24);
         __syncthreads();
         if (threadIdx.x == 0) {
             float raw[24], sorted[24];
             int order[24];
             for (int k = 0; k < 24; k++) raw[k] = acc[k];
             key_from_raw(raw, sorted, order);
-            KeyOut r{};
-            r.mode = order[0] < 12 ? 0 : 1;
-            r.tonic = order[0] % 12;
-            r.conf = sorted[0] > 0.0f ? sd_clampf((sorted[0] - sorted[1]) / sorted[0], 0.0f, 1.0f) : 0.0f;
-            r.clarity = clarity_of(sorted);
-            r.ok = 1;
-            r.used_segments = 0;
-            r.weights_used = use_w;
-            out[trk] = r;
+            int key = order[0];
+            float conf = sorted[0] > 0.0f ? sd_clampf((sorted[0] - sorted[1]) / sorted[0], 0.0f, 1.0f) : 0.0f;
+            if (P.mh_on) mode_heuristic(sorted, order, acc + 24, acc[36], P, &key, &conf);
+            write_out(key, conf, clarity_of(sorted), used_segments);
+        }
+    };
+    if (P.ensemble) {  // detect_key_ensemble (detector.rs:881-978), src/lib.rs:1289-1299
+        if (threadIdx.x < 48) acc[threadIdx.x] = wsd(0, F, threadIdx.x);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const float tot = P.kk_w + P.tp_w;
+            const float kn = tot > 1e-9f ? P.kk_w / tot : 0.5f;
+            const float tn = tot > 1e-9f ? P.tp_w / tot : 0.5f;
+            float raw[24], sorted[24], sa[24], sb[24], comb[24];
+            int order[24];
+            for (int k = 0; k < 24; k++) raw[k] = acc[k];
+            key_from_raw(raw, sorted, order);
+            for (int i = 0; i < 24; i++) sa[order[i]] = sorted[i];
+            for (int k = 0; k < 24; k++) raw[k] = acc[24 + k];
+            key_from_raw(raw, sorted, order);
+            for (int i = 0; i < 24; i++) sb[order[i]] = sorted[i];
+            for (int k = 0; k < 24; k++) comb[k] = kn * sa[k] + tn * sb[k];
+            float conf;
+            from_table(comb, sorted, order, &conf);
+            write_out(order[0], conf, clarity_of(sorted), 0);
         }
         return;
     }
+    // segment lists: multi-scale (detector.rs:546-719) or segment voting (src/lib.rs:1331-1436)
+    int mode = 0;  // 0 full, 1 multi-scale, 2 segment voting
+    if (P.ms_on && P.ms_n > 0) {
+        int mn = P.ms_len[0];
+        for (int i = 1; i < P.ms_n; i++) mn = min(mn, P.ms_len[i]);
+        if (F >= mn) mode = 1;
+    }
+    if (mode == 0 && P.seg_voting && F >= P.seg_len) mode = 2;
+    if (mode == 0) {
+        detect_full(0);
+        return;
+    }
     if (threadIdx.x == 0) {
-        int order[24];
-        for (int k = 0; k < 24; k++) order[k] = k;
-        for (int a = 1; a < 24; a++) {
-            const int o = order[a];
-            int b = a;
-            while (b > 0 && acc[order[b - 1]] < acc[o]) {
-                order[b] = order[b - 1];
-                b--;
-            }
-            order[b] = o;
+        int n = 0;
+        for (int si = 0; si < (mode == 1 ? P.ms_n : 1); si++) {
+            const int len = mode == 1 ? P.ms_len[si] : P.seg_len;
+            const int hop = mode == 1 ? max(P.ms_hop, 1) : P.seg_hop;
+            const float sw = mode == 1 ? (si < P.ms_nw ? P.ms_w[si] : 1.0f) : 1.0f;
+            sc_len[si] = len;
+            sc_w[si] = sw;
+            sc_pfx[si] = n;
+            if (!(len == 0 || len > F || sw <= 0.0f)) n += (int)((F - len) / hop) + 1;
         }
-        float sorted[24];
-        for (int k = 0; k < 24; k++) sorted[k] = acc[order[k]];
-        KeyOut r{};
-        r.mode = order[0] < 12 ? 0 : 1;
-        r.tonic = order[0] % 12;
-        const float bs = sorted[0], ss = sorted[1];
-        r.conf = bs > 0.0f ? sd_clampf((bs - ss) / bs, 0.0f, 1.0f) : 0.0f;
-        r.clarity = clarity_of(sorted);
-        r.ok = 1;
-        r.used_segments = used;
-        r.weights_used = use_w;
-        out[trk] = r;
+        sc_pfx[mode == 1 ? P.ms_n : 1] = n;
+    }
+    __syncthreads();
+    const int nsc = mode == 1 ? P.ms_n : 1;
+    const int nseg = sc_pfx[nsc];
+    auto seg_of = [&](int sg, int64_t* start, int* len, float* sw) {
+        int si = 0;
+        while (si + 1 < nsc && sc_pfx[si + 1] <= sg) si++;
+        const int hop = mode == 1 ? max(P.ms_hop, 1) : P.seg_hop;
+        *start = (int64_t)(sg - sc_pfx[si]) * hop;
+        *len = sc_len[si];
+        *sw = sc_w[si];
+    };
+    float* S = seg_scratch + seg_off[it];
+    for (int q = threadIdx.x; q < nseg * 24; q += blockDim.x) {
+        int64_t st;
+        int len;
+        float sw;
+        seg_of(q / 24, &st, &len, &sw);
+        S[(size_t)(q / 24) * KV_ROW + q % 24] = wsd(st, len, toff + q % 24);  // raw score
+    }
+    if (P.mh_on)
+        for (int q = threadIdx.x; q < nseg * 13; q += blockDim.x) {
+            int64_t st;
+            int len;
+            float sw;
+            seg_of(q / 13, &st, &len, &sw);
+            const int i = q % 13;
+            S[(size_t)(q / 13) * KV_ROW + (i == 12 ? 51 : 52 + i)] = avg_sum(st, len, i);
+        }
+    __syncthreads();
+    for (int sg = threadIdx.x; sg < nseg; sg += blockDim.x) {
+        float* row = S + (size_t)sg * KV_ROW;
+        float raw[24], sorted[24];
+        int order[24];
+        for (int k = 0; k < 24; k++) raw[k] = row[k];
+        key_from_raw(raw, sorted, order);
+        if (P.mh_on) {
+            int key;
+            float conf;
+            mode_heuristic(sorted, order, row + 52, row[51], P, &key, &conf);
+        }
+        int64_t st;
+        int len;
+        float sw;
+        seg_of(sg, &st, &len, &sw);
+        const float cl = clarity_of(sorted);
+        for (int k = 0; k < 24; k++) {
+            row[k] = sorted[k];
+            row[24 + k] = (float)order[k];
+        }
+        row[48] = cl;
+        row[49] = cl >= (mode == 1 ? P.ms_min_cl : P.min_clarity) ? 1.0f : 0.0f;
+        row[50] = cl * sw;
+    }
+    __syncthreads();
+    if (threadIdx.x < 24) {
+        const int key = threadIdx.x;
+        float a = 0.0f;
+        for (int sg = 0; sg < nseg; sg++) {
+            const float* row = S + (size_t)sg * KV_ROW;
+            if (row[49] == 0.0f) continue;
+            for (int k = 0; k < 24; k++)
+                if ((int)row[24 + k] == key) {
+                    a += row[k] * row[50];
+                    break;
+                }
+        }
+        acc[key] = a;
+    }
+    if (threadIdx.x == 32) {
+        int u = 0;
+        float tw = 0.0f;
+        for (int sg = 0; sg < nseg; sg++)
+            if (S[(size_t)sg * KV_ROW + 49] != 0.0f) {
+                u++;
+                tw += S[(size_t)sg * KV_ROW + 50];
+            }
+        used_s = u;
+        totw_s = tw;
+    }
+    __syncthreads();
+    const int used = used_s;
+    const float totw = totw_s;
+    if (used == 0 || (mode == 1 && totw <= 1e-12f)) {
+        detect_full(used);
+        return;
+    }
+    if (threadIdx.x == 0) {
+        float tab[24], sorted[24];
+        int order[24];
+        for (int k = 0; k < 24; k++) tab[k] = mode == 1 ? acc[k] / totw : acc[k];
+        float conf;
+        from_table(tab, sorted, order, &conf);
+        write_out(order[0], conf, clarity_of(sorted), used);
     }
 }
 
@@ -606,7 +838,7 @@ void launch_hpcp(const float* mags, const uint64_t* frame_pfx, const uint64_t* t
         hipLaunchKernelGGL(k_hpcp<HP_KMAX>, grid, block, 0, st, mags, frame_pfx, tile_pfx, tracks, n_items, P, harm,
                            chroma, energy);
 }
-void launch_key_vote(const int* tracks, int n_items, const uint64_t* frame_pfx, const float* chroma_raw,
+void launch_key_vote(const int* tracks, int n_items, const uint64_t* frame_pfx, float* chroma_raw,
                      const float* energy, float* chroma_s, float* weights, float* seg_scratch, const uint64_t* seg_off,
                      const float* tmpl, const KeyParams& P, KeyOut* out, hipStream_t st) {
     if (n_items == 0) return;

@@ -102,6 +102,20 @@ struct KeyParams {
     int seg_voting;
     int seg_len, seg_hop;
     float min_clarity;
+    // opt-in branches (src/lib.rs:1200-1470)
+    float sharpen;             // chroma_sharpening_power (applied when > 1)
+    int edge_trim;             // enable_key_edge_trim
+    float edge_frac;           // key_edge_trim_fraction
+    int ensemble;              // enable_key_ensemble
+    float kk_w, tp_w;          // key_ensemble_{kk,temperley}_weight
+    int tset;                  // key_template_set (0 K-K, 1 Temperley)
+    int mh_on, mh_bonus;       // mode heuristic || minor bonus; minor bonus
+    float mh_margin, mh_flip;  // third-ratio margin; flip ratio (0 unless the heuristic is on)
+    float mh_bonus_w;          // leading-tone bonus weight
+    int ms_on, ms_n, ms_hop, ms_nw;  // multi-scale: enabled, #lengths (<= 8), hop, #weights
+    float ms_min_cl;
+    int ms_len[8];
+    float ms_w[8];
 };
 struct KeyOut {
     int mode, tonic;
@@ -162,7 +176,7 @@ void launch_mask(float* mags, int stride, int B, const uint64_t* frame_pfx, cons
 void launch_hpcp(const float* mags, const uint64_t* frame_pfx, const uint64_t* tile_pfx, const int* tracks,
                  int n_items, uint64_t n_tiles, const HpcpParams& P, const HarmEntry* harm, float* chroma,
                  float* energy, hipStream_t st);
-void launch_key_vote(const int* tracks, int n_items, const uint64_t* frame_pfx, const float* chroma_raw,
+void launch_key_vote(const int* tracks, int n_items, const uint64_t* frame_pfx, float* chroma_raw,
                      const float* energy, float* chroma_s, float* weights, float* seg_scratch, const uint64_t* seg_off,
                      const float* tmpl, const KeyParams& P, KeyOut* out, hipStream_t st);
 void launch_synth(float* out, uint64_t n_tracks, uint64_t len, uint32_t sr, const float* bpm, const int* key,

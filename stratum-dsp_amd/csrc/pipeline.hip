@@ -197,13 +197,16 @@ std::vector<HarmEntry> harm_table(int B, uint32_t sr, int fft_size, float sigma_
     return t;
 }
 
-// templates.rs:64-145
-void kk_templates(float* out /*24x12*/) {
-    const float cM[12] = {6.35f, 2.23f, 3.48f, 2.33f, 4.38f, 4.09f, 2.52f, 5.19f, 2.39f, 3.66f, 2.29f, 2.88f};
-    const float cm[12] = {6.33f, 2.68f, 3.52f, 5.38f, 2.60f, 3.53f, 2.54f, 4.75f, 3.98f, 2.69f, 3.34f, 3.17f};
-    for (int k = 0; k < 24; k++) {
+// templates.rs:64-145 (Krumhansl-Kessler) and :147-235 (Temperley): rows 0-23 K-K major/minor
+// keys, rows 24-47 Temperley; each profile rotated to the key, then L2-normalised.
+void key_templates(float* out /*48x12*/) {
+    const float kM[12] = {6.35f, 2.23f, 3.48f, 2.33f, 4.38f, 4.09f, 2.52f, 5.19f, 2.39f, 3.66f, 2.29f, 2.88f};
+    const float km[12] = {6.33f, 2.68f, 3.52f, 5.38f, 2.60f, 3.53f, 2.54f, 4.75f, 3.98f, 2.69f, 3.34f, 3.17f};
+    const float tM[12] = {5.0f, 2.0f, 3.5f, 2.0f, 4.5f, 4.0f, 2.0f, 4.5f, 2.0f, 3.5f, 1.5f, 4.0f};
+    const float tm[12] = {5.0f, 2.0f, 3.5f, 5.0f, 2.0f, 3.5f, 2.0f, 4.5f, 3.5f, 2.0f, 4.0f, 3.5f};
+    for (int k = 0; k < 48; k++) {
         float* v = out + k * 12;
-        const float* base = k < 12 ? cM : cm;
+        const float* base = k < 24 ? (k < 12 ? kM : km) : (k < 36 ? tM : tm);
         const int key = k % 12;
         for (int s = 0; s < 12; s++) v[s] = base[(s + 12 - key) % 12];
         float sq = 0.0f;
@@ -345,12 +348,7 @@ std::string unsupported(const sdsp_config& c) {
         return "non-HPCP / bass-blend / whitened chroma";
     if (c.key_hpcp_peaks_per_frame > (uint64_t)HP_KMAX) return "key_hpcp_peaks_per_frame > 32";
     if (c.key_hpcp_num_harmonics > (uint64_t)SUPPORT_HMAX) return "key_hpcp_num_harmonics > 8";
-    if (c.chroma_sharpening_power > 1.0f) return "chroma sharpening";
-    if (c.enable_key_edge_trim) return "key edge trim";
-    if (c.enable_key_ensemble) return "key ensemble";
-    if (c.key_template_set != SDSP_TEMPLATES_KRUMHANSL_KESSLER) return "Temperley templates";
-    if (c.enable_key_multi_scale && c.key_multi_scale_lengths_len > 0) return "multi-scale key";
-    if (c.enable_key_mode_heuristic || c.enable_key_minor_harmonic_bonus) return "key mode heuristic";
+    if (c.enable_key_multi_scale && c.key_multi_scale_lengths_len > 8) return "more than 8 multi-scale key lengths";
     if (c.enable_ml_refinement) return "ML refinement";
     const bool use_aux = c.enable_tempogram_band_fusion || c.enable_tempogram_mel_novelty ||
                          c.tempogram_band_consensus_bonus > 0.0f;
@@ -807,6 +805,8 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     const int seg_hop = (int)std::max<uint64_t>(std::min<uint64_t>(cfg_.key_segment_hop_frames, (uint64_t)seg_len_cfg), 1);
     const bool seg_voting = cfg_.enable_key_segment_voting && cfg_.key_segment_len_frames >= 120 &&
                             cfg_.key_segment_hop_frames >= 1;
+    const bool ms_on = cfg_.enable_key_multi_scale && cfg_.key_multi_scale_lengths_len > 0;
+    const uint64_t ms_hop = std::max<uint64_t>(std::min<uint64_t>(cfg_.key_multi_scale_hop, INT32_MAX), 1);
     double key_in_bytes = 0;
     for (int i = 0; i < NR; i++) {
         const uint64_t n = bin.n_trim[(size_t)i];
@@ -815,8 +815,17 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         K.push_back(i);
         kpfx.push_back(kpfx.back() + F8);
         ktile.push_back(ktile.back() + (F8 + HP_FRAMES - 1) / HP_FRAMES);
-        const uint64_t ns = (seg_voting && F8 >= (uint64_t)std::max(seg_len_cfg, 1)) ? (F8 - seg_len_cfg) / seg_hop + 1 : 0;
-        kseg.push_back(kseg.back() + 50 * ns);
+        // segment rows (an upper bound: edge trim only shortens the frame range)
+        uint64_t ns = (seg_voting && F8 >= (uint64_t)std::max(seg_len_cfg, 1)) ? (F8 - seg_len_cfg) / seg_hop + 1 : 0;
+        if (ms_on) {
+            uint64_t nm = 0;
+            for (uint64_t j = 0; j < cfg_.key_multi_scale_lengths_len; j++) {
+                const uint64_t len = cfg_.key_multi_scale_lengths[j];
+                if (len != 0 && len <= F8) nm += (F8 - len) / ms_hop + 1;
+            }
+            ns = std::max(ns, nm);
+        }
+        kseg.push_back(kseg.back() + 64 * ns);
         ksrc.push_back(bin.src_off[(size_t)i]);
         kgain.push_back(bin.gain_h[(size_t)i]);
         key_in_bytes += 4.0 * (double)n;
@@ -883,8 +892,8 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         float* d_energy = c_.dev<float>("E.energy", total8);
         launch_hpcp(mags8, d_kpfx, d_ktile, d_kid, NK, ktile.back(), hp, d_ht, d_chroma, d_energy, st2);
         SDSP_HIP_CHECK(hipGetLastError());
-        std::vector<float> tpl(288);
-        kk_templates(tpl.data());
+        std::vector<float> tpl(576);
+        key_templates(tpl.data());
         float* d_tpl = c_.up("E.tpl", tpl);
         KeyParams kp{};
         kp.weighting = cfg_.enable_key_frame_weighting;
@@ -895,6 +904,26 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         kp.seg_len = std::max(seg_len_cfg, 1);
         kp.seg_hop = seg_hop;
         kp.min_clarity = sd_clampf(cfg_.key_segment_min_clarity, 0.0f, 1.0f);
+        kp.sharpen = cfg_.chroma_sharpening_power;
+        kp.edge_trim = cfg_.enable_key_edge_trim;
+        kp.edge_frac = cfg_.key_edge_trim_fraction;
+        kp.ensemble = cfg_.enable_key_ensemble;
+        kp.kk_w = cfg_.key_ensemble_kk_weight;
+        kp.tp_w = cfg_.key_ensemble_temperley_weight;
+        kp.tset = cfg_.key_template_set == SDSP_TEMPLATES_TEMPERLEY ? 1 : 0;
+        kp.mh_on = cfg_.enable_key_mode_heuristic || cfg_.enable_key_minor_harmonic_bonus;
+        kp.mh_bonus = cfg_.enable_key_minor_harmonic_bonus;
+        kp.mh_margin = cfg_.key_mode_third_ratio_margin;
+        kp.mh_flip = cfg_.enable_key_mode_heuristic ? cfg_.key_mode_flip_min_score_ratio : 0.0f;
+        kp.mh_bonus_w = cfg_.key_minor_leading_tone_bonus_weight;
+        kp.ms_on = ms_on;
+        kp.ms_n = ms_on ? (int)cfg_.key_multi_scale_lengths_len : 0;
+        kp.ms_hop = (int)ms_hop;
+        kp.ms_nw = (int)std::min<uint64_t>(cfg_.key_multi_scale_weights_len, 8);
+        kp.ms_min_cl = sd_clampf(cfg_.key_multi_scale_min_clarity, 0.0f, 1.0f);
+        for (int j = 0; j < kp.ms_n; j++)
+            kp.ms_len[j] = (int)std::min<uint64_t>(cfg_.key_multi_scale_lengths[j], INT32_MAX);
+        for (int j = 0; j < kp.ms_nw; j++) kp.ms_w[j] = cfg_.key_multi_scale_weights[j];
         float* d_cs = c_.dev<float>("E.chroma_s", total8 * 12);
         float* d_w = c_.dev<float>("E.weights", total8);
         float* d_sscr = c_.dev<float>("E.segscr", std::max<uint64_t>(kseg.back(), 1));
