@@ -163,8 +163,12 @@ void analyze(const float* samples, size_t n, uint32_t sr, const sdsp_config& c, 
     if (sr == 0) fail(SDSP_ERR_INVALID_INPUT, "Invalid sample rate");
     std::vector<float> x(samples, samples + n);
     if (c.enable_normalization) {  // lib.rs:116-127
-        if (c.normalization != SDSP_NORM_PEAK) not_impl("RMS/LUFS normalization");
-        normalize_peak(x, 1.0f);
+        if (c.normalization == SDSP_NORM_RMS)
+            normalize_rms(x, -14.0f, 1.0f);
+        else if (c.normalization == SDSP_NORM_LOUDNESS)
+            normalize_lufs(x, sr, -14.0f, 1.0f);
+        else
+            normalize_peak(x, 1.0f);
     }
     size_t ts = 0, te = x.size();
     if (c.enable_silence_trimming) detect_and_trim(x, sr, c.min_amplitude_db, 500, c.frame_size, &ts, &te);
@@ -788,6 +792,25 @@ void sdsp_oracle_key_templates(float* out) {
     key_templates(maj, mnr);
     std::memcpy(out, maj, sizeof maj);
     std::memcpy(out + 144, mnr, sizeof mnr);
+}
+
+// preprocessing::normalization::normalize with lib.rs's fixed config (target -14 LUFS, 1 dB
+// headroom), in place; method 0 peak, 1 RMS, 2 LUFS.  Returns 0 or the error code (msg in err).
+int32_t sdsp_oracle_normalize(int32_t method, float* x, uint64_t n, uint32_t sr, char* err, uint64_t errlen) {
+    try {
+        std::vector<float> v(x, x + n);
+        if (method == 1)
+            normalize_rms(v, -14.0f, 1.0f);
+        else if (method == 2)
+            normalize_lufs(v, sr, -14.0f, 1.0f);
+        else
+            normalize_peak(v, 1.0f);
+        std::copy(v.begin(), v.end(), x);
+        return 0;
+    } catch (const AErr& e) {
+        if (err && errlen) std::snprintf(err, errlen, "%s", e.msg.c_str());
+        return e.code;
+    }
 }
 
 // libm probes: op 0 ln, 1 exp, 2 cos, 3 log10, 4 log2, 5 pow(x, y)

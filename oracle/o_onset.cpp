@@ -1,5 +1,6 @@
 // o_onset.cpp — preprocessing and onset detectors (TEST INFRASTRUCTURE, see oracle_internal.hpp).
 #include <algorithm>
+#include <cmath>
 
 #include "oracle_internal.hpp"
 
@@ -15,6 +16,79 @@ void normalize_peak(std::vector<float>& x, float headroom_db) {
     float gain = target / peak;
     gain = sd_minf(gain, 1.0f / peak);  // :296
     for (float& v : x) v *= gain;
+}
+
+// normalization.rs:325-402 (normalize_rms; target_rms_db = target_lufs + 3, :534-539)
+void normalize_rms(std::vector<float>& x, float target_lufs, float headroom_db) {
+    if (x.empty()) fail(SDSP_ERR_INVALID_INPUT, "Empty audio samples");
+    float ss = 0.0f;
+    for (float v : x) ss += v * v;
+    const float rms = std::sqrt(ss / (float)x.size());
+    if (rms <= EPS) return;
+    float peak = 0.0f;
+    for (float v : x) peak = sd_maxf(peak, sd_absf(v));
+    const float target_rms_db = target_lufs + 3.0f;
+    const float target = sd_powf(10.0f, (target_rms_db - headroom_db) / 20.0f);
+    float gain = target / rms;
+    if (peak * gain > 1.0f) gain = 1.0f / peak;  // :367-385
+    for (float& v : x) v *= gain;
+}
+
+// normalization.rs:119-158 (KWeightingFilter) and :183-259 (calculate_lufs); returns false for
+// the -inf case (every block below the gate)
+static bool calculate_lufs(const std::vector<float>& x, uint32_t sr, float* lufs) {
+    const float fsr = (float)sr;
+    const size_t block = sd_f2u64(fsr * 400.0f / 1000.0f);
+    if (block == 0) fail(SDSP_ERR_INVALID_INPUT, "Sample rate too low for LUFS calculation");
+    const float w0 = 2.0f * 3.14159274f * 1681.9745f / fsr;
+    const float cw = std::cos(w0), sw = std::sin(w0);
+    const float alpha = sw / 2.0f * std::sqrt(1.0f / 0.707f);
+    const float a0 = 1.0f + alpha;
+    const float b0 = ((1.0f + cw) / 2.0f) / a0, b1 = (-(1.0f + cw)) / a0, b2 = ((1.0f + cw) / 2.0f) / a0;
+    const float a1 = (-2.0f * cw) / a0, a2 = (1.0f - alpha) / a0;
+    float x1 = 0.0f, x2 = 0.0f;
+    std::vector<float> y(x.size());
+    for (size_t i = 0; i < x.size(); i++) {  // Direct Form II transposed
+        const float s = x[i];
+        const float o = b0 * s + x1;
+        x1 = b1 * s + x2 - a1 * o;
+        x2 = b2 * s - a2 * o;
+        y[i] = o;
+    }
+    const float gate = sd_powf(10.0f, (-70.0f + 0.691f) / 10.0f);
+    float gsum = 0.0f;
+    size_t gn = 0;
+    for (size_t st = 0; st < y.size(); st += block) {
+        const size_t en = std::min(st + block, y.size());
+        float sq = 0.0f;
+        for (size_t i = st; i < en; i++) sq += y[i] * y[i];
+        const float ms = sq / (float)(en - st);
+        if (ms > gate) {
+            gsum += ms;
+            gn++;
+        }
+    }
+    if (gn == 0) return false;
+    const float mean = gsum / (float)gn;
+    if (mean <= EPS) fail(SDSP_ERR_NUMERICAL, "Mean square too small for LUFS calculation");
+    *lufs = -0.691f + 10.0f * sd_log10f(mean);
+    return true;
+}
+
+// normalization.rs:405-470 (normalize_lufs)
+void normalize_lufs(std::vector<float>& x, uint32_t sr, float target_lufs, float headroom_db) {
+    if (x.empty()) fail(SDSP_ERR_INVALID_INPUT, "Empty audio samples");
+    float lufs;
+    if (!calculate_lufs(x, sr, &lufs)) {
+        normalize_peak(x, headroom_db);
+        return;
+    }
+    const float gain = sd_powf(10.0f, (target_lufs - lufs) / 20.0f);
+    float peak = 0.0f;
+    for (float v : x) peak = sd_maxf(peak, sd_absf(v));
+    const float tpl = sd_powf(10.0f, (0.0f - headroom_db) / 20.0f);
+    const float g = peak * gain > tpl ? tpl / peak : gain;
+    for (float& v : x) v *= g;
 }
 
 // src/preprocessing/silence.rs:102-279

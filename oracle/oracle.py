@@ -53,6 +53,8 @@ def lib():
         L.sdsp_oracle_libm.argtypes = [C.c_int32, fp, fp, fp, C.c_uint64]
         L.sdsp_oracle_find_best.argtypes = [fp, fp, C.c_int32, fp, fp, fp]
         L.sdsp_oracle_find_best.restype = C.c_int32
+        L.sdsp_oracle_normalize.argtypes = [C.c_int32, fp, C.c_uint64, C.c_uint32, C.c_char_p, C.c_uint64]
+        L.sdsp_oracle_normalize.restype = C.c_int32
         L.sdsp_oracle_hmm_model.argtypes = [C.c_float, fp, fp]
         L.sdsp_oracle_hmm_track.argtypes = [C.c_float, fp, C.c_int32, fp, C.c_int32]
         L.sdsp_oracle_hmm_track.restype = C.c_int32
@@ -143,6 +145,14 @@ def key_templates():
     out = np.empty((24, 12), np.float32)
     lib().sdsp_oracle_key_templates(_fp(out))
     return out
+
+
+def normalize(x, method, sample_rate=44100):
+    """normalization::normalize (lib.rs's fixed config) -> (status, samples or error message)."""
+    v = np.array(x, dtype=np.float32)
+    err = C.create_string_buffer(256)
+    st = lib().sdsp_oracle_normalize(method, _fp(v), v.size, sample_rate, err, 256)
+    return (st, v) if st == 0 else (st, err.value.decode())
 
 
 def libm(op, x, y=None):

@@ -66,6 +66,8 @@ struct TempoCand {  // TempogramCandidateDebug, tempogram.rs:47-54
 
 // ---------- preprocessing + onsets ----------
 void normalize_peak(std::vector<float>& x, float headroom_db);
+void normalize_rms(std::vector<float>& x, float target_lufs, float headroom_db);
+void normalize_lufs(std::vector<float>& x, uint32_t sr, float target_lufs, float headroom_db);
 void detect_and_trim(const std::vector<float>& x, uint32_t sr, float threshold_db, uint32_t min_ms,
                      size_t frame_size, size_t* trim_start, size_t* trim_end);
 std::vector<size_t> energy_flux_onsets(const float* s, size_t n, size_t frame, size_t hop, float thr_db);

@@ -1,6 +1,7 @@
 // k_frontend.hip — preprocessing and onset front-end kernels.
 //
 //   k_peak_abs / k_gain      normalize_peak            src/preprocessing/normalization.rs:262-322
+//   k_loudness_gain          normalize_rms / _lufs     normalization.rs:119-259, 325-470
 //   k_frame_rms              frame RMS                 silence.rs:154-169, energy_flux.rs:122-131
 //   k_trim                   silence regions + trim    silence.rs:171-279
 //   k_energy_onsets          energy-flux onsets        energy_flux.rs:133-243
@@ -375,6 +376,202 @@ void launch_peak_gain(const float* x, const uint64_t* in_off, const uint64_t* n_
     (void)hipMemsetAsync(peak_bits, 0, (size_t)T * sizeof(unsigned int), st);
     if (n_chunks) hipLaunchKernelGGL(k_peak_abs, dim3((unsigned)n_chunks), dim3(256), 0, st, x, in_off, n_raw, chunk_pfx, T, peak_bits);
     hipLaunchKernelGGL(k_gain, dim3((T + 255) / 256), dim3(256), 0, st, peak_bits, T, target, enable, gain);
+}
+// ---- RMS / LUFS gain (normalization.rs:325-470): one lane per track ----
+// Both methods fold the whole track in sample order (the f32 sum of squares, and the K-weighting
+// biquad, a recurrence), so the fold itself is one lane per track.  A workgroup owns LG_TPW
+// tracks: lanes 0..LG_TPW-1 of wave 0 fold them while LG_LOADERS loader waves stage the next
+// LG_C-sample chunk of every track into the other half of a double-buffered LDS tile.  Each load
+// instruction reads 1 KB (aligned track) or 256 B (unaligned) of ONE track: a lane-per-track
+// global stream touches a page per lane per instruction and is TLB-bound, and the fold wave
+// alone cannot keep enough bytes in flight.  The LUFS lane runs the biquad, folds each 400-ms
+// block's mean square at its end and gates it on the fly, so nothing but the gain leaves the
+// lane.  The peak comes from k_peak_abs.
+constexpr int LG_TPW = 16;          // tracks per workgroup
+constexpr int LG_C = 1024;          // samples per track per chunk
+constexpr int LG_ROW = LG_C + 4;    // LDS row stride (floats): rows start 4 banks apart
+constexpr int LG_LOADERS = 8;       // loader waves
+template <bool RMS>
+__global__ __launch_bounds__(64 * (1 + LG_LOADERS)) void k_loudness_gain(
+    const float* __restrict__ x, const uint64_t* __restrict__ in_off, const uint64_t* __restrict__ n_raw, int T,
+    const unsigned int* __restrict__ peak_bits, LoudnessParams P, float* __restrict__ gain, int* __restrict__ status) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    extern __shared__ float lg_tile[];  // [2][LG_TPW][LG_ROW]
+    __shared__ uint64_t nmax_s, nmin_s;
+    const int w = threadIdx.x / 64, lane = threadIdx.x % 64;
+    const int t0 = blockIdx.x * LG_TPW;
+    const int nt = T - t0 < LG_TPW ? T - t0 : LG_TPW;
+    if (threadIdx.x == 0) nmax_s = 0, nmin_s = ~0ull;
+    __syncthreads();
+    if (w == 0 && lane < nt) {
+        atomicMax((unsigned long long*)&nmax_s, (unsigned long long)n_raw[t0 + lane]);
+        atomicMin((unsigned long long*)&nmin_s, (unsigned long long)n_raw[t0 + lane]);
+    }
+    __syncthreads();
+    const uint64_t nch = (nmax_s + LG_C - 1) / LG_C;
+    auto load = [&](uint64_t c, int buf) {  // loader waves: chunk c of every track
+        float* base = lg_tile + (size_t)buf * LG_TPW * LG_ROW;
+        const uint64_t s0 = c * LG_C;
+        for (int tt = w - 1; tt < nt; tt += LG_LOADERS) {
+            const uint64_t a = in_off[t0 + tt], n = n_raw[t0 + tt];
+            float* row = base + tt * LG_ROW;
+            if ((a & 3u) == 0 && s0 + LG_C <= n) {  // whole aligned chunk: 16-B loads
+                const f4* q = reinterpret_cast<const f4*>(x + a + s0);
+                f4 v[LG_C / 256];
+#pragma unroll
+                for (int i = 0; i < LG_C / 256; i++) v[i] = q[i * 64 + lane];
+#pragma unroll
+                for (int i = 0; i < LG_C / 256; i++) reinterpret_cast<f4*>(row)[i * 64 + lane] = v[i];
+            } else {
+                float v[LG_C / 64];
+#pragma unroll
+                for (int i = 0; i < LG_C / 64; i++) {
+                    const uint64_t sm = s0 + (uint64_t)(i * 64 + lane);
+                    v[i] = sm < n ? x[a + sm] : 0.0f;
+                }
+#pragma unroll
+                for (int i = 0; i < LG_C / 64; i++) row[i * 64 + lane] = v[i];
+            }
+        }
+    };
+    if (w > 0 && nch > 0) load(0, 0);
+    __syncthreads();
+
+    // ---- wave 0: the per-track folds ----
+    // Every track starts at sample 0 and chunk c covers samples [c*LG_C, (c+1)*LG_C) of every
+    // track, so the position inside the 400-ms block is the same for all lanes: the block
+    // bookkeeping is wave-uniform (scalar branches, no exec-mask divergence), and a chunk that
+    // every track fills completely runs without per-lane tests.
+    const bool act = w == 0 && lane < nt;
+    const uint64_t n = act ? n_raw[t0 + lane] : 0;
+    const float b0 = P.b0, b1 = P.b1, b2 = P.b2, a1 = P.a1, a2 = P.a2;
+    const int64_t bs = P.block;
+    constexpr bool rms = RMS;
+    float ss = 0.0f;                                        // RMS: sum of squares
+    // LUFS: biquad state (x1, x2), block and gated sums.  The state update is written on f32
+    // pairs so that it issues as packed ops (v_pk_add/mul_f32, each lane of a pair rounded
+    // exactly like the scalar op): (o, t) = (x1, x2) + (b0 v, b1 v); (x1, x2) = (t, b2 v) -
+    // (a1 o, a2 o) -- the reference's `b0*s + x1`, `b1*s + x2 - a1*o`, `b2*s - a2*o`.
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    f2 xs = {0.0f, 0.0f};
+    const f2 B01 = {b0, b1}, A12 = {a1, a2};
+    float bsum = 0.0f, gsum = 0.0f;
+    int64_t cnt = 0;  // samples into the current block (uniform)
+    int gn = 0;
+    auto biquad = [&](float v) {  // Direct Form II transposed, KWeightingFilter::process
+        const f2 vv = {v, v};
+        const f2 ot = B01 * vv + xs;
+        const f2 oo = {ot.x, ot.x};
+        const f2 tb = {ot.y, b2 * v};
+        xs = tb - A12 * oo;
+        bsum += ot.x * ot.x;
+    };
+    auto step = [&](float v) {
+        if (rms)
+            ss += v * v;
+        else
+            biquad(v);
+    };
+    auto close_block = [&](int64_t len) {
+        const float ms = bsum / (float)len;
+        if (ms > P.gate) {
+            gsum += ms;
+            gn++;
+        }
+        bsum = 0.0f;
+    };
+    for (uint64_t c = 0; c < nch; c++) {
+        const int buf = (int)(c & 1);
+        if (w > 0) {
+            if (c + 1 < nch) load(c + 1, buf ^ 1);
+        } else {
+            const float* row = lg_tile + (size_t)buf * LG_TPW * LG_ROW + lane * LG_ROW;
+            const f4* row4 = reinterpret_cast<const f4*>(row);
+            const uint64_t s0 = c * LG_C;
+            if (s0 + LG_C <= nmin_s) {  // every track fills this chunk
+                int i = 0;
+                while (i < LG_C) {
+                    // samples up to the next block end (or the chunk end), uniform
+                    const int64_t room = rms ? (int64_t)LG_C : bs - cnt;
+                    const int e = (int64_t)(LG_C - i) < room ? LG_C : i + (int)room;
+                    int k = i;
+                    for (; k < e && (k & 3); k++) step(row[k]);
+                    for (; k + 16 <= e; k += 16) {
+                        const f4 v0 = row4[k / 4], v1 = row4[k / 4 + 1], v2 = row4[k / 4 + 2], v3 = row4[k / 4 + 3];
+                        step(v0.x), step(v0.y), step(v0.z), step(v0.w);
+                        step(v1.x), step(v1.y), step(v1.z), step(v1.w);
+                        step(v2.x), step(v2.y), step(v2.z), step(v2.w);
+                        step(v3.x), step(v3.y), step(v3.z), step(v3.w);
+                    }
+                    for (; k + 4 <= e; k += 4) {
+                        const f4 v = row4[k / 4];
+                        step(v.x), step(v.y), step(v.z), step(v.w);
+                    }
+                    for (; k < e; k++) step(row[k]);
+                    if (!rms) {
+                        cnt += e - i;
+                        if (cnt == bs) {
+                            close_block(bs);
+                            cnt = 0;
+                        }
+                    }
+                    i = e;
+                }
+            } else {  // some track ends inside this chunk: per-lane bounds
+                const int m = !act || s0 >= n ? 0 : (n - s0 < (uint64_t)LG_C ? (int)(n - s0) : LG_C);
+                for (int k = 0; k < LG_C; k++) {
+                    if (k < m) step(row[k]);
+                    if (!rms && ++cnt == bs) {
+                        if (k < m) close_block(bs);
+                        cnt = 0;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (!act) return;
+    const int t = t0 + lane;
+    const float peak = sd_from_bits_f(peak_bits[t]);
+    float g = 1.0f;
+    int stt = 0;
+    if (rms) {  // normalize_rms :325-402
+        const float rms = __builtin_sqrtf(ss / (float)n);
+        if (rms > EPS) {
+            g = P.target_rms / rms;
+            if (peak * g > 1.0f) g = 1.0f / peak;
+        }
+    } else {  // normalize_lufs :405-470 with calculate_lufs :183-259
+        const int64_t rem = (int64_t)(n % (uint64_t)bs);
+        if (rem > 0) close_block(rem);  // this track's last, partial block
+        if (gn == 0) {  // every block under the gate: measured_lufs = -inf -> normalize_peak
+            if (peak > EPS) g = sd_minf(P.target_peak / peak, 1.0f / peak);
+        } else {
+            const float mean = gsum / (float)gn;
+            if (mean <= EPS) {
+                stt = 1;  // NumericalError("Mean square too small for LUFS calculation")
+            } else {
+                const float lufs = -0.691f + 10.0f * sd_log10f(mean);
+                const float gl = sd_powf(10.0f, (P.target_lufs - lufs) / 20.0f);
+                g = peak * gl > P.target_peak ? P.target_peak / peak : gl;
+            }
+        }
+    }
+    gain[t] = g;
+    status[t] = stt;
+}
+
+void launch_loudness_gain(const float* x, const uint64_t* in_off, const uint64_t* n_raw, const uint64_t* chunk_pfx,
+                          int T, uint64_t n_chunks, unsigned int* peak_bits, const LoudnessParams& P, float* gain,
+                          int* status, hipStream_t st) {
+    if (T == 0) return;
+    (void)hipMemsetAsync(peak_bits, 0, (size_t)T * sizeof(unsigned int), st);
+    if (n_chunks) hipLaunchKernelGGL(k_peak_abs, dim3((unsigned)n_chunks), dim3(256), 0, st, x, in_off, n_raw, chunk_pfx, T, peak_bits);
+    const size_t lds = 2 * LG_TPW * LG_ROW * sizeof(float);
+    auto kern = P.method == 1 ? k_loudness_gain<true> : k_loudness_gain<false>;
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3((T + LG_TPW - 1) / LG_TPW), dim3(64 * (1 + LG_LOADERS)), lds, st, x, in_off, n_raw, T,
+                       peak_bits, P, gain, status);
 }
 // ---- frame RMS: sqrt(sum_{k in frame} (x_k*gain)^2 / len), the sum folded in sample order ----
 // Each thread streams its own frame from global memory in 16-B aligned blocks (lanes read

@@ -133,6 +133,19 @@ void launch_stft(int nfft, bool frame_max, const float* samples, const uint64_t*
 void launch_peak_gain(const float* x, const uint64_t* in_off, const uint64_t* n_raw, const uint64_t* chunk_pfx, int T,
                       uint64_t n_chunks, unsigned int* peak_bits, float target, int enable, float* gain,
                       hipStream_t st);
+// RMS / LUFS normalization constants, computed on the host (normalization.rs:119-158, 325-470)
+struct LoudnessParams {
+    int method;          // 1 RMS, 2 LUFS
+    float target_rms;    // 10^((target_lufs + 3 - headroom) / 20)
+    float target_peak;   // 10^((0 - headroom) / 20)
+    float target_lufs;   // -14
+    float gate;          // 10^((-70 + 0.691) / 10)
+    int64_t block;       // 400-ms block, samples
+    float b0, b1, b2, a1, a2;  // K-weighting biquad, normalised by a0
+};
+void launch_loudness_gain(const float* x, const uint64_t* in_off, const uint64_t* n_raw, const uint64_t* chunk_pfx,
+                          int T, uint64_t n_chunks, unsigned int* peak_bits, const LoudnessParams& P, float* gain,
+                          int* status, hipStream_t st);
 void launch_frame_rms(const float* x, const uint64_t* src_off, const float* gain, const uint64_t* n_len,
                       const uint64_t* frame_pfx, int T, uint64_t total, int fs, int hop, float* rms, hipStream_t st);
 void launch_trim(const float* rms, const uint64_t* frame_pfx, int T, const uint64_t* n_raw, int hop, float thr,

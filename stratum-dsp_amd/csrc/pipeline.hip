@@ -217,6 +217,32 @@ void key_templates(float* out /*48x12*/) {
     }
 }
 
+// RMS / LUFS constants (normalization.rs:119-158, 183-259, 325-470; lib.rs:118-122 fixes
+// target_loudness_lufs = -14 and max_headroom_db = 1).  The K-weighting coefficients use the C
+// library's sinf/cosf, the functions f32::sin/cos lower to.
+LoudnessParams loudness_params(int method, uint32_t sr) {
+    LoudnessParams p{};
+    p.method = method == SDSP_NORM_RMS ? 1 : 2;
+    const float target_lufs = -14.0f, headroom = 1.0f;
+    p.target_lufs = target_lufs;
+    p.target_rms = sd_powf(10.0f, ((target_lufs + 3.0f) - headroom) / 20.0f);
+    p.target_peak = sd_powf(10.0f, (0.0f - headroom) / 20.0f);
+    p.gate = sd_powf(10.0f, (-70.0f + 0.691f) / 10.0f);
+    const float fsr = (float)sr;
+    p.block = (int64_t)sd_f2u64(fsr * 400.0f / 1000.0f);
+    const float w0 = 2.0f * 3.14159274f * 1681.9745f / fsr;
+    const float cw = cosf(w0), sw = sinf(w0);
+    const float alpha = sw / 2.0f * sqrtf(1.0f / 0.707f);
+    const float b0 = (1.0f + cw) / 2.0f, b1 = -(1.0f + cw), b2 = (1.0f + cw) / 2.0f;
+    const float a0 = 1.0f + alpha, a1 = -2.0f * cw, a2 = 1.0f - alpha;
+    p.b0 = b0 / a0;
+    p.b1 = b1 / a0;
+    p.b2 = b2 / a0;
+    p.a1 = a1 / a0;
+    p.a2 = a2 / a0;
+    return p;
+}
+
 // autocorrelation_tempogram's BPM grid and lags for one hop (tempogram_autocorr.rs:128-140)
 void acf_grid(uint32_t sr, int hop, float min_bpm, float max_bpm, float res, std::vector<float>* bpms,
               std::vector<int>* lags) {
@@ -324,7 +350,9 @@ struct TrackRes {
 
 // Configuration support (everything the default path and its numeric knobs need).
 std::string unsupported(const sdsp_config& c) {
-    if (c.enable_normalization && c.normalization != SDSP_NORM_PEAK) return "RMS/LUFS normalization";
+    if (c.enable_normalization && c.normalization != SDSP_NORM_PEAK && c.normalization != SDSP_NORM_RMS &&
+        c.normalization != SDSP_NORM_LOUDNESS)
+        return "unknown normalization method";
     if (c.frame_size != 2048) return "frame_size other than 2048";
     if (c.hop_size == 0 || c.hop_size > 8192) return "hop_size outside 1..8192";
     if (c.enable_hpss_onsets) return "HPSS onsets";
@@ -399,6 +427,13 @@ class Pipeline {
     const sdsp_config& cfg_;
     uint32_t sr_;
     sdsp_stage_times times_{};
+    // RMS / LUFS: gains (and LUFS status) of every track, folded once for the whole batch
+    // before the sub-batches (the fold is a per-track sequential latency, not a throughput)
+    std::vector<float> loud_gain_;
+    std::vector<int> loud_stat_;
+
+    void loudness_prepass(const float* d_samples, const std::vector<uint64_t>& in_off,
+                          const std::vector<uint64_t>& n_raw, std::vector<TrackRes>& res);
 
     void sub_batch(const float* d_samples, const std::vector<uint64_t>& in_off, const std::vector<uint64_t>& n_raw,
                    const std::vector<int>& idx, std::vector<TrackRes>& res);
@@ -445,6 +480,8 @@ void Pipeline::run(const float* d_samples, const std::vector<uint64_t>& in_off, 
     };
     times_ = sdsp_stage_times{};
     auto t0 = std::chrono::steady_clock::now();
+    if (cfg_.enable_normalization && cfg_.normalization != SDSP_NORM_PEAK && why.empty())
+        loudness_prepass(d_samples, in_off, n_raw, res);
     // equal shares: the fewest sub-batches that fit the budget, each near total / count (a
     // short last sub-batch runs at a fraction of the chip)
     std::vector<double> need(T, 0.0);
@@ -473,6 +510,44 @@ void Pipeline::run(const float* d_samples, const std::vector<uint64_t>& in_off, 
     flush();
     times_.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     d_.last = times_;
+}
+
+void Pipeline::loudness_prepass(const float* d_samples, const std::vector<uint64_t>& in_off,
+                                const std::vector<uint64_t>& n_raw, std::vector<TrackRes>& res) {
+    const size_t T = n_raw.size();
+    loud_gain_.assign(T, 1.0f);
+    loud_stat_.assign(T, 0);
+    const LoudnessParams lp = loudness_params(cfg_.normalization, sr_);
+    std::vector<uint64_t> off, nr, cpfx(1, 0);
+    std::vector<size_t> at;
+    for (size_t i = 0; i < T; i++) {
+        if (res[i].status != SDSP_OK) continue;
+        if (lp.method == 2 && lp.block == 0) {  // calculate_lufs :199-204
+            res[i].status = SDSP_ERR_INVALID_INPUT;
+            res[i].err = "Invalid input: Sample rate too low for LUFS calculation";
+            continue;
+        }
+        at.push_back(i);
+        off.push_back(in_off[i]);
+        nr.push_back(n_raw[i]);
+        cpfx.push_back(cpfx.back() + (n_raw[i] + PK_CH - 1) / PK_CH);
+    }
+    const int L = (int)at.size();
+    if (L == 0) return;
+    uint64_t* d_off = c_.up("L.off", off);
+    uint64_t* d_nr = c_.up("L.nr", nr);
+    uint64_t* d_cpfx = c_.up("L.cpfx", cpfx);
+    unsigned int* d_peak = c_.dev<unsigned int>("L.peak", (size_t)L);
+    float* d_gain = c_.dev<float>("L.gain", (size_t)L);
+    int* d_stat = c_.dev<int>("L.stat", (size_t)L);
+    launch_loudness_gain(d_samples, d_off, d_nr, d_cpfx, L, cpfx.back(), d_peak, lp, d_gain, d_stat, d_.stream);
+    SDSP_HIP_CHECK(hipGetLastError());
+    const std::vector<float> g = c_.down(d_gain, (size_t)L);
+    const std::vector<int> st = c_.down(d_stat, (size_t)L);
+    for (int k = 0; k < L; k++) {
+        loud_gain_[at[(size_t)k]] = g[(size_t)k];
+        loud_stat_[at[(size_t)k]] = st[(size_t)k];
+    }
 }
 
 void Pipeline::tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPassOut& o) {
@@ -746,8 +821,19 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     unsigned int* d_peak = c_.dev<unsigned int>("A.peak", (size_t)T);
     float* d_gain = c_.dev<float>("A.gain", (size_t)T);
     const float target = sd_powf(10.0f, (0.0f - 1.0f) / 20.0f);  // lib.rs:121 max_headroom_db = 1.0
-    launch_peak_gain(d_samples, d_off, d_nr, d_cpfx, T, cpfx[(size_t)T], d_peak, target, cfg_.enable_normalization, d_gain,
-                     st);
+    const bool loud = cfg_.enable_normalization && cfg_.normalization != SDSP_NORM_PEAK;
+    std::vector<int> nstat((size_t)T, 0);
+    if (loud) {  // gains from the batch-wide pre-pass (loudness_prepass)
+        std::vector<float> g((size_t)T);
+        for (int t = 0; t < T; t++) {
+            g[(size_t)t] = loud_gain_[(size_t)idx[(size_t)t]];
+            nstat[(size_t)t] = loud_stat_[(size_t)idx[(size_t)t]];
+        }
+        d_gain = c_.up("A.gain", g);
+    } else {
+        launch_peak_gain(d_samples, d_off, d_nr, d_cpfx, T, cpfx[(size_t)T], d_peak, target, cfg_.enable_normalization,
+                         d_gain, st);
+    }
     float* d_srms = c_.dev<float>("A.srms", spfx[(size_t)T]);
     launch_frame_rms(d_samples, d_off, d_gain, d_nr, d_spfx, T, spfx[(size_t)T], FS, FS / 2, d_srms, st);
     const float thr = sd_powf(10.0f, cfg_.min_amplitude_db / 20.0f);
@@ -766,6 +852,11 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     for (int t = 0; t < T; t++) {
         TrackRes& r = res[(size_t)idx[(size_t)t]];
         const uint64_t n = te[(size_t)t] - ts[(size_t)t];
+        if (nstat[(size_t)t] != 0) {
+            r.status = SDSP_ERR_NUMERICAL;
+            r.err = "Numerical error: Mean square too small for LUFS calculation";
+            continue;
+        }
         if (n == 0) {
             r.status = SDSP_ERR_PROCESSING;
             r.err = "Processing error: Audio is entirely silent after trimming";
