@@ -284,6 +284,94 @@ SD_HD float sd_cosf(float x) {
     return (float)sd_cos_d((double)x);
 }
 
+/* f32::sin: sd_cos_d's reduction and polynomials, quadrant shifted by one */
+SD_HD double sd_sin_d(double x) {
+    const double PIO2_HI = 1.57079632673412561417e+00;
+    const double PIO2_LO = 6.07710050650619224932e-11;
+    const double TWO_OVER_PI = 6.36619772367581382433e-01;
+    double t = x * TWO_OVER_PI;
+    double kd = (double)(int64_t)(t >= 0.0 ? t + 0.5 : t - 0.5);
+    double r = (x - kd * PIO2_HI) - kd * PIO2_LO;
+    double z = r * r;
+    double c = 1.0 / 6402373705728000.0;
+    c = 1.0 / 20922789888000.0 - z * c;
+    c = 1.0 / 87178291200.0 - z * c;
+    c = 1.0 / 479001600.0 - z * c;
+    c = 1.0 / 3628800.0 - z * c;
+    c = 1.0 / 40320.0 - z * c;
+    c = 1.0 / 720.0 - z * c;
+    c = 1.0 / 24.0 - z * c;
+    c = 0.5 - z * c;
+    double cosr = 1.0 - z * c;
+    double s = 1.0 / 121645100408832000.0;
+    s = 1.0 / 355687428096000.0 - z * s;
+    s = 1.0 / 1307674368000.0 - z * s;
+    s = 1.0 / 6227020800.0 - z * s;
+    s = 1.0 / 39916800.0 - z * s;
+    s = 1.0 / 362880.0 - z * s;
+    s = 1.0 / 5040.0 - z * s;
+    s = 1.0 / 120.0 - z * s;
+    s = 1.0 / 6.0 - z * s;
+    double sinr = r - r * (z * s);
+    int q = (int)((int64_t)kd & 3);
+    if (q == 0) return sinr;
+    if (q == 1) return cosr;
+    if (q == 2) return -sinr;
+    return -cosr;
+}
+SD_HD float sd_sinf(float x) {
+    if (x != x) return x;
+    return (float)sd_sin_d((double)x);
+}
+
+/* atan on [0, inf): atan(x) = atan(c) + atan(t), c = k/8 nearest x (x <= 1; 1/x above),
+ * t = (x - c) / (1 + x c), |t| <= 1/16, odd Taylor series to t^19 (truncation < 2^-80). */
+SD_HD double sd_atan_pos_d(double ax) {
+    const int inv = ax > 1.0;
+    double x = inv ? 1.0 / ax : ax;
+    int k = (int)(x * 8.0 + 0.5);
+    double c = (double)k * 0.125;
+    double t = (x - c) / (1.0 + x * c);
+    double z = t * t;
+    double p = 1.0 / 19.0;
+    p = 1.0 / 17.0 - z * p;
+    p = 1.0 / 15.0 - z * p;
+    p = 1.0 / 13.0 - z * p;
+    p = 1.0 / 11.0 - z * p;
+    p = 1.0 / 9.0 - z * p;
+    p = 1.0 / 7.0 - z * p;
+    p = 1.0 / 5.0 - z * p;
+    p = 1.0 / 3.0 - z * p;
+    /* atan(k/8), correctly rounded doubles (selects, not a table: no scratch on the GPU) */
+    const double ak = k == 0   ? 0.0
+                      : k == 1 ? 0.12435499454676144
+                      : k == 2 ? 0.24497866312686414
+                      : k == 3 ? 0.35877067027057225
+                      : k == 4 ? 0.4636476090008061
+                      : k == 5 ? 0.5585993153435624
+                      : k == 6 ? 0.6435011087932844
+                      : k == 7 ? 0.7188299996216245
+                               : 0.7853981633974483;
+    double a = ak + (t - t * (z * p));
+    return inv ? 1.5707963267948966 - a : a;
+}
+/* f32::atan2 (IEEE signed-zero / axis conventions) */
+SD_HD float sd_atan2f(float y, float x) {
+    if (x != x || y != y) return SD_NAN_F;
+    const double PI = 3.141592653589793;
+    const int ys = (sd_bits_f(y) >> 31) != 0, xs = (sd_bits_f(x) >> 31) != 0;
+    if (y == 0.0f) {
+        if (!xs) return y;                     /* atan2(+-0, +x or +0) = +-0 */
+        return ys ? (float)-PI : (float)PI;    /* atan2(+-0, -x or -0) = +-pi */
+    }
+    if (x == 0.0f) return ys ? (float)(-PI / 2.0) : (float)(PI / 2.0);
+    const double q = (double)y / (double)x;
+    double a = sd_atan_pos_d(q < 0.0 ? -q : q);
+    if (q < 0.0) a = -a;
+    if (!xs) return (float)a;
+    return ys ? (float)(a - PI) : (float)(a + PI);
+}
+
 /* f32::powf (IEEE special cases for the operand ranges the pipeline produces) */
 SD_HD float sd_powf(float x, float y) {
     if (y == 2.0f) return x * x; /* == glibc powf(x, 2) on 3.0e8 sampled inputs */

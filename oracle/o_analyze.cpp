@@ -1,9 +1,9 @@
 // o_analyze.cpp — analyze_audio orchestration + the oracle's C API (TEST INFRASTRUCTURE).
 //
-// Follows src/lib.rs:86-1635 with AnalysisConfig::default() (src/config.rs:594-744).  Branches
-// that the default config never takes and that are outside the hot-path scope (HPSS onsets /
-// percussive fallback / key HPSS, log-frequency, tuning, beat-synchronous chroma, multi-scale,
-// ensemble, mode heuristic, edge trim, RMS/LUFS normalisation) raise NotImplemented here.
+// Follows src/lib.rs:86-1635 with AnalysisConfig::default() (src/config.rs:594-744) and the opt-in
+// branches restated so far (normalisation methods, key scoring options, chroma front-ends).
+// Branches not restated yet (HPSS onsets / percussive fallback / key HPSS, the legacy-BPM output
+// paths) raise NotImplemented here, as they do in the engine.
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -429,24 +429,55 @@ void analyze(const float* samples, size_t n, uint32_t sr, const sdsp_config& c, 
         const size_t khop = c.enable_key_stft_override ? std::max<size_t>(c.key_stft_hop_size, 1) : HOP;
         if (kfft & (kfft - 1)) not_impl("non power-of-two key_stft_frame_size");
         Spec ks = c.enable_key_stft_override ? compute_stft(trim.data(), trim.size(), kfft, khop) : mags;
-        if (!ks.empty()) {
+        if (!ks.empty()) {  // :1011-1060
             if (c.enable_key_hpss_harmonic) not_impl("key HPSS harmonic mask");
-            if (c.enable_key_harmonic_mask) {
+            if (c.enable_key_harmonic_mask)
                 harmonic_mask_inplace(ks, (size_t)c.key_spectrogram_smooth_margin, c.key_harmonic_mask_power);
-            } else if (c.enable_key_spectrogram_time_smoothing) {
-                not_impl("key spectrogram time smoothing without mask");
-            }
+            else if (c.enable_key_spectrogram_time_smoothing)
+                smooth_time_inplace(ks, (size_t)c.key_spectrogram_smooth_margin);
         }
-        if (c.enable_key_log_frequency) not_impl("key log-frequency spectrogram");
-        if (c.enable_key_tuning_compensation) not_impl("key tuning compensation");
-        if (c.enable_key_beat_synchronous) not_impl("beat-synchronous chroma");
-        if (!c.enable_key_hpcp || c.enable_key_hpcp_bass_blend || c.enable_key_hpcp_whitening)
-            not_impl("non-HPCP / bass-blend / whitened chroma");
+        // log-frequency spectrogram (:1062-1095)
         std::vector<float> chroma, energies;
-        hpcp_frames(ks, sr, kfft, c.soft_mapping_sigma, (size_t)c.key_hpcp_peaks_per_frame,
-                    (size_t)c.key_hpcp_num_harmonics, c.key_hpcp_harmonic_decay, c.key_hpcp_mag_power, &chroma,
-                    &energies);
-        const size_t F_all = ks.frames;
+        bool use_log = false;
+        if (c.enable_key_log_frequency && !ks.empty()) {
+            use_log = log_freq_chroma(ks, sr, kfft, &chroma, &energies);
+            if (!use_log) not_impl("degenerate key log-frequency range");
+        }
+        // tuning offset (:1097-1119)
+        float tuning = 0.0f;
+        if (c.enable_key_tuning_compensation && !ks.empty() && !use_log) {
+            const float lim = sd_absf(c.key_tuning_max_abs_semitones);
+            tuning = sd_clampf(estimate_tuning(ks, sr, kfft, 80.0f, 2000.0f, (size_t)c.key_tuning_frame_step,
+                                               c.key_tuning_peak_rel_threshold),
+                               -lim, lim);
+        }
+        tr.tuning = tuning;
+        // chroma front-end dispatch (:1121-1198)
+        if (c.enable_key_beat_synchronous && !o.beats.empty() && !use_log) {
+            beat_sync_chroma(ks, sr, kfft, khop, o.beats, c.soft_chroma_mapping != 0, c.soft_mapping_sigma, tuning,
+                             &chroma, &energies);
+        } else if (use_log) {
+            // chroma / energies computed above
+        } else if (c.enable_key_hpcp) {
+            HpcpCfg hc;
+            hc.sigma = c.soft_mapping_sigma;
+            hc.tuning = tuning;
+            hc.peaks = (size_t)c.key_hpcp_peaks_per_frame;
+            hc.harmonics = (size_t)c.key_hpcp_num_harmonics;
+            hc.decay = c.key_hpcp_harmonic_decay;
+            hc.mag_power = c.key_hpcp_mag_power;
+            hc.whitening = c.enable_key_hpcp_whitening != 0;
+            hc.whitening_bins = (size_t)c.key_hpcp_whitening_smooth_bins;
+            hc.bass_blend = c.enable_key_hpcp_bass_blend != 0;
+            hc.bass_fmin = c.key_hpcp_bass_fmin_hz;
+            hc.bass_fmax = c.key_hpcp_bass_fmax_hz;
+            hc.bass_weight = c.key_hpcp_bass_weight;
+            hpcp_frames_x(ks, sr, kfft, hc, &chroma, &energies);
+        } else {
+            const float t = (c.enable_key_tuning_compensation && sd_absf(tuning) > 1e-6f) ? tuning : 0.0f;
+            chroma_frames(ks, sr, kfft, c.soft_chroma_mapping != 0, c.soft_mapping_sigma, t, &chroma, &energies);
+        }
+        const size_t F_all = energies.size();
         if (c.chroma_sharpening_power > 1.0f)  // :1200-1208
             for (size_t f = 0; f < F_all; f++) sharpen_chroma_inplace(chroma.data() + f * 12, c.chroma_sharpening_power);
         if (F_all > 5) smooth_chroma_inplace(chroma, F_all, 5);  // :1211-1213
@@ -813,7 +844,7 @@ int32_t sdsp_oracle_normalize(int32_t method, float* x, uint64_t n, uint32_t sr,
     }
 }
 
-// libm probes: op 0 ln, 1 exp, 2 cos, 3 log10, 4 log2, 5 pow(x, y)
+// libm probes: op 0 ln, 1 exp, 2 cos, 3 log10, 4 log2, 5 pow(x, y), 6 sin, 7 atan2(x, y)
 void sdsp_oracle_libm(int32_t op, const float* x, const float* y, float* out, uint64_t n) {
     for (uint64_t i = 0; i < n; i++) {
         switch (op) {
@@ -822,6 +853,8 @@ void sdsp_oracle_libm(int32_t op, const float* x, const float* y, float* out, ui
             case 2: out[i] = sd_cosf(x[i]); break;
             case 3: out[i] = sd_log10f(x[i]); break;
             case 4: out[i] = sd_log2f(x[i]); break;
+            case 6: out[i] = sd_sinf(x[i]); break;
+            case 7: out[i] = sd_atan2f(x[i], y[i]); break;
             default: out[i] = sd_powf(x[i], y[i]); break;
         }
     }

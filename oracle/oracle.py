@@ -58,6 +58,11 @@ def lib():
         L.sdsp_oracle_hmm_model.argtypes = [C.c_float, fp, fp]
         L.sdsp_oracle_hmm_track.argtypes = [C.c_float, fp, C.c_int32, fp, C.c_int32]
         L.sdsp_oracle_hmm_track.restype = C.c_int32
+        L.sdsp_oracle_chroma.argtypes = [C.c_int32, fp, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint64,
+                                         C.c_int32, C.c_float, C.c_float, fp, C.c_uint64, fp, fp, C.c_uint64]
+        L.sdsp_oracle_chroma.restype = C.c_int64
+        L.sdsp_oracle_tuning.argtypes = [fp, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint64, C.c_float]
+        L.sdsp_oracle_tuning.restype = C.c_float
         _lib = L
     return _lib
 
@@ -156,12 +161,34 @@ def normalize(x, method, sample_rate=44100):
 
 
 def libm(op, x, y=None):
-    ops = {"ln": 0, "exp": 1, "cos": 2, "log10": 3, "log2": 4, "pow": 5}
+    ops = {"ln": 0, "exp": 1, "cos": 2, "log10": 3, "log2": 4, "pow": 5, "sin": 6, "atan2": 7}
     x = np.ascontiguousarray(x, dtype=np.float32)
     y = np.ascontiguousarray(y if y is not None else np.zeros_like(x), dtype=np.float32)
     out = np.empty_like(x)
     lib().sdsp_oracle_libm(ops[op], _fp(x), _fp(y), _fp(out), x.size)
     return out
+
+
+def chroma(mode, spec, sample_rate=44100, fft_size=8192, hop=512, soft=True, sigma=0.5, tuning=0.0, beats=()):
+    """Key chroma front-ends on a (frames, bins) magnitude spectrogram -> (chroma (rows, 12), energies).
+    mode: "plain" frame_to_chroma_tuned, "hpcp", "logfreq", "beatsync"."""
+    m = {"plain": 0, "hpcp": 1, "logfreq": 2, "beatsync": 3}[mode]
+    s = np.ascontiguousarray(spec, dtype=np.float32)
+    b = np.ascontiguousarray(beats, dtype=np.float32)
+    cap = max(s.shape[0], b.size) + 1
+    ch = np.zeros((cap, 12), np.float32)
+    en = np.zeros(cap, np.float32)
+    n = lib().sdsp_oracle_chroma(m, _fp(s), s.shape[0], s.shape[1], sample_rate, fft_size, hop, int(soft),
+                                 C.c_float(sigma), C.c_float(tuning), _fp(b), b.size, _fp(ch), _fp(en), cap)
+    assert n >= 0
+    return ch[:n].copy(), en[:n].copy()
+
+
+def tuning(spec, sample_rate=44100, fft_size=8192, frame_step=20, rel_threshold=0.35):
+    """estimate_tuning_offset_semitones_from_spectrogram over [80, 2000] Hz (src/lib.rs:1101-1109)."""
+    s = np.ascontiguousarray(spec, dtype=np.float32)
+    return lib().sdsp_oracle_tuning(_fp(s), s.shape[0], s.shape[1], sample_rate, fft_size, frame_step,
+                                    C.c_float(rel_threshold))
 
 
 def find_best(tempogram):

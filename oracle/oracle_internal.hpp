@@ -118,6 +118,28 @@ void harmonic_mask_inplace(Spec& s, size_t margin, float power);
 void hpcp_frames(const Spec& s, uint32_t sr, size_t fft_size, float sigma, size_t peaks, size_t harmonics,
                  float decay, float mag_power, std::vector<float>* chroma12, std::vector<float>* energies);
 void smooth_chroma_inplace(std::vector<float>& ch, size_t frames, size_t window);
+// opt-in chroma front-ends (o_chroma.cpp)
+struct HpcpCfg {
+    float sigma = 0.5f, tuning = 0.0f;
+    size_t peaks = 24, harmonics = 4;
+    float decay = 0.6f, mag_power = 0.5f;
+    bool whitening = false;
+    size_t whitening_bins = 31;
+    bool bass_blend = false;
+    float bass_fmin = 55.0f, bass_fmax = 300.0f, bass_weight = 0.35f;
+};
+float estimate_tuning(const Spec& s, uint32_t sr, size_t fft_size, float fmin_hz, float fmax_hz, size_t frame_step,
+                      float peak_rel_threshold);
+void chroma_frames(const Spec& s, uint32_t sr, size_t fft_size, bool soft, float sigma, float tuning,
+                   std::vector<float>* chroma12, std::vector<float>* energies);
+void hpcp_frames_x(const Spec& s, uint32_t sr, size_t fft_size, const HpcpCfg& c, std::vector<float>* chroma12,
+                   std::vector<float>* energies);
+bool log_freq_chroma(const Spec& s, uint32_t sr, size_t fft_size, std::vector<float>* chroma12,
+                     std::vector<float>* energies);
+void beat_sync_chroma(const Spec& s, uint32_t sr, size_t fft_size, size_t hop, const std::vector<float>& beats,
+                      bool soft, float sigma, float tuning, std::vector<float>* chroma12, std::vector<float>* energies);
+void smooth_time_inplace(Spec& s, size_t margin);
+
 struct KeyResult {
     int mode;
     uint32_t tonic;
@@ -161,6 +183,7 @@ struct Trace {
     std::vector<float> energies;  // per key frame
     std::vector<float> weights;
     bool weights_used = false;
+    float tuning = 0.0f;
     int used_segments = 0;
 };
 

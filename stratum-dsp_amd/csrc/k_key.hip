@@ -33,7 +33,7 @@ __device__ __forceinline__ float mask_pow(float x, float p) {
 template <int PW>
 __global__ __launch_bounds__(MASK_T) void k_mask(float* __restrict__ mags, int stride, int B,
                                                   const uint64_t* __restrict__ frame_pfx, const int* __restrict__ tracks,
-                                                  int blocks_per_track, int margin, float power) {
+                                                  int blocks_per_track, int margin, float power, int smooth_only) {
     extern __shared__ float mask_lds[];
     const int it = blockIdx.x / blocks_per_track;
     const int trk = tracks[it];
@@ -79,6 +79,12 @@ __global__ __launch_bounds__(MASK_T) void k_mask(float* __restrict__ mags, int s
             const float x_raw = M == 0 ? xv[u] : raw[xr * MASK_T];
             // margin 0: smooth_spectrogram_time returns its input unchanged (extractor.rs:1250-1252)
             const float hm = M == 0 ? x_raw : (pre[w_slot * MASK_T] - pre[s_slot * MASK_T]) / denom;
+            if (smooth_only) {  // smooth_spectrogram_time alone (src/lib.rs:1042-1055)
+                col[t * stride] = hm;
+                if (M > 0) xr = xr + 1 == RX ? 0 : xr + 1;
+                if (t >= M) s_slot = s_slot + 1 == R ? 0 : s_slot + 1;
+                continue;
+            }
             const float x = max_bnn(x_raw, 0.0f);
             const float h = max_bnn(hm, 0.0f);
             const float r = max_bnn(x - h, 0.0f);
@@ -800,11 +806,17 @@ __global__ __launch_bounds__(256) void k_key_vote(const int* __restrict__ tracks
 
 // ---- launchers ----
 void launch_mask(float* mags, int stride, int B, const uint64_t* frame_pfx, const int* tracks, int n_items, int margin,
-                 float power, hipStream_t st) {
+                 float power, hipStream_t st, bool smooth_only) {
     if (n_items == 0) return;
     const int bpt = (B + MASK_T - 1) / MASK_T;
     const size_t lds = (size_t)(2 * margin + 2 + margin + 1) * MASK_T * sizeof(float);
     const float p = sd_maxf(power, 1.0f);
+    if (smooth_only) {
+        if (margin == 0) return;  // smooth_spectrogram_time returns its input (extractor.rs:1250-1252)
+        hipLaunchKernelGGL(k_mask<1>, dim3(n_items * bpt), dim3(MASK_T), lds, st, mags, stride, B, frame_pfx, tracks,
+                           bpt, margin, power, 1);
+        return;
+    }
     if (margin == 12 && p == 2.0f) {
         hipLaunchKernelGGL((k_mask_r<12, 2>), dim3(n_items * bpt), dim3(MASK_T), 0, st, mags, stride, B, frame_pfx,
                            tracks, bpt, power);
@@ -812,13 +824,13 @@ void launch_mask(float* mags, int stride, int B, const uint64_t* frame_pfx, cons
     }
     if (p == 2.0f)
         hipLaunchKernelGGL(k_mask<2>, dim3(n_items * bpt), dim3(MASK_T), lds, st, mags, stride, B, frame_pfx, tracks,
-                           bpt, margin, power);
+                           bpt, margin, power, 0);
     else if (p == 1.0f)
         hipLaunchKernelGGL(k_mask<1>, dim3(n_items * bpt), dim3(MASK_T), lds, st, mags, stride, B, frame_pfx, tracks,
-                           bpt, margin, power);
+                           bpt, margin, power, 0);
     else
         hipLaunchKernelGGL(k_mask<0>, dim3(n_items * bpt), dim3(MASK_T), lds, st, mags, stride, B, frame_pfx, tracks,
-                           bpt, margin, power);
+                           bpt, margin, power, 0);
 }
 void launch_hpcp(const float* mags, const uint64_t* frame_pfx, const uint64_t* tile_pfx, const int* tracks,
                  int n_items, uint64_t n_tiles, const HpcpParams& P, const HarmEntry* harm, float* chroma,

@@ -125,6 +125,30 @@ struct KeyOut {
     int weights_used;
 };
 
+// ---- k_chroma (opt-in chroma front-ends) ----
+struct TuningParams {
+    int stride, lo, hi, step, chf;  // band bins [lo, hi]; sampled-frame step; frames per LDS batch
+    float fres, thr, lim;           // bin spacing; peak-relative threshold; |offset| clamp
+};
+struct ChromaBin {
+    int a, b;  // k_chroma<0>: primary class; k_chroma<1>: lo, hi semitone bins (a = -1: none)
+    float w0, w1, w2;
+};
+struct ChromaParams {
+    int B, stride, lo, hi;  // bins per row, row stride, mapped bin range [lo, hi]
+    int soft, gate_small;   // soft mapping; tuning used only if |offset| > 1e-6
+    int n_log, log_off, bmin;  // log-frequency: semitone bins, pitch-class offset, first semitone
+    float fres, sigma;
+};
+struct HpcpXParams {
+    int B, stride;
+    int pk_lo, pk_hi, bk_lo, bk_hi;  // main / bass candidate bins
+    int K, KB, hmax;
+    int half, rp, rp_mask, rx, rx_mask;  // whitening half width (0 = off) and LDS ring sizes
+    int bass, main_ok, bass_ok;
+    float p, fres, fmin, fmax, bfmin, bfmax, decay, sigma, bw;
+};
+
 // ---- launchers ----
 void launch_stft(int nfft, bool frame_max, const float* samples, const uint64_t* frame_pfx, int n_tracks,
                  uint64_t total_frames, const uint64_t* src_off, const float* gain, int hop, const float* window,
@@ -185,7 +209,18 @@ void launch_beat(const int* tracks, int n_items, const uint32_t* onsets, const u
 void launch_beat_compact(int n, const BeatOut* out, const uint64_t* beat_off, const float* beats, const float* downs,
                          uint64_t* pfx, float* cb, float* cd, hipStream_t st);
 void launch_mask(float* mags, int stride, int B, const uint64_t* frame_pfx, const int* tracks, int n_items, int margin,
-                 float power, hipStream_t st);
+                 float power, hipStream_t st, bool smooth_only = false);
+void launch_tuning(const float* mags, const uint64_t* frame_pfx, const int* tracks, int n_items, const TuningParams& P,
+                   float* out, hipStream_t st);
+void launch_chroma(int mode, const float* mags, const uint64_t* frame_pfx, const uint64_t* tile_pfx, const int* tracks,
+                   int n_items, uint64_t n_tiles, const ChromaParams& P, const float* tuning, float* chroma,
+                   float* energy, hipStream_t st);
+void launch_hpcp_x(const float* mags, const uint64_t* frame_pfx, const uint64_t* tile_pfx, const int* tracks,
+                   int n_items, uint64_t n_tiles, const HpcpXParams& P, const float* tuning, float* chroma,
+                   float* energy, hipStream_t st);
+void launch_beat_sync(const int* tracks, int n_items, const uint64_t* frame_pfx, const float* fchroma,
+                      const float* fenergy, const float* beats, const uint64_t* beat_off, const uint64_t* row_pfx,
+                      float fd, float* chroma, float* energy, hipStream_t st);
 void launch_hpcp(const float* mags, const uint64_t* frame_pfx, const uint64_t* tile_pfx, const int* tracks,
                  int n_items, uint64_t n_tiles, const HpcpParams& P, const HarmEntry* harm, float* chroma,
                  float* energy, hipStream_t st);

@@ -197,6 +197,145 @@ std::vector<HarmEntry> harm_table(int B, uint32_t sr, int fft_size, float sigma_
     return t;
 }
 
+// Contiguous candidate bins of a band, as the reference's peak loops visit them:
+// `for bin in 1..len-1 { if f < fmin continue; if f > fmax break; ... }` (extractor.rs:599-617).
+// Leaves *lo > *hi when the band is empty.
+void band_bins(int B, float fres, float fmin, float fmax, int* lo, int* hi) {
+    *lo = 1;
+    *hi = 0;
+    if (!(fmax > fmin)) return;
+    int l = -1, h = -1;
+    for (int b = 1; b + 1 < B; b++) {
+        const float f = (float)b * fres;
+        if (f < fmin) continue;
+        if (f > fmax) break;
+        if (l < 0) l = b;
+        h = b;
+    }
+    if (l >= 0) *lo = l, *hi = h;
+}
+
+// estimate_tuning_offset_semitones_from_spectrogram over [80, 2000] Hz (src/lib.rs:1101-1109,
+// extractor.rs:98-140): the band is every bin with fmin <= f <= fmax
+TuningParams tuning_params(const sdsp_config& c, uint32_t sr, int B, float fres) {
+    TuningParams t{};
+    t.stride = STRIDE8;
+    const float fmin = sd_maxf(80.0f, 20.0f);
+    const float fmax = sd_clampf(2000.0f, fmin + 1.0f, (float)sr / 2.0f);
+    t.lo = 1;
+    t.hi = 0;
+    for (int b = 0; b < B; b++) {
+        const float f = (float)b * fres;
+        if (f < fmin) continue;
+        if (f > fmax) break;
+        if (t.lo > t.hi) t.lo = b;
+        t.hi = b;
+    }
+    t.step = (int)std::min<uint64_t>(std::max<uint64_t>(c.key_tuning_frame_step, 1), INT32_MAX);
+    const int tb = t.hi - t.lo + 1;
+    t.chf = tb > 0 ? std::max(1, std::min(8, 4096 / tb)) : 1;
+    t.fres = fres;
+    t.thr = sd_clampf(c.key_tuning_peak_rel_threshold, 0.0f, 1.0f);
+    t.lim = sd_absf(c.key_tuning_max_abs_semitones);
+    return t;
+}
+
+// k_chroma parameters: mode 0 frame_to_chroma_tuned (extractor.rs:393-481), mode 1 the
+// log-frequency conversion (extractor.rs:701-828, fmin 100, fmax 5000 from src/lib.rs:1068-1073)
+ChromaParams chroma_params(const sdsp_config& c, uint32_t sr, int mode, int B, float fres) {
+    ChromaParams p{};
+    p.B = B;
+    p.stride = STRIDE8;
+    p.fres = fres;
+    p.soft = c.soft_chroma_mapping ? 1 : 0;
+    p.sigma = c.soft_mapping_sigma;
+    p.gate_small = 1;
+    p.lo = 1;
+    p.hi = 0;
+    const float nyq = (float)sr / 2.0f;
+    if (mode == 0) {
+        const float top = sd_minf(5000.0f, nyq);
+        for (int b = 0; b < B; b++) {
+            const float f = (float)b * fres;
+            if (f < 100.0f) continue;
+            if (f > top || f >= nyq) break;
+            if (p.lo > p.hi) p.lo = b;
+            p.hi = b;
+        }
+    } else {
+        const float fmin = sd_maxf(100.0f, 20.0f), fmax = sd_minf(5000.0f, nyq - 1.0f);
+        const float smin = 12.0f * sd_log2f(fmin / 440.0f) + 57.0f;
+        const float smax = 12.0f * sd_log2f(fmax / 440.0f) + 57.0f;
+        p.bmin = sd_f2i32(__builtin_floorf(smin));
+        p.n_log = sd_f2i32(__builtin_ceilf(smax)) - p.bmin + 1;
+        p.log_off = sd_f2i32(__builtin_floorf(12.0f * sd_log2f(100.0f / 440.0f) + 57.0f));
+        for (int b = 0; b < B; b++) {
+            const float f = (float)b * fres;
+            if (f < fmin || f >= fmax || f >= nyq) continue;
+            if (p.lo > p.hi) p.lo = b;
+            p.hi = b;
+        }
+    }
+    return p;
+}
+
+// k_hpcp_x parameters (extractor.rs:529-680 with whitening, :1154-1244 bass blend)
+HpcpXParams hpcp_x_params(const sdsp_config& c, uint32_t sr, int B, float fres, bool whiten) {
+    HpcpXParams h{};
+    h.B = B;
+    h.stride = STRIDE8;
+    h.fres = fres;
+    h.fmin = sd_maxf(100.0f, 20.0f);
+    h.fmax = sd_minf(5000.0f, (float)sr / 2.0f);
+    h.main_ok = h.fmax > h.fmin;
+    band_bins(B, fres, h.fmin, h.fmax, &h.pk_lo, &h.pk_hi);
+    h.K = (int)std::max<uint64_t>(c.key_hpcp_peaks_per_frame, 1);
+    h.hmax = (int)std::max<uint64_t>(c.key_hpcp_num_harmonics, 1);
+    h.p = sd_clampf(c.key_hpcp_mag_power, 0.05f, 1.0f);
+    h.decay = sd_clampf(c.key_hpcp_harmonic_decay, 0.0f, 1.0f);
+    h.sigma = c.soft_mapping_sigma;
+    h.bass = c.enable_key_hpcp_bass_blend ? 1 : 0;
+    h.bk_lo = 1;
+    h.bk_hi = 0;
+    if (h.bass) {
+        h.bfmin = sd_maxf(c.key_hpcp_bass_fmin_hz, 20.0f);
+        h.bfmax = sd_minf(c.key_hpcp_bass_fmax_hz, (float)sr / 2.0f);
+        h.bass_ok = h.bfmax > h.bfmin;
+        band_bins(B, fres, h.bfmin, h.bfmax, &h.bk_lo, &h.bk_hi);
+        h.KB = (int)std::min<uint64_t>(std::max<uint64_t>(c.key_hpcp_peaks_per_frame, 1), 12);
+        h.bw = sd_clampf(c.key_hpcp_bass_weight, 0.0f, 1.0f);
+    }
+    if (whiten) {
+        const int win = (int)(std::max<uint64_t>(c.key_hpcp_whitening_smooth_bins, 3) | 1);
+        h.half = win / 2;
+        int rp = 1, rx = 1;
+        while (rp < 2 * h.half + 2) rp <<= 1;
+        while (rx < h.half + 1) rx <<= 1;
+        h.rp = rp, h.rp_mask = rp - 1, h.rx = rx, h.rx_mask = rx - 1;
+    }
+    return h;
+}
+
+// Configuration support that depends on the sample rate.
+std::string unsupported_sr(const sdsp_config& c, uint32_t sr) {
+    if (sr == 0) return "";
+    const int B8 = 8192 / 2 + 1;
+    const float fres = (float)sr / 8192.0f;
+    if (c.enable_key_log_frequency) {
+        const ChromaParams p = chroma_params(c, sr, 1, B8, fres);
+        if (p.n_log <= 0) return "degenerate key log-frequency range (sample rate too low)";
+        if ((size_t)(p.hi - p.lo + 1) * sizeof(ChromaBin) > 65536) return "log-frequency chroma band > 3276 bins";
+    } else if (c.enable_key_tuning_compensation) {
+        const TuningParams t = tuning_params(c, sr, B8, fres);
+        if (t.hi - t.lo + 1 > 4096) return "tuning band > 4096 bins";
+    }
+    if (!c.enable_key_log_frequency && !c.enable_key_hpcp) {
+        const ChromaParams p = chroma_params(c, sr, 0, B8, fres);
+        if ((size_t)(p.hi - p.lo + 1) * sizeof(ChromaBin) > 65536) return "chroma band > 3276 bins (sample rate too low)";
+    }
+    return "";
+}
+
 // templates.rs:64-145 (Krumhansl-Kessler) and :147-235 (Temperley): rows 0-23 K-K major/minor
 // keys, rows 24-47 Temperley; each profile rotated to the key, then L2-normalised.
 void key_templates(float* out /*48x12*/) {
@@ -367,13 +506,8 @@ std::string unsupported(const sdsp_config& c) {
         return "key STFT other than 8192";
     if (c.key_stft_hop_size == 0) return "key_stft_hop_size 0";
     if (c.enable_key_hpss_harmonic) return "key HPSS harmonic mask";
-    if (!c.enable_key_harmonic_mask && c.enable_key_spectrogram_time_smoothing) return "key time smoothing without mask";
     if (c.key_spectrogram_smooth_margin > 31) return "key_spectrogram_smooth_margin > 31";
-    if (c.enable_key_log_frequency) return "key log-frequency spectrogram";
-    if (c.enable_key_tuning_compensation) return "key tuning compensation";
-    if (c.enable_key_beat_synchronous) return "beat-synchronous chroma";
-    if (!c.enable_key_hpcp || c.enable_key_hpcp_bass_blend || c.enable_key_hpcp_whitening)
-        return "non-HPCP / bass-blend / whitened chroma";
+    if (c.enable_key_hpcp_whitening && c.key_hpcp_whitening_smooth_bins > 63) return "key_hpcp_whitening_smooth_bins > 63";
     if (c.key_hpcp_peaks_per_frame > (uint64_t)HP_KMAX) return "key_hpcp_peaks_per_frame > 32";
     if (c.key_hpcp_num_harmonics > (uint64_t)SUPPORT_HMAX) return "key_hpcp_num_harmonics > 8";
     if (c.enable_key_multi_scale && c.key_multi_scale_lengths_len > 8) return "more than 8 multi-scale key lengths";
@@ -444,7 +578,8 @@ void Pipeline::run(const float* d_samples, const std::vector<uint64_t>& in_off, 
                    std::vector<TrackRes>& res) {
     const size_t T = n_raw.size();
     res.assign(T, TrackRes{});
-    const std::string why = unsupported(cfg_);
+    std::string why = unsupported(cfg_);
+    if (why.empty()) why = unsupported_sr(cfg_, sr_);
     for (size_t i = 0; i < T; i++) {
         if (n_raw[i] == 0) {
             res[i].status = SDSP_ERR_INVALID_INPUT;
@@ -898,6 +1033,19 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
                             cfg_.key_segment_hop_frames >= 1;
     const bool ms_on = cfg_.enable_key_multi_scale && cfg_.key_multi_scale_lengths_len > 0;
     const uint64_t ms_hop = std::max<uint64_t>(std::min<uint64_t>(cfg_.key_multi_scale_hop, INT32_MAX), 1);
+    // segment scratch rows of a chroma slice of F rows (an upper bound: edge trim only shortens it)
+    auto seg_rows = [&](uint64_t F) -> uint64_t {
+        uint64_t ns = (seg_voting && F >= (uint64_t)std::max(seg_len_cfg, 1)) ? (F - seg_len_cfg) / seg_hop + 1 : 0;
+        if (ms_on) {
+            uint64_t nm = 0;
+            for (uint64_t j = 0; j < cfg_.key_multi_scale_lengths_len; j++) {
+                const uint64_t len = cfg_.key_multi_scale_lengths[j];
+                if (len != 0 && len <= F) nm += (F - len) / ms_hop + 1;
+            }
+            ns = std::max(ns, nm);
+        }
+        return ns;
+    };
     double key_in_bytes = 0;
     for (int i = 0; i < NR; i++) {
         const uint64_t n = bin.n_trim[(size_t)i];
@@ -906,17 +1054,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         K.push_back(i);
         kpfx.push_back(kpfx.back() + F8);
         ktile.push_back(ktile.back() + (F8 + HP_FRAMES - 1) / HP_FRAMES);
-        // segment rows (an upper bound: edge trim only shortens the frame range)
-        uint64_t ns = (seg_voting && F8 >= (uint64_t)std::max(seg_len_cfg, 1)) ? (F8 - seg_len_cfg) / seg_hop + 1 : 0;
-        if (ms_on) {
-            uint64_t nm = 0;
-            for (uint64_t j = 0; j < cfg_.key_multi_scale_lengths_len; j++) {
-                const uint64_t len = cfg_.key_multi_scale_lengths[j];
-                if (len != 0 && len <= F8) nm += (F8 - len) / ms_hop + 1;
-            }
-            ns = std::max(ns, nm);
-        }
-        kseg.push_back(kseg.back() + 64 * ns);
+        kseg.push_back(kseg.back() + 64 * seg_rows(F8));
         ksrc.push_back(bin.src_off[(size_t)i]);
         kgain.push_back(bin.gain_h[(size_t)i]);
         key_in_bytes += 4.0 * (double)n;
@@ -929,18 +1067,27 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     // SDSP_SERIAL_STREAMS=1 keeps the key path on the main stream (per-kernel profiling)
     static const bool serial_streams = std::getenv("SDSP_SERIAL_STREAMS") != nullptr;
     hipStream_t st2 = serial_streams ? st : d_.stream2;
+    float* d_tune = nullptr;  // per key track tuning offset (tuning compensation)
+    float* mags8 = nullptr;
+    uint64_t* d_kpfx = nullptr;
+    uint64_t* d_ktile = nullptr;
+    int* d_kid = nullptr;
+    float* d_tpl = nullptr;
+    KeyParams kp{};
+    const int B8 = KFS / 2 + 1;
+    const float fres8 = (float)sr_ / (float)KFS;
     if (NK > 0) {
         const uint64_t total8 = kpfx.back();
-        uint64_t* d_kpfx = c_.up("E.kpfx", kpfx);
-        uint64_t* d_ktile = c_.up("E.ktile", ktile);
+        d_kpfx = c_.up("E.kpfx", kpfx);
+        d_ktile = c_.up("E.ktile", ktile);
         uint64_t* d_kseg = c_.up("E.kseg", kseg);
         uint64_t* d_ksrc = c_.up("E.ksrc", ksrc);
         float* d_kgain = c_.up("E.kgain", kgain);
         std::vector<int> kid((size_t)NK);
         for (int k = 0; k < NK; k++) kid[(size_t)k] = k;
-        int* d_kid = c_.up("E.kid", kid);
+        d_kid = c_.up("E.kid", kid);
         FftTables& t8 = d_.tables(KFS, true);
-        float* mags8 = c_.dev<float>("E.mags8", total8 * STRIDE8);
+        mags8 = c_.dev<float>("E.mags8", total8 * STRIDE8);
         // uploads above were queued on the main stream: order the key stream after them
         kt.mark(7);
         SDSP_HIP_CHECK(hipStreamWaitEvent(st2, kt.ev[7], 0));
@@ -949,44 +1096,52 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
                     t8.stft_rt.as<cx>(), mags8, d_kpfx, STRIDE8, nullptr, st2);
         SDSP_HIP_CHECK(hipGetLastError());
         kt.mark(1, st2);
-        const int B8 = KFS / 2 + 1;
+        // key spectrogram conditioning (src/lib.rs:1011-1060)
         if (cfg_.enable_key_harmonic_mask)
             launch_mask(mags8, STRIDE8, B8, d_kpfx, d_kid, NK, (int)cfg_.key_spectrogram_smooth_margin,
                         cfg_.key_harmonic_mask_power, st2);
-        HpcpParams hp{};
-        hp.B = B8;
-        hp.stride = STRIDE8;
-        const float fres8 = (float)sr_ / (float)KFS;
-        const float fmin = sd_maxf(100.0f, 20.0f), fmax = sd_minf(5000.0f, (float)sr_ / 2.0f);
-        hp.pk_lo = 1;
-        hp.pk_hi = 0;
-        if (fmax > fmin) {
-            int lo = -1, hi = -1;
-            for (int b = 1; b + 1 < B8; b++) {
-                const float f = (float)b * fres8;
-                if (f < fmin) continue;
-                if (f > fmax) break;
-                if (lo < 0) lo = b;
-                hi = b;
-            }
-            if (lo >= 0) {
-                hp.pk_lo = lo;
-                hp.pk_hi = hi;
-            }
+        else if (cfg_.enable_key_spectrogram_time_smoothing)
+            launch_mask(mags8, STRIDE8, B8, d_kpfx, d_kid, NK, (int)cfg_.key_spectrogram_smooth_margin,
+                        cfg_.key_harmonic_mask_power, st2, true);
+        const bool use_log = cfg_.enable_key_log_frequency;  // :1062-1095
+        // tuning offset per track (:1097-1119)
+        if (cfg_.enable_key_tuning_compensation && !use_log) {
+            TuningParams tp = tuning_params(cfg_, sr_, B8, fres8);
+            d_tune = c_.dev<float>("E.tune", (size_t)NK);
+            launch_tuning(mags8, d_kpfx, d_kid, NK, tp, d_tune, st2);
+            SDSP_HIP_CHECK(hipGetLastError());
         }
-        hp.K = (int)std::max<uint64_t>(cfg_.key_hpcp_peaks_per_frame, 1);
-        hp.hmax = (int)std::max<uint64_t>(cfg_.key_hpcp_num_harmonics, 1);
-        hp.p = sd_clampf(cfg_.key_hpcp_mag_power, 0.05f, 1.0f);
-        std::vector<HarmEntry> ht = harm_table(B8, sr_, KFS, cfg_.soft_mapping_sigma, hp.hmax, cfg_.key_hpcp_harmonic_decay);
-        HarmEntry* d_ht = c_.up("E.harm", ht);
         float* d_chroma = c_.dev<float>("E.chroma", total8 * 12);
         float* d_energy = c_.dev<float>("E.energy", total8);
-        launch_hpcp(mags8, d_kpfx, d_ktile, d_kid, NK, ktile.back(), hp, d_ht, d_chroma, d_energy, st2);
+        const bool whiten = cfg_.enable_key_hpcp_whitening && cfg_.key_hpcp_whitening_smooth_bins >= 3;
+        if (use_log) {  // :1120-1131
+            const ChromaParams cp = chroma_params(cfg_, sr_, 1, B8, fres8);
+            launch_chroma(1, mags8, d_kpfx, d_ktile, d_kid, NK, ktile.back(), cp, nullptr, d_chroma, d_energy, st2);
+        } else if (cfg_.enable_key_hpcp && (d_tune || whiten || cfg_.enable_key_hpcp_bass_blend)) {  // :1133-1168
+            const HpcpXParams hx = hpcp_x_params(cfg_, sr_, B8, fres8, whiten);
+            launch_hpcp_x(mags8, d_kpfx, d_ktile, d_kid, NK, ktile.back(), hx, d_tune, d_chroma, d_energy, st2);
+        } else if (cfg_.enable_key_hpcp) {
+            HpcpParams hp{};
+            hp.B = B8;
+            hp.stride = STRIDE8;
+            hp.pk_lo = 1;
+            hp.pk_hi = 0;
+            band_bins(B8, fres8, sd_maxf(100.0f, 20.0f), sd_minf(5000.0f, (float)sr_ / 2.0f), &hp.pk_lo, &hp.pk_hi);
+            hp.K = (int)std::max<uint64_t>(cfg_.key_hpcp_peaks_per_frame, 1);
+            hp.hmax = (int)std::max<uint64_t>(cfg_.key_hpcp_num_harmonics, 1);
+            hp.p = sd_clampf(cfg_.key_hpcp_mag_power, 0.05f, 1.0f);
+            std::vector<HarmEntry> ht =
+                harm_table(B8, sr_, KFS, cfg_.soft_mapping_sigma, hp.hmax, cfg_.key_hpcp_harmonic_decay);
+            HarmEntry* d_ht = c_.up("E.harm", ht);
+            launch_hpcp(mags8, d_kpfx, d_ktile, d_kid, NK, ktile.back(), hp, d_ht, d_chroma, d_energy, st2);
+        } else {  // :1169-1197 (the tuned variant only when |offset| > 1e-6)
+            const ChromaParams cp = chroma_params(cfg_, sr_, 0, B8, fres8);
+            launch_chroma(0, mags8, d_kpfx, d_ktile, d_kid, NK, ktile.back(), cp, d_tune, d_chroma, d_energy, st2);
+        }
         SDSP_HIP_CHECK(hipGetLastError());
         std::vector<float> tpl(576);
         key_templates(tpl.data());
-        float* d_tpl = c_.up("E.tpl", tpl);
-        KeyParams kp{};
+        d_tpl = c_.up("E.tpl", tpl);
         kp.weighting = cfg_.enable_key_frame_weighting;
         kp.min_tonal = cfg_.key_min_tonalness;
         kp.tonal_pow = cfg_.key_tonalness_power;
@@ -1213,6 +1368,51 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     std::vector<float> cand_h;
     if (cfg_.emit_tempogram_candidates) cand_h = c_.down(bo.cand, (size_t)NR * (size_t)bin.cand_cap * 4);
     htr("D down");
+    // beat-synchronous chroma (src/lib.rs:1121-1133): for key tracks with a non-empty beat grid the
+    // chroma rows are the beat intervals' mean frame chroma; the key vote is re-run on them
+    if (cfg_.enable_key_beat_synchronous && !cfg_.enable_key_log_frequency && NK > 0) {
+        std::vector<int> sel, sel_id;
+        std::vector<uint64_t> sb_off, rpfx(1, 0), sseg(1, 0);
+        for (int k = 0; k < NK; k++) {
+            const int i = K[(size_t)k];
+            const int nb = bout[(size_t)i].ok > 0 ? bout[(size_t)i].n_beats : 0;
+            if (nb < 1) continue;
+            sel.push_back(k);
+            sel_id.push_back((int)sel_id.size());
+            sb_off.push_back(bpfx[(size_t)i]);
+            const uint64_t rows = (uint64_t)nb - 1;
+            rpfx.push_back(rpfx.back() + rows);
+            sseg.push_back(sseg.back() + 64 * seg_rows(rows));
+        }
+        const int NS = (int)sel.size();
+        if (NS > 0) {
+            const uint64_t total8 = kpfx.back();
+            ChromaParams cp = chroma_params(cfg_, sr_, 0, B8, fres8);
+            cp.gate_small = 0;  // extract_beat_synchronous_chroma takes the offset as is
+            float* fc = c_.dev<float>("E.bs_fc", total8 * 12);
+            float* fe = c_.dev<float>("E.bs_fe", total8);
+            launch_chroma(0, mags8, d_kpfx, d_ktile, d_kid, NK, ktile.back(), cp, d_tune, fc, fe, st);
+            int* d_sel = c_.up("E.bs_sel", sel);
+            int* d_sid = c_.up("E.bs_id", sel_id);
+            uint64_t* d_sboff = c_.up("E.bs_boff", sb_off);
+            uint64_t* d_rpfx = c_.up("E.bs_rpfx", rpfx);
+            uint64_t* d_sseg = c_.up("E.bs_seg", sseg);
+            const uint64_t rows = std::max<uint64_t>(rpfx.back(), 1);
+            float* bc = c_.dev<float>("E.bs_chroma", rows * 12);
+            float* be = c_.dev<float>("E.bs_energy", rows);
+            const float fd = (float)KHOP / (float)sr_;
+            launch_beat_sync(d_sel, NS, d_kpfx, fc, fe, d_cbeats, d_sboff, d_rpfx, fd, bc, be, st);
+            float* bcs = c_.dev<float>("E.bs_chroma_s", rows * 12);
+            float* bw = c_.dev<float>("E.bs_weights", rows);
+            float* bscr = c_.dev<float>("E.bs_segscr", std::max<uint64_t>(sseg.back(), 1));
+            KeyOut* d_bko = c_.dev<KeyOut>("E.bs_kout", (size_t)NS);
+            launch_key_vote(d_sid, NS, d_rpfx, bc, be, bcs, bw, bscr, d_sseg, d_tpl, kp, d_bko, st);
+            SDSP_HIP_CHECK(hipGetLastError());
+            std::vector<KeyOut> bko = c_.down(d_bko, (size_t)NS);
+            for (int j = 0; j < NS; j++) kout[(size_t)sel[(size_t)j]] = bko[(size_t)j];
+        }
+        htr("E beat-sync");
+    }
     times_.beat_ms += tm.ms(4, 5);
     for (int i = 0; i < NR; i++) {
         TrackRes& r = res[(size_t)idx[(size_t)R[(size_t)i]]];
