@@ -430,8 +430,11 @@ void analyze(const float* samples, size_t n, uint32_t sr, const sdsp_config& c, 
         if (kfft & (kfft - 1)) not_impl("non power-of-two key_stft_frame_size");
         Spec ks = c.enable_key_stft_override ? compute_stft(trim.data(), trim.size(), kfft, khop) : mags;
         if (!ks.empty()) {  // :1011-1060
-            if (c.enable_key_hpss_harmonic) not_impl("key HPSS harmonic mask");
-            if (c.enable_key_harmonic_mask)
+            if (c.enable_key_hpss_harmonic)
+                key_hpss_mask_inplace(ks, sr, kfft, 100.0f, 5000.0f, (size_t)c.key_hpss_frame_step,
+                                      (size_t)c.key_hpss_time_margin, (size_t)c.key_hpss_freq_margin,
+                                      c.key_hpss_mask_power);
+            else if (c.enable_key_harmonic_mask)
                 harmonic_mask_inplace(ks, (size_t)c.key_spectrogram_smooth_margin, c.key_harmonic_mask_power);
             else if (c.enable_key_spectrogram_time_smoothing)
                 smooth_time_inplace(ks, (size_t)c.key_spectrogram_smooth_margin);

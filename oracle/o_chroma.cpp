@@ -374,3 +374,79 @@ float sdsp_oracle_tuning(const float* spec, uint64_t frames, uint64_t bins, uint
 }
 
 }  // extern "C"
+
+namespace orc {
+
+// extractor.rs:1369-1501 (harmonic_spectrogram_hpss_median_mask), in place.  The medians are
+// order statistics (element len/2 of the sorted window), so any selection algorithm gives the
+// reference's value.
+void key_hpss_mask_inplace(Spec& s, uint32_t sr, size_t fft_size, float fmin_hz, float fmax_hz, size_t frame_step,
+                           size_t time_margin, size_t freq_margin, float mask_power) {
+    if (s.empty() || sr == 0 || fft_size == 0) return;
+    const size_t F = s.frames, B = s.bins;
+    const float fres = (float)sr / (float)fft_size;
+    const float fmin = sd_maxf(fmin_hz, 20.0f);
+    const float fmax = sd_clampf(fmax_hz, fmin + 1.0f, (float)sr / 2.0f);
+    int64_t bs = sd_f2i64(__builtin_floorf(fmin / fres)), be = sd_f2i64(__builtin_ceilf(fmax / fres));
+    bs = std::min<int64_t>(std::max<int64_t>(bs, 0), (int64_t)B);
+    be = std::min<int64_t>(std::max<int64_t>(be, 0), (int64_t)B);
+    if (be <= bs) return;
+    const size_t b0 = (size_t)bs, nb = (size_t)(be - bs);
+    const size_t step = std::max<size_t>(frame_step, 1);
+    const size_t nds = std::max<size_t>((F + step - 1) / step, 1);
+    auto san = [](float x) { return sd_isfinite_f(x) ? sd_maxf(x, 0.0f) : 0.0f; };
+    std::vector<float> ds(nds * nb), h(nds * nb), pe(nds * nb);
+    for (size_t k = 0; k < nds; k++)
+        for (size_t b = 0; b < nb; b++) ds[k * nb + b] = s.row(k * step)[b0 + b];
+    std::vector<float> w;
+    auto median = [&](std::vector<float>& v) {
+        if (v.empty()) return 0.0f;
+        const size_t mid = v.size() / 2;
+        std::nth_element(v.begin(), v.begin() + (long)mid, v.end());
+        return v[mid];
+    };
+    for (size_t b = 0; b < nb; b++)
+        for (size_t t = 0; t < nds; t++) {
+            w.clear();
+            const size_t st = t >= time_margin ? t - time_margin : 0, en = std::min(t + time_margin + 1, nds);
+            for (size_t k = st; k < en; k++) w.push_back(san(ds[k * nb + b]));
+            h[t * nb + b] = median(w);
+        }
+    for (size_t t = 0; t < nds; t++)
+        for (size_t b = 0; b < nb; b++) {
+            w.clear();
+            const size_t st = b >= freq_margin ? b - freq_margin : 0, en = std::min(b + freq_margin + 1, nb);
+            for (size_t q = st; q < en; q++) w.push_back(san(ds[t * nb + q]));
+            pe[t * nb + b] = median(w);
+        }
+    const float p = sd_maxf(mask_power, 1.0f);
+    std::vector<float> mask(nds * nb);
+    for (size_t i = 0; i < nds * nb; i++) {
+        const float hh = sd_maxf(h[i], 0.0f), pp = sd_maxf(pe[i], 0.0f);
+        const float hp = sd_powf(hh, p), ppw = sd_powf(pp, p);
+        mask[i] = hp / (hp + ppw + 1e-12f);
+    }
+    for (size_t t = 0; t < F; t++) {
+        float* row = s.row(t);
+        const size_t k = std::min(t / step, nds - 1);
+        for (size_t b = 0; b < B; b++) {
+            if (b < b0 || b >= b0 + nb) {
+                row[b] = 0.0f;  // the reference's output starts as zeros; only the band is written
+                continue;
+            }
+            row[b] = san(row[b]) * mask[k * nb + (b - b0)];
+        }
+    }
+}
+
+}  // namespace orc
+
+extern "C" void sdsp_oracle_key_hpss(float* spec, uint64_t frames, uint64_t bins, uint32_t sr, uint64_t fft_size,
+                                     uint64_t step, uint64_t tm, uint64_t fm, float power) {
+    orc::Spec s;
+    s.frames = (size_t)frames;
+    s.bins = (size_t)bins;
+    s.d.assign(spec, spec + frames * bins);
+    orc::key_hpss_mask_inplace(s, sr, (size_t)fft_size, 100.0f, 5000.0f, (size_t)step, (size_t)tm, (size_t)fm, power);
+    std::copy(s.d.begin(), s.d.end(), spec);
+}

@@ -63,6 +63,8 @@ def lib():
         L.sdsp_oracle_chroma.restype = C.c_int64
         L.sdsp_oracle_tuning.argtypes = [fp, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint64, C.c_float]
         L.sdsp_oracle_tuning.restype = C.c_float
+        L.sdsp_oracle_key_hpss.argtypes = [fp, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64,
+                                           C.c_uint64, C.c_float]
         _lib = L
     return _lib
 
@@ -182,6 +184,14 @@ def chroma(mode, spec, sample_rate=44100, fft_size=8192, hop=512, soft=True, sig
                                  C.c_float(sigma), C.c_float(tuning), _fp(b), b.size, _fp(ch), _fp(en), cap)
     assert n >= 0
     return ch[:n].copy(), en[:n].copy()
+
+
+def key_hpss(spec, sample_rate=44100, fft_size=8192, step=4, time_margin=8, freq_margin=8, power=2.0):
+    """harmonic_spectrogram_hpss_median_mask over [100, 5000] Hz (src/lib.rs:1014-1024)."""
+    s = np.array(spec, dtype=np.float32, order="C")
+    lib().sdsp_oracle_key_hpss(_fp(s), s.shape[0], s.shape[1], sample_rate, fft_size, step, time_margin, freq_margin,
+                               C.c_float(power))
+    return s
 
 
 def tuning(spec, sample_rate=44100, fft_size=8192, frame_step=20, rel_threshold=0.35):

@@ -139,6 +139,8 @@ bool log_freq_chroma(const Spec& s, uint32_t sr, size_t fft_size, std::vector<fl
 void beat_sync_chroma(const Spec& s, uint32_t sr, size_t fft_size, size_t hop, const std::vector<float>& beats,
                       bool soft, float sigma, float tuning, std::vector<float>* chroma12, std::vector<float>* energies);
 void smooth_time_inplace(Spec& s, size_t margin);
+void key_hpss_mask_inplace(Spec& s, uint32_t sr, size_t fft_size, float fmin_hz, float fmax_hz, size_t frame_step,
+                           size_t time_margin, size_t freq_margin, float mask_power);
 
 struct KeyResult {
     int mode;

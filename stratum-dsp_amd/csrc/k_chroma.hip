@@ -532,6 +532,118 @@ __global__ __launch_bounds__(256) void k_beat_sync(const int* __restrict__ track
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Key HPSS median mask (extractor.rs:1369-1501).  k_key_hpss_mask: for every downsampled frame k
+// (every `step`-th frame) and band bin b, the median over time (ds frames k +- tm) and over
+// frequency (bins b +- fm) of the sanitised magnitudes, and the soft mask h^p / (h^p + p^p + eps).
+// A workgroup owns KH_TK ds frames x 64 bins; the tile plus its halo is staged in LDS, and each
+// median is a rank selection over the window held in registers (out-of-range slots are +inf, so
+// they rank last and the order statistic len/2 of the real values is unchanged).
+constexpr int KH_TK = 16, KH_MAXM = 16, KH_COLS = 64;
+__device__ __forceinline__ float kh_san(float x) { return sd_isfinite_f(x) ? sd_maxf(x, 0.0f) : 0.0f; }
+
+template <int W>
+__device__ __forceinline__ float rank_select(const float (&v)[W], int mid) {
+    float med = 0.0f;
+#pragma unroll
+    for (int j = 0; j < W; j++) {
+        int lt = 0, le = 0;
+#pragma unroll
+        for (int q = 0; q < W; q++) {
+            lt += v[q] < v[j];
+            le += v[q] <= v[j];
+        }
+        if (lt <= mid && mid < le) med = v[j];
+    }
+    return med;
+}
+
+template <int M>  // M: compile-time window half width bound (== the margins when FIXED)
+__global__ __launch_bounds__(256) void k_key_hpss_mask(const float* __restrict__ mags,
+                                                       const uint64_t* __restrict__ frame_pfx,
+                                                       const uint64_t* __restrict__ tile_pfx,
+                                                       const uint64_t* __restrict__ mask_off,
+                                                       const int* __restrict__ tracks, int n_items, KeyHpssParams P,
+                                                       float* __restrict__ mask) {
+    constexpr int W = 2 * M + 1;
+    __shared__ float tl[KH_TK + 2 * KH_MAXM][KH_COLS + 2 * KH_MAXM + 1];
+    const uint64_t gb = blockIdx.x;
+    const int it = find_track(tile_pfx, n_items, gb);
+    const int trk = tracks[it];
+    const int64_t F = (int64_t)(frame_pfx[trk + 1] - frame_pfx[trk]);
+    const int64_t nds = F > 0 ? (F + P.step - 1) / P.step : 1;
+    const int64_t nbt = (P.nb + KH_COLS - 1) / KH_COLS;
+    const int64_t lt_ = (int64_t)(gb - tile_pfx[it]);
+    const int64_t k0 = (lt_ / nbt) * KH_TK;
+    const int b0 = (int)(lt_ % nbt) * KH_COLS;
+    const float* base = mags + frame_pfx[trk] * (uint64_t)P.stride + P.bin0;
+    const int tm = P.tm, fm = P.fm;
+    const int rows = KH_TK + 2 * tm, cols = KH_COLS + 2 * fm;
+    const float INF = __builtin_inff();
+    for (int e = threadIdx.x; e < rows * cols; e += 256) {
+        const int r = e / cols, c = e % cols;
+        const int64_t k = k0 - tm + r;
+        const int b = b0 - fm + c;
+        float v = INF;
+        if (k >= 0 && k < nds && b >= 0 && b < P.nb) v = kh_san(base[(uint64_t)(k * P.step) * (uint64_t)P.stride + b]);
+        tl[r][c] = v;
+    }
+    __syncthreads();
+    const int c = threadIdx.x % KH_COLS, q0 = threadIdx.x / KH_COLS;
+    const int b = b0 + c;
+    if (b >= P.nb) return;
+    float* mo = mask + mask_off[it];
+    for (int kk = q0; kk < KH_TK; kk += 256 / KH_COLS) {
+        const int64_t k = k0 + kk;
+        if (k >= nds) break;
+        float v[W];
+#pragma unroll
+        for (int o = 0; o < W; o++) {
+            const int d = o - M;
+            v[o] = (d >= -tm && d <= tm) ? tl[kk + tm + d][c + fm] : INF;
+        }
+        const int64_t ts = k >= tm ? k - tm : 0, te = k + tm + 1 < nds ? k + tm + 1 : nds;
+        const float h = rank_select<W>(v, (int)((te - ts) / 2));
+#pragma unroll
+        for (int o = 0; o < W; o++) {
+            const int d = o - M;
+            v[o] = (d >= -fm && d <= fm) ? tl[kk + tm][c + fm + d] : INF;
+        }
+        const int bs = b >= fm ? b - fm : 0, be = b + fm + 1 < P.nb ? b + fm + 1 : P.nb;
+        const float pe = rank_select<W>(v, (be - bs) / 2);
+        const float hh = sd_maxf(h, 0.0f), pp = sd_maxf(pe, 0.0f);
+        const float hp = sd_powf(hh, P.p), ppw = sd_powf(pp, P.p);
+        mo[(uint64_t)k * (uint64_t)P.nb + (uint64_t)b] = hp / (hp + ppw + 1e-12f);
+    }
+}
+
+// Applies the downsampled mask to every frame in place: band bins -> sanitised x * mask, every
+// other bin -> 0 (the reference's output rows start as zeros).  KH_FR frames per workgroup.
+constexpr int KH_FR = 8;
+__global__ __launch_bounds__(256) void k_key_hpss_apply(float* __restrict__ mags, const uint64_t* __restrict__ frame_pfx,
+                                                        const uint64_t* __restrict__ tile_pfx,
+                                                        const uint64_t* __restrict__ mask_off,
+                                                        const int* __restrict__ tracks, int n_items, KeyHpssParams P,
+                                                        const float* __restrict__ mask) {
+    const uint64_t gb = blockIdx.x;
+    const int it = find_track(tile_pfx, n_items, gb);
+    const int trk = tracks[it];
+    const int64_t F = (int64_t)(frame_pfx[trk + 1] - frame_pfx[trk]);
+    const int64_t nds = (F + P.step - 1) / P.step;
+    const int64_t t0 = (int64_t)(gb - tile_pfx[it]) * KH_FR;
+    const float* mo = mask + mask_off[it];
+    for (int64_t t = t0; t < t0 + KH_FR && t < F; t++) {
+        float* row = mags + (frame_pfx[trk] + (uint64_t)t) * (uint64_t)P.stride;
+        int64_t k = t / P.step;
+        if (k > nds - 1) k = nds - 1;
+        const float* mk = mo + (uint64_t)k * (uint64_t)P.nb;
+        for (int b = threadIdx.x; b < P.B; b += 256) {
+            const int j = b - P.bin0;
+            row[b] = (j >= 0 && j < P.nb) ? kh_san(row[b]) * mk[j] : 0.0f;
+        }
+    }
+}
+
 // ---- launchers ----
 void launch_tuning(const float* mags, const uint64_t* frame_pfx, const int* tracks, int n_items, const TuningParams& P,
                    float* out, hipStream_t st) {
@@ -586,6 +698,19 @@ void launch_hpcp_x(const float* mags, const uint64_t* frame_pfx, const uint64_t*
     else
         hpcp_x_dispatch<HP_KMAX>(wh, P.bass, g, lds, st, mags, frame_pfx, tile_pfx, tracks, n_items, P, tuning, chroma,
                                  energy);
+}
+void launch_key_hpss(float* mags, const uint64_t* frame_pfx, const uint64_t* mtile_pfx, uint64_t n_mtiles,
+                     const uint64_t* atile_pfx, uint64_t n_atiles, const uint64_t* mask_off, const int* tracks,
+                     int n_items, const KeyHpssParams& P, float* mask, hipStream_t st) {
+    if (n_items == 0) return;
+    if (P.tm <= 8 && P.fm <= 8)
+        hipLaunchKernelGGL(k_key_hpss_mask<8>, dim3((unsigned)n_mtiles), dim3(256), 0, st, mags, frame_pfx, mtile_pfx,
+                           mask_off, tracks, n_items, P, mask);
+    else
+        hipLaunchKernelGGL(k_key_hpss_mask<KH_MAXM>, dim3((unsigned)n_mtiles), dim3(256), 0, st, mags, frame_pfx,
+                           mtile_pfx, mask_off, tracks, n_items, P, mask);
+    hipLaunchKernelGGL(k_key_hpss_apply, dim3((unsigned)n_atiles), dim3(256), 0, st, mags, frame_pfx, atile_pfx,
+                       mask_off, tracks, n_items, P, mask);
 }
 void launch_beat_sync(const int* tracks, int n_items, const uint64_t* frame_pfx, const float* fchroma,
                       const float* fenergy, const float* beats, const uint64_t* beat_off, const uint64_t* row_pfx,

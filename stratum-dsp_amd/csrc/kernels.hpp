@@ -149,6 +149,13 @@ struct HpcpXParams {
     float p, fres, fmin, fmax, bfmin, bfmax, decay, sigma, bw;
 };
 
+struct KeyHpssParams {
+    int B, stride, bin0, nb;  // bins per row; row stride; median band [bin0, bin0 + nb)
+    int step, tm, fm;         // frame step; time / frequency margins (<= 16)
+    float p;                  // mask power (>= 1)
+};
+constexpr int KH_TILE_FRAMES = 16, KH_TILE_BINS = 64, KH_APPLY_FRAMES = 8;  // k_key_hpss_* tiling
+
 // ---- launchers ----
 void launch_stft(int nfft, bool frame_max, const float* samples, const uint64_t* frame_pfx, int n_tracks,
                  uint64_t total_frames, const uint64_t* src_off, const float* gain, int hop, const float* window,
@@ -218,6 +225,9 @@ void launch_chroma(int mode, const float* mags, const uint64_t* frame_pfx, const
 void launch_hpcp_x(const float* mags, const uint64_t* frame_pfx, const uint64_t* tile_pfx, const int* tracks,
                    int n_items, uint64_t n_tiles, const HpcpXParams& P, const float* tuning, float* chroma,
                    float* energy, hipStream_t st);
+void launch_key_hpss(float* mags, const uint64_t* frame_pfx, const uint64_t* mtile_pfx, uint64_t n_mtiles,
+                     const uint64_t* atile_pfx, uint64_t n_atiles, const uint64_t* mask_off, const int* tracks,
+                     int n_items, const KeyHpssParams& P, float* mask, hipStream_t st);
 void launch_beat_sync(const int* tracks, int n_items, const uint64_t* frame_pfx, const float* fchroma,
                       const float* fenergy, const float* beats, const uint64_t* beat_off, const uint64_t* row_pfx,
                       float fd, float* chroma, float* energy, hipStream_t st);

@@ -316,6 +316,26 @@ HpcpXParams hpcp_x_params(const sdsp_config& c, uint32_t sr, int B, float fres, 
     return h;
 }
 
+// harmonic_spectrogram_hpss_median_mask's band and windows (extractor.rs:1400-1420, with
+// fmin 100 / fmax 5000 from src/lib.rs:1014-1024); nb = 0 when the band is empty
+KeyHpssParams key_hpss_params(const sdsp_config& c, uint32_t sr, int B, float fres) {
+    KeyHpssParams k{};
+    k.B = B;
+    k.stride = STRIDE8;
+    const float fmin = sd_maxf(100.0f, 20.0f);
+    const float fmax = sd_clampf(5000.0f, fmin + 1.0f, (float)sr / 2.0f);
+    int64_t bs = sd_f2i64(__builtin_floorf(fmin / fres)), be = sd_f2i64(__builtin_ceilf(fmax / fres));
+    bs = std::min<int64_t>(std::max<int64_t>(bs, 0), B);
+    be = std::min<int64_t>(std::max<int64_t>(be, 0), B);
+    k.bin0 = (int)bs;
+    k.nb = be > bs ? (int)(be - bs) : 0;
+    k.step = (int)std::min<uint64_t>(std::max<uint64_t>(c.key_hpss_frame_step, 1), INT32_MAX);
+    k.tm = (int)std::min<uint64_t>(c.key_hpss_time_margin, 1u << 20);
+    k.fm = (int)std::min<uint64_t>(c.key_hpss_freq_margin, 1u << 20);
+    k.p = sd_maxf(c.key_hpss_mask_power, 1.0f);
+    return k;
+}
+
 // Configuration support that depends on the sample rate.
 std::string unsupported_sr(const sdsp_config& c, uint32_t sr) {
     if (sr == 0) return "";
@@ -505,7 +525,8 @@ std::string unsupported(const sdsp_config& c) {
     if (!c.enable_key_stft_override || std::max<uint64_t>(c.key_stft_frame_size, 256) != 8192)
         return "key STFT other than 8192";
     if (c.key_stft_hop_size == 0) return "key_stft_hop_size 0";
-    if (c.enable_key_hpss_harmonic) return "key HPSS harmonic mask";
+    if (c.enable_key_hpss_harmonic && (c.key_hpss_time_margin > 16 || c.key_hpss_freq_margin > 16))
+        return "key_hpss_time_margin / key_hpss_freq_margin > 16";
     if (c.key_spectrogram_smooth_margin > 31) return "key_spectrogram_smooth_margin > 31";
     if (c.enable_key_hpcp_whitening && c.key_hpcp_whitening_smooth_bins > 63) return "key_hpcp_whitening_smooth_bins > 63";
     if (c.key_hpcp_peaks_per_frame > (uint64_t)HP_KMAX) return "key_hpcp_peaks_per_frame > 32";
@@ -1097,7 +1118,28 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         SDSP_HIP_CHECK(hipGetLastError());
         kt.mark(1, st2);
         // key spectrogram conditioning (src/lib.rs:1011-1060)
-        if (cfg_.enable_key_harmonic_mask)
+        if (cfg_.enable_key_hpss_harmonic) {
+            const KeyHpssParams kh = key_hpss_params(cfg_, sr_, B8, fres8);
+            if (kh.nb > 0) {  // an empty band returns the spectrogram unchanged (extractor.rs:1408-1410)
+                std::vector<uint64_t> moff(1, 0), mt(1, 0), at(1, 0);
+                for (int k = 0; k < NK; k++) {
+                    const uint64_t F8 = kpfx[(size_t)k + 1] - kpfx[(size_t)k];
+                    const uint64_t nds = (F8 + (uint64_t)kh.step - 1) / (uint64_t)kh.step;
+                    moff.push_back(moff.back() + nds * (uint64_t)kh.nb);
+                    mt.push_back(mt.back() + ((nds + KH_TILE_FRAMES - 1) / KH_TILE_FRAMES) *
+                                                 (((uint64_t)kh.nb + KH_TILE_BINS - 1) / KH_TILE_BINS));
+                    at.push_back(at.back() + (F8 + KH_APPLY_FRAMES - 1) / KH_APPLY_FRAMES);
+                }
+                uint64_t* d_moff = c_.up("E.kh_off", moff);
+                uint64_t* d_mt = c_.up("E.kh_mt", mt);
+                uint64_t* d_at = c_.up("E.kh_at", at);
+                float* d_kmask = c_.dev<float>("E.kh_mask", std::max<uint64_t>(moff.back(), 1));
+                // the uploads are on the main stream
+                kt.mark(9);
+                SDSP_HIP_CHECK(hipStreamWaitEvent(st2, kt.ev[9], 0));
+                launch_key_hpss(mags8, d_kpfx, d_mt, mt.back(), d_at, at.back(), d_moff, d_kid, NK, kh, d_kmask, st2);
+            }
+        } else if (cfg_.enable_key_harmonic_mask)
             launch_mask(mags8, STRIDE8, B8, d_kpfx, d_kid, NK, (int)cfg_.key_spectrogram_smooth_margin,
                         cfg_.key_harmonic_mask_power, st2);
         else if (cfg_.enable_key_spectrogram_time_smoothing)

@@ -1,7 +1,8 @@
 """Parity of the opt-in key chroma front-ends against the oracle.
 
 Each case switches the key path's spectrogram conditioning or chroma front-end
-(src/lib.rs:1011-1198): time smoothing without the mask, no conditioning, plain
+(src/lib.rs:1011-1198): the HPSS median mask (extractor.rs:1369-1501), time smoothing without the
+mask, no conditioning, plain
 frame_to_chroma (soft / hard), tuning compensation (extractor.rs:66-177) with HPCP and with plain
 chroma, HPCP whitening and bass blend (extractor.rs:529-680, 1154-1244), the log-frequency
 spectrogram (extractor.rs:701-985) and beat-synchronous chroma (extractor.rs:830-935).  A ragged
@@ -69,6 +70,11 @@ CASES = {
     "beat_sync_tuned_hard": dict(enable_key_beat_synchronous=1, enable_key_tuning_compensation=1,
                                  key_tuning_max_abs_semitones=0.5, soft_chroma_mapping=0),
     "beat_sync_log": dict(enable_key_beat_synchronous=1, enable_key_log_frequency=1),
+    "key_hpss": dict(enable_key_hpss_harmonic=1),
+    "key_hpss_small": dict(enable_key_hpss_harmonic=1, key_hpss_frame_step=1, key_hpss_time_margin=3,
+                           key_hpss_freq_margin=5, key_hpss_mask_power=1.0),
+    "key_hpss_wide": dict(enable_key_hpss_harmonic=1, key_hpss_frame_step=3, key_hpss_time_margin=12,
+                          key_hpss_freq_margin=16, key_hpss_mask_power=3.0, enable_key_hpcp=0),
     "beat_sync_no_voting": dict(enable_key_beat_synchronous=1, enable_key_segment_voting=0,
                                 chroma_sharpening_power=2.0),
 }
@@ -99,7 +105,8 @@ def test_chroma_option_parity(case):
 
 
 @pytest.mark.parametrize("sr", [22050, 48000])
-@pytest.mark.parametrize("case", ["plain_soft", "tuning_hpcp_wide", "log_frequency", "bass_white_tuned", "beat_sync"])
+@pytest.mark.parametrize("case", ["plain_soft", "tuning_hpcp_wide", "log_frequency", "bass_white_tuned", "beat_sync",
+                                  "key_hpss"])
 def test_chroma_option_sample_rates(case, sr):
     xs = [synth.make_track(s, seconds=20.0, sr=sr)[0] for s in (5, 7)]
     _run(case, xs, sr)
@@ -111,7 +118,7 @@ def test_chroma_options_change_results():
     base = sdsp.analyze_batch(xs, SR, sdsp.default_config())
     changed = set()
     for case in ("plain_soft", "tuning_hpcp_wide", "whitening", "bass_heavy", "log_frequency", "beat_sync",
-                 "time_smooth"):
+                 "time_smooth", "key_hpss"):
         cfg = sdsp.default_config()
         for k, v in CASES[case].items():
             setattr(cfg, k, v)

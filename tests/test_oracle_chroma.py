@@ -5,7 +5,8 @@ Pinned two ways:
     the oracle: A4 maps to pitch class 9, unit L2 norms, soft and hard mapping give equal lengths;
   * independent float64 numpy restatements of each function's arithmetic (extractor.rs:66-177
     tuning, :393-481 chroma, :529-680 whitened HPCP peaks, :701-985 log-frequency chroma,
-    :830-935 beat-synchronous chroma), which must agree to float32 rounding.  The reference has no
+    :830-935 beat-synchronous chroma, :1369-1501 the key HPSS median mask), which must agree to
+    float32 rounding.  The reference has no
     unit test of these numbers, so beyond the restated formulas their values are "parity unpinned".
 """
 import math
@@ -219,3 +220,36 @@ def test_hpcp_tuning_shifts(key_spec):
     assert np.array_equal(a, b)
     c, _ = oracle.chroma("hpcp", key_spec, tuning=0.3)
     assert not np.array_equal(a, c)
+
+
+def np_key_hpss(spec, sr, fft, step, tm, fm, p):
+    F, B = spec.shape
+    fres = np.float32(sr) / np.float32(fft)
+    fmax = min(max(5000.0, 101.0), sr / 2)
+    b0 = min(max(int(np.floor(np.float32(100.0) / fres)), 0), B)
+    b1 = min(max(int(np.ceil(np.float32(fmax) / fres)), 0), B)
+    san = np.where(np.isfinite(spec), np.maximum(spec, 0), 0).astype(np.float64)
+    ds = san[::step, b0:b1]
+    nds, nb = ds.shape
+    h = np.zeros_like(ds)
+    pe = np.zeros_like(ds)
+    for t in range(nds):
+        for b in range(nb):
+            w = np.sort(ds[max(t - tm, 0):min(t + tm + 1, nds), b])
+            h[t, b] = w[w.size // 2]
+            w = np.sort(ds[t, max(b - fm, 0):min(b + fm + 1, nb)])
+            pe[t, b] = w[w.size // 2]
+    m = h ** p / (h ** p + pe ** p + 1e-12)
+    out = np.zeros_like(san)
+    k = np.minimum(np.arange(F) // step, nds - 1)
+    out[:, b0:b1] = san[:, b0:b1] * m[k]
+    return out
+
+
+@pytest.mark.parametrize("step,tm,fm,p", [(4, 8, 8, 2.0), (1, 3, 5, 1.0), (3, 12, 2, 3.0)])
+def test_key_hpss_vs_numpy(key_spec, step, tm, fm, p):
+    spec = key_spec[:60]
+    got = oracle.key_hpss(spec, step=step, time_margin=tm, freq_margin=fm, power=p)
+    ref = np_key_hpss(spec, SR, 8192, step, tm, fm, p)
+    assert np.allclose(got, ref, rtol=1e-5, atol=1e-7 * float(np.max(spec)))
+    assert not got[:, :18].any() and not got[:, 930:].any()  # outside [100, 5000] Hz -> 0
