@@ -183,6 +183,21 @@ void analyze(const float* samples, size_t n, uint32_t sr, const sdsp_config& c, 
     tr.energy_onsets = energy;
     Spec mags = compute_stft(trim.data(), trim.size(), FS, HOP);  // :166
     std::vector<size_t> on_legacy = energy, on_beat = energy;
+    // HPSS percussive component of the base spectrogram (hpss.rs:71-172): shared by the HPSS onsets
+    // (:222-236) and the percussive tempogram fallback (:587-683), which decompose the same input
+    Spec hp_H, hp_P;
+    int hp_state = 0;  // 0 not computed, 1 ok, -1 failed
+    auto percussive = [&]() -> const Spec* {
+        if (hp_state == 0) {
+            try {
+                hpss_decompose(mags, (size_t)c.hpss_margin, &hp_H, &hp_P);
+                hp_state = 1;
+            } catch (const AErr&) {
+                hp_state = -1;
+            }
+        }
+        return hp_state == 1 ? &hp_P : nullptr;
+    };
     if (c.enable_onset_consensus && !mags.empty()) {  // :176-291
         auto to_samples = [&](const std::vector<size_t>& fr) {
             std::vector<size_t> s;
@@ -204,7 +219,12 @@ void analyze(const float* samples, size_t n, uint32_t sr, const sdsp_config& c, 
             lists[2] = to_samples(hfc_onsets(mags, sr, c.onset_threshold_percentile));
         } catch (const AErr&) {
         }
-        if (c.enable_hpss_onsets) not_impl("HPSS onsets");
+        if (c.enable_hpss_onsets) {
+            try {
+                if (const Spec* p = percussive()) lists[3] = to_samples(hpss_onsets(*p, c.onset_threshold_percentile));
+            } catch (const AErr&) {
+            }
+        }
         tr.spectral_onsets = lists[1];
         tr.hfc_onsets = lists[2];
         try {
@@ -349,7 +369,43 @@ void analyze(const float* samples, size_t n, uint32_t sr, const sdsp_config& c, 
                 o.mr_used = used;
                 tr.used_mr = used;
                 o.perc_trig = ambiguous && trap_low;
-                if (c.enable_tempogram_percussive_fallback) not_impl("percussive tempogram fallback");
+                if (c.enable_tempogram_percussive_fallback && ambiguous && trap_low) {  // :587-679
+                    const Spec* p = percussive();
+                    BpmEstimate pe;
+                    std::vector<TempoCand> pc;
+                    bool ok = p != nullptr;
+                    if (ok) {
+                        try {
+                            tempogram_impl(*p, sr, (uint32_t)HOP, c.min_bpm, c.max_bpm, c.bpm_resolution, bp, &pe, &pc);
+                            if (pc.size() > base_top_n) pc.resize(base_top_n);
+                        } catch (const AErr&) {
+                            ok = false;
+                        }
+                    }
+                    bool p_used = false;
+                    if (ok) {
+                        const float rel =
+                            chosen.bpm > 1e-6f ? sd_maxf(pe.bpm / chosen.bpm, chosen.bpm / pe.bpm) : 1.0f;
+                        const bool fam = sd_absf(rel - 2.0f) < 0.05f || sd_absf(rel - 1.5f) < 0.05f ||
+                                         sd_absf(rel - (4.0f / 3.0f)) < 0.05f || sd_absf(rel - (3.0f / 2.0f)) < 0.05f ||
+                                         sd_absf(rel - (2.0f / 3.0f)) < 0.05f || sd_absf(rel - (3.0f / 4.0f)) < 0.05f;
+                        const bool forbid = chosen.bpm <= 180.0f && pe.bpm > 180.0f;
+                        const bool base_low_trap = trap_low || base.bpm < 95.0f;
+                        const bool in_common = pe.bpm >= 70.0f && pe.bpm <= 180.0f;
+                        p_used = !forbid && fam && in_common &&
+                                 (pe.confidence >= chosen.confidence + 0.04f ||
+                                  (base_low_trap && pe.confidence >= chosen.confidence * 0.85f) ||
+                                  (pe.method_agreement > chosen.method_agreement &&
+                                   pe.confidence >= chosen.confidence * 0.92f));
+                        if (p_used) {
+                            chosen = pe;
+                            chosen_c = pc;
+                        }
+                    }
+                    o.perc_used = p_used;
+                } else if (c.enable_tempogram_percussive_fallback) {
+                    o.perc_used = 0;
+                }
                 if (c.emit_tempogram_candidates) {
                     o.has_cands = true;
                     o.cands = chosen_c;

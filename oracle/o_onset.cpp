@@ -329,3 +329,110 @@ std::vector<OnsetCand> vote_onsets(const std::vector<size_t> lists[4], const flo
 }
 
 }  // namespace orc
+
+namespace orc {
+
+// hpss.rs:179-243: the median of every window [i - margin, i + margin] ∩ [0, n) along one row or
+// column (sorted window; even length -> mean of the middle two times 0.5).  The sorted window is
+// kept across positions (insert the entering value, erase the leaving one): the same multiset the
+// reference collects and sorts per position, so the same median.
+static void sliding_medians(const float* src, size_t n, size_t stride, size_t margin, float* dst, size_t dstride,
+                            std::vector<float>& w) {
+    w.clear();
+    const size_t e0 = std::min(margin + 1, n);
+    for (size_t k = 0; k < e0; k++) w.insert(std::upper_bound(w.begin(), w.end(), src[k * stride]), src[k * stride]);
+    for (size_t i = 0; i < n; i++) {
+        const size_t c = w.size(), mid = c / 2;
+        dst[i * dstride] = c == 0 ? 0.0f : (c % 2 ? w[mid] : (w[mid - 1] + w[mid]) * 0.5f);
+        if (i + margin + 1 < n) {
+            const float v = src[(i + margin + 1) * stride];
+            w.insert(std::upper_bound(w.begin(), w.end(), v), v);
+        }
+        if (i >= margin) w.erase(std::lower_bound(w.begin(), w.end(), src[(i - margin) * stride]));
+    }
+}
+
+// src/features/onset/hpss.rs:71-172 (hpss_decompose, DEFAULT_ITERATIONS = 10)
+void hpss_decompose(const Spec& m, size_t margin, Spec* H, Spec* P) {
+    if (m.empty()) fail(SDSP_ERR_INVALID_INPUT, "Empty spectrogram");
+    if (m.bins == 0) fail(SDSP_ERR_INVALID_INPUT, "Empty frames");
+    const size_t F = m.frames, B = m.bins;
+    *H = m;
+    *P = m;
+    Spec hf = m, pf = m;
+    std::vector<float> w;
+    for (int it = 0; it < 10; it++) {
+        const Spec hprev = *H, pprev = *P;
+        for (size_t b = 0; b < B; b++)  // apply_horizontal_median_filter (:179-209)
+            sliding_medians(H->d.data() + b, F, B, margin, hf.d.data() + b, B, w);
+        for (size_t t = 0; t < F; t++)  // apply_vertical_median_filter (:213-243)
+            sliding_medians(P->row(t), B, 1, margin, pf.row(t), 1, w);
+        float max_change = 0.0f;
+        for (size_t i = 0; i < F * B; i++) {
+            const float orig = m.d[i], h = hf.d[i], p = pf.d[i];
+            const float total = h + p;
+            if (total > 1e-10f) {
+                H->d[i] = orig * (h / total);
+                P->d[i] = orig * (p / total);
+            } else {
+                H->d[i] = orig * 0.5f;
+                P->d[i] = orig * 0.5f;
+            }
+            if (it > 0)
+                max_change = sd_maxf(sd_maxf(max_change, sd_absf(H->d[i] - hprev.d[i])), sd_absf(P->d[i] - pprev.d[i]));
+        }
+        if (it > 0 && max_change < 1e-6f) break;
+    }
+}
+
+// hpss.rs:290-372 (detect_hpss_onsets): energy flux of the percussive frames, percentile peaks
+std::vector<size_t> hpss_onsets(const Spec& p, float pct) {
+    if (p.empty()) return {};
+    if (!(pct >= 0.0f && pct <= 1.0f)) fail(SDSP_ERR_INVALID_INPUT, "Threshold percentile must be in [0, 1]");
+    if (p.frames < 2) return {};
+    std::vector<float> e(p.frames);
+    for (size_t t = 0; t < p.frames; t++) {
+        float s = 0.0f;
+        const float* r = p.row(t);
+        for (size_t b = 0; b < p.bins; b++) s += r[b] * r[b];
+        e[t] = s;
+    }
+    std::vector<float> flux(p.frames - 1);
+    for (size_t i = 1; i < p.frames; i++) flux[i - 1] = sd_maxf(e[i] - e[i - 1], 0.0f);
+    return peaks_over_percentile(flux, pct);
+}
+
+}  // namespace orc
+
+// ctypes entry points for the HPSS unit tests (tests/test_oracle_hpss.py)
+extern "C" int32_t sdsp_oracle_hpss(const float* spec, uint64_t frames, uint64_t bins, uint64_t margin, float* h,
+                                    float* p) {
+    orc::Spec s, H, P;
+    s.frames = (size_t)frames;
+    s.bins = (size_t)bins;
+    s.d.assign(spec, spec + frames * bins);
+    try {
+        orc::hpss_decompose(s, (size_t)margin, &H, &P);
+    } catch (const orc::AErr& e) {
+        return e.code;
+    }
+    std::copy(H.d.begin(), H.d.end(), h);
+    std::copy(P.d.begin(), P.d.end(), p);
+    return 0;
+}
+
+extern "C" int64_t sdsp_oracle_hpss_onsets(const float* p, uint64_t frames, uint64_t bins, float pct, uint64_t* out,
+                                           uint64_t cap) {
+    orc::Spec s;
+    s.frames = (size_t)frames;
+    s.bins = (size_t)bins;
+    s.d.assign(p, p + frames * bins);
+    std::vector<size_t> on;
+    try {
+        on = orc::hpss_onsets(s, pct);
+    } catch (const orc::AErr&) {
+        return -1;
+    }
+    for (size_t i = 0; i < on.size() && i < cap; i++) out[i] = (uint64_t)on[i];
+    return (int64_t)on.size();
+}

@@ -65,6 +65,11 @@ def lib():
         L.sdsp_oracle_tuning.restype = C.c_float
         L.sdsp_oracle_key_hpss.argtypes = [fp, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64,
                                            C.c_uint64, C.c_float]
+        L.sdsp_oracle_hpss.argtypes = [fp, C.c_uint64, C.c_uint64, C.c_uint64, fp, fp]
+        L.sdsp_oracle_hpss.restype = C.c_int32
+        L.sdsp_oracle_hpss_onsets.argtypes = [fp, C.c_uint64, C.c_uint64, C.c_float, C.POINTER(C.c_uint64),
+                                              C.c_uint64]
+        L.sdsp_oracle_hpss_onsets.restype = C.c_int64
         _lib = L
     return _lib
 
@@ -192,6 +197,28 @@ def key_hpss(spec, sample_rate=44100, fft_size=8192, step=4, time_margin=8, freq
     lib().sdsp_oracle_key_hpss(_fp(s), s.shape[0], s.shape[1], sample_rate, fft_size, step, time_margin, freq_margin,
                                C.c_float(power))
     return s
+
+
+def hpss(spec, margin):
+    """hpss_decompose (hpss.rs:71-172) -> (status, harmonic, percussive)."""
+    s = np.ascontiguousarray(spec, dtype=np.float32)
+    frames = s.shape[0] if s.ndim == 2 else 0
+    bins = s.shape[1] if s.ndim == 2 else 0
+    h = np.zeros((frames, bins), np.float32)
+    p = np.zeros((frames, bins), np.float32)
+    st = lib().sdsp_oracle_hpss(_fp(s), frames, bins, margin, _fp(h), _fp(p))
+    return st, h, p
+
+
+def hpss_onsets(perc, pct):
+    """detect_hpss_onsets (hpss.rs:275-373) -> onset frame list, or None on Err."""
+    s = np.ascontiguousarray(perc, dtype=np.float32)
+    frames = s.shape[0] if s.ndim == 2 else 0
+    bins = s.shape[1] if s.ndim == 2 else 0
+    out = np.zeros(frames + 2, np.uint64)
+    n = lib().sdsp_oracle_hpss_onsets(_fp(s), frames, bins, C.c_float(pct), out.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                      out.size)
+    return None if n < 0 else [int(v) for v in out[:n]]
 
 
 def tuning(spec, sample_rate=44100, fft_size=8192, frame_step=20, rel_threshold=0.35):

@@ -78,6 +78,8 @@ struct OnsetCand {
     float time_seconds, confidence;
     uint32_t voted_by;
 };
+void hpss_decompose(const Spec& m, size_t margin, Spec* H, Spec* P);  // hpss.rs:71-172
+std::vector<size_t> hpss_onsets(const Spec& p, float pct);            // hpss.rs:290-372
 std::vector<OnsetCand> vote_onsets(const std::vector<size_t> lists[4], const float w[4], uint32_t tol_ms,
                                    uint32_t sr);
 

@@ -165,11 +165,12 @@ __global__ __launch_bounds__(256) void k_energy_onsets(const float* __restrict__
     if (threadIdx.x == 0) out_n[trk] = base;
 }
 
-// Spectral-flux (kind 0) or HFC (kind 1) onsets: percentile threshold + local peaks, as
-// sample positions f*hop < n (spectral_flux.rs:160-215, hfc.rs:156-208, src/lib.rs:181-190).
-// sfo: per-frame-pair spectral flux (index t-1 for pair (t-1,t)); hfc: per-frame HFC.
+// Spectral-flux (kind 0), HFC (kind 1) or HPSS (kind 2) onsets: percentile threshold + local
+// peaks, as sample positions f*hop < n (spectral_flux.rs:160-215, hfc.rs:156-208,
+// hpss.rs:318-368, src/lib.rs:181-236).  sfo: per-frame-pair spectral flux (index t-1 for pair
+// (t-1,t)); hfc: per-frame HFC; hpe: per-frame energy of the percussive spectrogram.
 __global__ __launch_bounds__(256) void k_flux_onsets(const float* __restrict__ sfo, const float* __restrict__ hfc,
-                                                     float* __restrict__ scratch,
+                                                     const float* __restrict__ hpe, float* __restrict__ scratch,
                                                      const uint64_t* __restrict__ frame_pfx,
                                                      const uint64_t* __restrict__ n_trim, int hop, float pct,
                                                      uint32_t* __restrict__ out, const uint64_t* __restrict__ out_off,
@@ -192,8 +193,8 @@ __global__ __launch_bounds__(256) void k_flux_onsets(const float* __restrict__ s
     if (kind == 0) {
         const float* s = sfo + frame_pfx[trk];
         for (int64_t i = threadIdx.x; i < L; i += blockDim.x) fl[i] = s[i];
-    } else {
-        const float* h = hfc + frame_pfx[trk];
+    } else {  // kind 1: HFC flux (hfc.rs:143-146); kind 2: percussive energy flux (hpss.rs:311-316)
+        const float* h = (kind == 1 ? hfc : hpe) + frame_pfx[trk];
         for (int64_t i = threadIdx.x; i < L; i += blockDim.x) fl[i] = sd_maxf(h[i + 1] - h[i], 0.0f);
     }
     __syncthreads();
@@ -260,7 +261,7 @@ __global__ __launch_bounds__(256) void k_consensus(const uint32_t* __restrict__ 
                                                    uint64_t kind_stride, int T, uint32_t tol, int enable,
                                                    const int* __restrict__ has_mags, uint32_t* __restrict__ chosen,
                                                    const uint64_t* __restrict__ c_off, int* __restrict__ c_n,
-                                                   uint32_t* __restrict__ scr) {
+                                                   uint32_t* __restrict__ scr, int hpss) {
     SDSP_LATENCY_CRITICAL();
     __shared__ int red[8];
     const int t = blockIdx.x;
@@ -278,10 +279,11 @@ __global__ __launch_bounds__(256) void k_consensus(const uint32_t* __restrict__ 
     }
     const uint32_t* L1 = flux_on + f_off[t];
     const uint32_t* L2 = flux_on + f_off[t] + kind_stride;
-    const int n1 = f_n[t], n2 = f_n[T + t];
-    const int N = n0 + n1 + n2;
+    const uint32_t* L3 = flux_on + f_off[t] + 2 * kind_stride;  // HPSS onsets (kind 2) when enabled
+    const int n1 = f_n[t], n2 = f_n[T + t], n3 = hpss ? f_n[2 * T + t] : 0;
+    const int N = n0 + n1 + n2 + n3;
     const uint64_t cap = (uint64_t)N > 0 ? (uint64_t)N : 1;
-    uint32_t* mv = scr + c_off[t] * 5;  // c_off = 3 * frame offset: 3F slots per array
+    uint32_t* mv = scr + c_off[t] * 5;  // c_off = (3 or 4) * frame offset: 3F / 4F slots per array
     uint32_t* mm = mv + cap;
     uint32_t* cs = mm + cap;
     uint32_t* cc = cs + cap;
@@ -298,15 +300,20 @@ __global__ __launch_bounds__(256) void k_consensus(const uint32_t* __restrict__ 
             a = 1;
             i = e - n0;
             s = L1[i];
-        } else {
+        } else if (e < n0 + n1 + n2) {
             a = 2;
             i = e - n0 - n1;
             s = L2[i];
+        } else {
+            a = 3;
+            i = e - n0 - n1 - n2;
+            s = L3[i];
         }
-        int pos = i;
-        pos += a == 0 ? 0 : ub_u32(L0, n0, s);  // earlier lists win ties
+        int pos = i;  // stable merge rank: earlier lists win ties
+        pos += a == 0 ? 0 : ub_u32(L0, n0, s);
         pos += a == 1 ? 0 : (a < 1 ? lb_u32(L1, n1, s) : ub_u32(L1, n1, s));
-        pos += a == 2 ? 0 : lb_u32(L2, n2, s);
+        pos += a == 2 ? 0 : (a < 2 ? lb_u32(L2, n2, s) : ub_u32(L2, n2, s));
+        pos += a == 3 ? 0 : lb_u32(L3, n3, s);
         mv[pos] = s;
         mm[pos] = (uint32_t)a;
     }
@@ -656,20 +663,21 @@ void launch_energy_onsets(const float* rms, const uint64_t* frame_pfx, const uin
     hipLaunchKernelGGL(k_energy_onsets, dim3(T), dim3(256), 0, st, rms, frame_pfx, n_trim, hop, factor, out, out_off,
                        out_n);
 }
-void launch_flux_onsets(const float* sfo, const float* hfc, float* scratch, const uint64_t* frame_pfx,
+void launch_flux_onsets(const float* sfo, const float* hfc, const float* hpe, float* scratch, const uint64_t* frame_pfx,
                         const uint64_t* n_trim, int hop, float pct, uint32_t* out, const uint64_t* out_off,
                         int* out_n, int T, hipStream_t st) {
     if (T == 0) return;
-    hipLaunchKernelGGL(k_flux_onsets, dim3(2 * T), dim3(256), 0, st, sfo, hfc, scratch, frame_pfx, n_trim, hop, pct,
-                       out, out_off, out_n, T);
+    const int kinds = hpe ? 3 : 2;
+    hipLaunchKernelGGL(k_flux_onsets, dim3(kinds * T), dim3(256), 0, st, sfo, hfc, hpe, scratch, frame_pfx, n_trim, hop,
+                       pct, out, out_off, out_n, T);
 }
 void launch_consensus(const uint32_t* energy, const uint64_t* e_off, const int* e_n, const uint32_t* flux_on,
                       const uint64_t* f_off, const int* f_n, uint64_t kind_stride, int T, uint32_t tol, int enable,
                       const int* has_mags, uint32_t* chosen, const uint64_t* c_off, int* c_n, uint32_t* scratch,
-                      hipStream_t st) {
+                      hipStream_t st, int hpss) {
     if (T == 0) return;
     hipLaunchKernelGGL(k_consensus, dim3(T), dim3(256), 0, st, energy, e_off, e_n, flux_on, f_off, f_n, kind_stride, T,
-                       tol, enable, has_mags, chosen, c_off, c_n, scratch);
+                       tol, enable, has_mags, chosen, c_off, c_n, scratch, hpss);
 }
 
 }  // namespace sdsp

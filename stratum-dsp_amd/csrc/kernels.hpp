@@ -156,6 +156,28 @@ struct KeyHpssParams {
 };
 constexpr int KH_TILE_FRAMES = 16, KH_TILE_BINS = 64, KH_APPLY_FRAMES = 8;  // k_key_hpss_* tiling
 
+// ---- k_hpss (hpss_decompose, hpss.rs:71-281) ----
+struct HpssParams {
+    int B, stride, m;  // bins per row, row stride, median half width (hpss_margin, <= 16)
+};
+struct HpssLaunch {
+    HpssParams P;
+    const float* orig;           // the spectrogram (round 0 input, re-partitioned every round)
+    const uint64_t* orig_row0;   // per item: first row of its frames in `orig`
+    float* h[2];                 // ping-pong harmonic buffers
+    float* p[2];                 // ping-pong percussive buffers (the result ends in p[0])
+    const uint64_t* row0;        // per item: first row in h / p (== fpfx: compact)
+    const uint64_t* fpfx;        // frame prefix over the items
+    const uint64_t* htile_pfx;   // k_hpss_hmed tiles: ceil(F / 256) * ceil(B / 256) per item
+    uint64_t n_htiles;
+    const uint64_t* vtile_pfx;   // k_hpss_vmed tiles: ceil(F / 32) * ceil(B / 256) per item
+    uint64_t n_vtiles;
+    int* last_it;                // per item: last round run (init 9)
+    unsigned int* change;        // per item: the round's largest change (f32 bits)
+    int n_items;
+};
+constexpr int HPSS_HM_FRAMES = 256, HPSS_VM_FRAMES = 32, HPSS_COLS = 256, HPSS_ROW_FRAMES = 256;
+
 // ---- launchers ----
 void launch_stft(int nfft, bool frame_max, const float* samples, const uint64_t* frame_pfx, int n_tracks,
                  uint64_t total_frames, const uint64_t* src_off, const float* gain, int hop, const float* window,
@@ -183,13 +205,13 @@ void launch_trim(const float* rms, const uint64_t* frame_pfx, int T, const uint6
                  uint64_t min_frames, int enable, uint64_t* trim_start, uint64_t* trim_end, hipStream_t st);
 void launch_energy_onsets(const float* rms, const uint64_t* frame_pfx, const uint64_t* n_trim, int hop, float factor,
                           uint32_t* out, const uint64_t* out_off, int* out_n, int T, hipStream_t st);
-void launch_flux_onsets(const float* sfo, const float* hfc, float* scratch, const uint64_t* frame_pfx,
+void launch_flux_onsets(const float* sfo, const float* hfc, const float* hpe, float* scratch, const uint64_t* frame_pfx,
                         const uint64_t* n_trim, int hop, float pct, uint32_t* out, const uint64_t* out_off,
                         int* out_n, int T, hipStream_t st);
 void launch_consensus(const uint32_t* energy, const uint64_t* e_off, const int* e_n, const uint32_t* flux_on,
                       const uint64_t* f_off, const int* f_n, uint64_t kind_stride, int T, uint32_t tol, int enable,
                       const int* has_mags, uint32_t* chosen, const uint64_t* c_off, int* c_n, uint32_t* scratch,
-                      hipStream_t st);
+                      hipStream_t st, int hpss = 0);
 void launch_features(const float* mags, const float* fmax, const uint64_t* frame_pfx, const uint64_t* tile_pfx,
                      int T, uint64_t n_tiles, const FeatParams& P, const MelPlan* mel, float* E, float* H, float* SFX,
                      float* SFO, float* MEL, uint64_t total, hipStream_t st);
@@ -228,6 +250,9 @@ void launch_hpcp_x(const float* mags, const uint64_t* frame_pfx, const uint64_t*
 void launch_key_hpss(float* mags, const uint64_t* frame_pfx, const uint64_t* mtile_pfx, uint64_t n_mtiles,
                      const uint64_t* atile_pfx, uint64_t n_atiles, const uint64_t* mask_off, const int* tracks,
                      int n_items, const KeyHpssParams& P, float* mask, hipStream_t st);
+void launch_hpss(const HpssLaunch& L, hipStream_t st);
+void launch_hpss_rows(const float* p, const uint64_t* row0, const uint64_t* fpfx, const uint64_t* tile_pfx,
+                      uint64_t n_tiles, int n_items, int stride, int B, float* energy, float* fmax, hipStream_t st);
 void launch_beat_sync(const int* tracks, int n_items, const uint64_t* frame_pfx, const float* fchroma,
                       const float* fenergy, const float* beats, const uint64_t* beat_off, const uint64_t* row_pfx,
                       float fd, float* chroma, float* energy, hipStream_t st);

@@ -454,6 +454,13 @@ struct Ctx {
         }
         return b.as<T>();
     }
+    // a host copy that lives until the context's queued work is done (async H2D source)
+    template <class T>
+    const void* keep_bytes(const std::vector<T>& v) {
+        keep.emplace_back(reinterpret_cast<const uint8_t*>(v.data()),
+                          reinterpret_cast<const uint8_t*>(v.data()) + v.size() * sizeof(T));
+        return keep.back().data();
+    }
     template <class T>
     T* dev(const std::string& name, size_t n) {
         DevBuf& b = d.buf(name);
@@ -514,9 +521,8 @@ std::string unsupported(const sdsp_config& c) {
         return "unknown normalization method";
     if (c.frame_size != 2048) return "frame_size other than 2048";
     if (c.hop_size == 0 || c.hop_size > 8192) return "hop_size outside 1..8192";
-    if (c.enable_hpss_onsets) return "HPSS onsets";
+    if ((c.enable_hpss_onsets || c.enable_tempogram_percussive_fallback) && c.hpss_margin > 16) return "hpss_margin > 16";
     if (c.force_legacy_bpm || c.enable_bpm_fusion) return "legacy-BPM output paths (force_legacy_bpm / enable_bpm_fusion)";
-    if (c.enable_tempogram_percussive_fallback) return "percussive tempogram fallback";
     if (!(c.min_bpm > 0.0f && c.max_bpm > c.min_bpm && c.bpm_resolution > 0.0f)) return "BPM range/resolution";
     if (c.tempogram_superflux_max_filter_bins > (uint64_t)FT_KMAX) return "superflux_max_filter_bins > 8";
     if (c.enable_tempogram_mel_novelty && std::max<uint64_t>(c.tempogram_mel_n_mels, 4) > (uint64_t)FT_MELMAX)
@@ -550,6 +556,10 @@ struct TempoPassIn {
     std::vector<uint64_t> n_trim;
     bool want_onsets;  // hop-512 pass: also spectral/HFC onset features (SFO)
     int top_n, gate, cand_cap;
+    // a precomputed 2048-point spectrogram (rows at the pass's frame prefix, STRIDE2) and its frame
+    // maxima: the STFT is skipped (the percussive tempogram fallback runs on the HPSS output)
+    const float* mags_in = nullptr;
+    const float* fmax_in = nullptr;
 };
 struct TempoPassOut {
     std::vector<uint64_t> fpfx;  // frame prefix over the pass's tracks
@@ -647,6 +657,9 @@ void Pipeline::run(const float* d_samples, const std::vector<uint64_t>& in_off, 
         const double n = (double)n_raw[i];
         need[i] = n / hop * (STRIDE2 * 4.0 * 1.3 + 4 * 70.0) + n / khop * STRIDE8 * 4.0 +
                   (n / 256 + n / 1024) * STRIDE2 * 4.0 + 1e6;
+        if (cfg_.enable_hpss_onsets || cfg_.enable_tempogram_percussive_fallback)  // H, P ping-pong + a copy
+            need[i] += n / hop * STRIDE2 * 4.0 * 5.0;
+        if (cfg_.enable_key_hpss_harmonic) need[i] += n / khop * 1024.0 * 4.0;
         total_need += need[i];
     }
     const double parts = std::max(1.0, std::ceil(total_need / budget));
@@ -729,17 +742,22 @@ void Pipeline::tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPa
     o.active = c_.up(tag + "active", o.active_h);
     // STFT
     FftTables& tb = d_.tables(FS, true);
-    o.mags = c_.dev<float>(tag + "mags", total * STRIDE2);
-    o.fmax = c_.dev<float>(tag + "fmax", total);
     Timers tm;
     tm.init(d_);
     tm.mark(0);
-    launch_stft(FS, true, in.samples, o.d_fpfx, P_T, total, d_src, d_gain, hop, tb.window.as<float>(), tb.stft_tw.as<cx>(),
-                tb.stft_rt.as<cx>(), o.mags, o.d_fpfx, STRIDE2, o.fmax, d_.stream);
-    SDSP_HIP_CHECK(hipGetLastError());
+    if (in.mags_in) {
+        o.mags = const_cast<float*>(in.mags_in);
+        o.fmax = const_cast<float*>(in.fmax_in);
+    } else {
+        o.mags = c_.dev<float>(tag + "mags", total * STRIDE2);
+        o.fmax = c_.dev<float>(tag + "fmax", total);
+        launch_stft(FS, true, in.samples, o.d_fpfx, P_T, total, d_src, d_gain, hop, tb.window.as<float>(),
+                    tb.stft_tw.as<cx>(), tb.stft_rt.as<cx>(), o.mags, o.d_fpfx, STRIDE2, o.fmax, d_.stream);
+        SDSP_HIP_CHECK(hipGetLastError());
+    }
     tm.mark(1);
-    o.stft_launch = total ? 1 : 0;
-    {
+    o.stft_launch = (total && !in.mags_in) ? 1 : 0;
+    if (!in.mags_in) {
         double inb = 0;
         for (int t = 0; t < P_T; t++) inb += 4.0 * (double)in.n_trim[(size_t)t];
         o.stft_bytes = inb + 4.0 * (double)total * 1025.0;
@@ -1233,7 +1251,67 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     times_.features_ms += bo.feat_ms;
     times_.tempogram_ms += bo.tempo_ms;
     tm.mark(2);
-    // onsets: energy flux (frame FS, hop HOP; same framing as the STFT), spectral flux, HFC, consensus
+    // HPSS (hpss.rs:71-172) of the hop-512 spectrogram: for the HPSS onsets every track
+    // (src/lib.rs:222-236), for the percussive tempogram fallback only the tracks in the low
+    // trap zone (src/lib.rs:587-598); both read the same decomposition.
+    const bool hpss_on = cfg_.enable_hpss_onsets && cfg_.enable_onset_consensus;
+    const bool perc_on = mr_on && cfg_.enable_tempogram_percussive_fallback;
+    std::vector<TempoEst> best;
+    std::vector<int> S;                 // HPSS items (positions in R)
+    std::vector<uint64_t> hpfx(1, 0);   // frame prefix over S
+    float *d_P0 = nullptr, *d_hpe = nullptr, *d_hfmax = nullptr;
+    if (hpss_on || perc_on) {
+        best = c_.down(bo.est, (size_t)NR);
+        for (int i = 0; i < NR; i++) {
+            const TempoEst& e = best[(size_t)i];
+            if (hpss_on || (e.ok && e.ambiguous && e.trap_low)) {
+                S.push_back(i);
+                hpfx.push_back(hpfx.back() + (bo.fpfx[(size_t)i + 1] - bo.fpfx[(size_t)i]));
+            }
+        }
+        const int NS = (int)S.size();
+        const uint64_t totS = hpfx.back();
+        if (NS > 0 && totS > 0) {
+            std::vector<uint64_t> orow, ht(1, 0), vt(1, 0), rt(1, 0);
+            const uint64_t ncb = (1025 + HPSS_COLS - 1) / HPSS_COLS;
+            for (int k = 0; k < NS; k++) {
+                const uint64_t F = hpfx[(size_t)k + 1] - hpfx[(size_t)k];
+                orow.push_back(bo.fpfx[(size_t)S[(size_t)k]]);
+                ht.push_back(ht.back() + (F + HPSS_HM_FRAMES - 1) / HPSS_HM_FRAMES * ncb);
+                vt.push_back(vt.back() + (F + HPSS_VM_FRAMES - 1) / HPSS_VM_FRAMES * ncb);
+                rt.push_back(rt.back() + (F + HPSS_ROW_FRAMES - 1) / HPSS_ROW_FRAMES);
+            }
+            HpssLaunch L{};
+            L.P.B = 1025;
+            L.P.stride = STRIDE2;
+            L.P.m = (int)cfg_.hpss_margin;
+            L.orig = bo.mags;
+            L.orig_row0 = c_.up("H.orow", orow);
+            for (int q = 0; q < 2; q++) {
+                L.h[q] = c_.dev<float>("H.h" + std::to_string(q), totS * STRIDE2);
+                L.p[q] = c_.dev<float>("H.p" + std::to_string(q), totS * STRIDE2);
+            }
+            uint64_t* d_hpfx = c_.up("H.hpfx", hpfx);
+            L.row0 = d_hpfx;
+            L.fpfx = d_hpfx;
+            L.htile_pfx = c_.up("H.ht", ht);
+            L.n_htiles = ht.back();
+            L.vtile_pfx = c_.up("H.vt", vt);
+            L.n_vtiles = vt.back();
+            L.last_it = c_.up("H.last", std::vector<int>((size_t)NS, 9));
+            L.change = c_.dev<unsigned int>("H.chg", (size_t)NS);
+            L.n_items = NS;
+            launch_hpss(L, st);
+            SDSP_HIP_CHECK(hipGetLastError());
+            d_P0 = L.p[0];
+            d_hpe = c_.dev<float>("H.e", totS);
+            d_hfmax = c_.dev<float>("H.fmax", totS);
+            launch_hpss_rows(d_P0, d_hpfx, d_hpfx, c_.up("H.rt", rt), rt.back(), NS, STRIDE2, 1025, d_hpe, d_hfmax, st);
+            SDSP_HIP_CHECK(hipGetLastError());
+            htr("HPSS");
+        }
+    }
+    // onsets: energy flux (frame FS, hop HOP; same framing as the STFT), spectral flux, HFC, HPSS, consensus
     uint64_t* d_src = c_.up("B.src2", bin.src_off);
     float* d_g = c_.up("B.gain2", bin.gain_h);
     uint64_t* d_nt = c_.up("B.ntrim", bin.n_trim);
@@ -1242,32 +1320,37 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     uint32_t* d_eon = c_.dev<uint32_t>("B.eon", std::max<uint64_t>(bo.total, 1));
     int* d_en = c_.dev<int>("B.en", (size_t)NR);
     launch_energy_onsets(d_erms, bo.d_fpfx, d_nt, HOP, sd_powf(10.0f, -20.0f / 20.0f), d_eon, bo.d_fpfx, d_en, NR, st);
-    uint32_t* d_fon = c_.dev<uint32_t>("B.fon", 2 * std::max<uint64_t>(bo.total, 1));
-    int* d_fn = c_.dev<int>("B.fn", 2 * (size_t)NR);
-    float* d_fscr = c_.dev<float>("B.fscr", 2 * std::max<uint64_t>(bo.total, 1));
+    const int kinds = hpss_on ? 3 : 2;  // spectral flux, HFC (+ HPSS)
+    uint32_t* d_fon = c_.dev<uint32_t>("B.fon", kinds * std::max<uint64_t>(bo.total, 1));
+    int* d_fn = c_.dev<int>("B.fn", kinds * (size_t)NR);
+    float* d_fscr = c_.dev<float>("B.fscr", kinds * std::max<uint64_t>(bo.total, 1));
     const float pct = cfg_.onset_threshold_percentile;
     if (pct >= 0.0f && pct <= 1.0f)
-        launch_flux_onsets(bo.SFO, bo.H, d_fscr, bo.d_fpfx, d_nt, HOP, pct, d_fon, bo.d_fpfx, d_fn, NR, st);
-    else  // detect_*_onsets return Err -> warn + empty lists (src/lib.rs:196-218)
-        SDSP_HIP_CHECK(hipMemsetAsync(d_fn, 0, 2 * (size_t)NR * sizeof(int), st));
+        launch_flux_onsets(bo.SFO, bo.H, hpss_on ? d_hpe : nullptr, d_fscr, bo.d_fpfx, d_nt, HOP, pct, d_fon, bo.d_fpfx,
+                           d_fn, NR, st);
+    else  // detect_*_onsets return Err -> warn + empty lists (src/lib.rs:196-236)
+        SDSP_HIP_CHECK(hipMemsetAsync(d_fn, 0, kinds * (size_t)NR * sizeof(int), st));
+    if (hpss_on && !d_hpe)  // no frames at all: empty HPSS lists
+        SDSP_HIP_CHECK(hipMemsetAsync(d_fn + 2 * NR, 0, (size_t)NR * sizeof(int), st));
+    const uint64_t lists = hpss_on ? 4 : 3;
     std::vector<int> has_mags((size_t)NR);
     std::vector<uint64_t> coff((size_t)NR);
     for (int i = 0; i < NR; i++) {
         has_mags[(size_t)i] = bo.fpfx[(size_t)i + 1] > bo.fpfx[(size_t)i];
-        coff[(size_t)i] = 3 * bo.fpfx[(size_t)i];
+        coff[(size_t)i] = lists * bo.fpfx[(size_t)i];
     }
     int* d_hm = c_.up("B.hasm", has_mags);
     uint64_t* d_coff = c_.up("B.coff", coff);
-    uint32_t* d_chosen = c_.dev<uint32_t>("B.chosen", 3 * std::max<uint64_t>(bo.total, 1));
+    uint32_t* d_chosen = c_.dev<uint32_t>("B.chosen", lists * std::max<uint64_t>(bo.total, 1));
     int* d_cn = c_.dev<int>("B.cn", (size_t)NR);
     bool cons_ok = cfg_.enable_onset_consensus && cfg_.onset_consensus_tolerance_ms > 0;
     for (int k = 0; k < 4; k++) cons_ok = cons_ok && !(cfg_.onset_consensus_weights[k] < 0.0f);
     const uint32_t tol = (uint32_t)sd_f2u64((float)cfg_.onset_consensus_tolerance_ms / 1000.0f * (float)sr_);
-    uint32_t* d_cscr = c_.dev<uint32_t>("B.cscr", 15 * std::max<uint64_t>(bo.total, 1));
+    uint32_t* d_cscr = c_.dev<uint32_t>("B.cscr", 5 * lists * std::max<uint64_t>(bo.total, 1));
     launch_consensus(d_eon, bo.d_fpfx, d_en, d_fon, bo.d_fpfx, d_fn, bo.total, NR, tol, cons_ok, d_hm, d_chosen, d_coff,
-                     d_cn, d_cscr, st);
+                     d_cn, d_cscr, st, hpss_on ? 1 : 0);
     SDSP_HIP_CHECK(hipGetLastError());
-    std::vector<TempoEst> best = c_.down(bo.est, (size_t)NR);
+    if (best.empty()) best = c_.down(bo.est, (size_t)NR);
     std::vector<int> en_h = c_.down(d_en, (size_t)NR);
     htr("B");
     tm.mark(3);
@@ -1294,6 +1377,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     float* d_fconf = c_.up("B.fconf", fconf);
     int* d_used = c_.up("B.used", used);
     // ---------------- C: escalation (multi_resolution.rs:205-901) ----------------
+    TempoEst* d_mr_all = nullptr;  // multi-res estimates of the escalated tracks (E order)
     if (mr_on && !E.empty()) {
         const int NE = (int)E.size();
         const int top_k = (int)std::max<uint64_t>(cfg_.tempogram_multi_res_top_k, 1);
@@ -1347,6 +1431,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         mp.sr = (int)sr_;
         mp.hop512 = 512;
         TempoEst* d_mr = c_.dev<TempoEst>("C.mr", (size_t)NE);
+        d_mr_all = d_mr;
         launch_multires(d_E, NE, o256.cand, d_n256, bo.cand, d_n512, o1024.cand, d_n1024, ein.cand_cap, bin.cand_cap,
                         ein.cand_cap, bo.est, bo.nov, bo.d_fpfx, mp, d_mr, d_used, d_fbpm, d_fconf, st);
         SDSP_HIP_CHECK(hipGetLastError());
@@ -1364,6 +1449,99 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     }
     std::vector<float> fbpm_h = c_.down(d_fbpm, (size_t)NR), fconf_h = c_.down(d_fconf, (size_t)NR);
     htr("C");
+    // ---------------- C': percussive tempogram fallback (src/lib.rs:582-683) ----------------
+    std::vector<std::vector<float>> perc_cands((size_t)NR);  // emitted candidates of tracks that took it
+    std::vector<uint8_t> perc_took((size_t)NR, 0);
+    if (perc_on) {
+        std::vector<int> Q;  // positions in R
+        for (int i = 0; i < NR; i++) {
+            const TempoEst& e = best[(size_t)i];
+            if (!e.ok) continue;
+            res[(size_t)idx[(size_t)R[(size_t)i]]].perc_used = 0;
+            if (e.ambiguous && e.trap_low) Q.push_back(i);
+        }
+        const int NQ = (int)Q.size();
+        if (NQ > 0 && d_P0) {
+            TempoPassIn pin;
+            pin.hop = HOP;
+            pin.samples = d_samples;
+            std::vector<uint64_t> qpfx(1, 0);
+            for (int i : Q) {
+                pin.src_off.push_back(bin.src_off[(size_t)i]);
+                pin.gain_h.push_back(bin.gain_h[(size_t)i]);
+                pin.n_trim.push_back(bin.n_trim[(size_t)i]);
+                qpfx.push_back(qpfx.back() + (bo.fpfx[(size_t)i + 1] - bo.fpfx[(size_t)i]));
+            }
+            pin.want_onsets = false;
+            pin.top_n = bin.top_n;
+            pin.cand_cap = bin.cand_cap;
+            pin.gate = 0;
+            if (hpss_on) {  // S holds every track: gather Q's rows (S == Q otherwise)
+                float* pq = c_.dev<float>("P.in", std::max<uint64_t>(qpfx.back(), 1) * STRIDE2);
+                float* pm = c_.dev<float>("P.inmax", std::max<uint64_t>(qpfx.back(), 1));
+                for (int k = 0; k < NQ; k++) {
+                    const uint64_t F = qpfx[(size_t)k + 1] - qpfx[(size_t)k], r0 = bo.fpfx[(size_t)Q[(size_t)k]];
+                    if (F == 0) continue;
+                    SDSP_HIP_CHECK(hipMemcpyAsync(pq + qpfx[(size_t)k] * STRIDE2, d_P0 + r0 * STRIDE2,
+                                                  F * STRIDE2 * sizeof(float), hipMemcpyDeviceToDevice, st));
+                    SDSP_HIP_CHECK(hipMemcpyAsync(pm + qpfx[(size_t)k], d_hfmax + r0, F * sizeof(float),
+                                                  hipMemcpyDeviceToDevice, st));
+                }
+                pin.mags_in = pq;
+                pin.fmax_in = pm;
+            } else {
+                pin.mags_in = d_P0;
+                pin.fmax_in = d_hfmax;
+            }
+            TempoPassOut po;
+            tempo_pass("P.", pin, po);
+            times_.features_ms += po.feat_ms;
+            times_.tempogram_ms += po.tempo_ms;
+            std::vector<TempoEst> pe = c_.down(po.est, (size_t)NQ);
+            std::vector<TempoEst> mr_h;
+            if (d_mr_all) mr_h = c_.down(d_mr_all, E.size());
+            std::vector<int> epos((size_t)NR, -1);
+            for (size_t k = 0; k < E.size(); k++) epos[(size_t)E[k]] = (int)k;
+            std::vector<float> pc_h;
+            if (cfg_.emit_tempogram_candidates) pc_h = c_.down(po.cand, (size_t)NQ * (size_t)pin.cand_cap * 4);
+            bool changed = false;
+            for (int k = 0; k < NQ; k++) {
+                const int i = Q[(size_t)k];
+                const TempoEst& p = pe[(size_t)k];
+                if (!p.ok) continue;  // "Percussive tempogram fallback failed" -> not used
+                const TempoEst& b = best[(size_t)i];
+                const float cb = fbpm_h[(size_t)i], cc = fconf_h[(size_t)i];
+                const int ca = (used[(size_t)i] && epos[(size_t)i] >= 0) ? mr_h[(size_t)epos[(size_t)i]].agree : b.agree;
+                const float rel = cb > 1e-6f ? sd_maxf(p.bpm / cb, cb / p.bpm) : 1.0f;
+                const bool fam = sd_absf(rel - 2.0f) < 0.05f || sd_absf(rel - 1.5f) < 0.05f ||
+                                 sd_absf(rel - (4.0f / 3.0f)) < 0.05f || sd_absf(rel - (3.0f / 2.0f)) < 0.05f ||
+                                 sd_absf(rel - (2.0f / 3.0f)) < 0.05f || sd_absf(rel - (3.0f / 4.0f)) < 0.05f;
+                const bool forbid = cb <= 180.0f && p.bpm > 180.0f;
+                const bool base_low_trap = b.trap_low || b.bpm < 95.0f;
+                const bool in_common = p.bpm >= 70.0f && p.bpm <= 180.0f;
+                const bool better = !forbid && fam && in_common &&
+                                    (p.conf >= cc + 0.04f || (base_low_trap && p.conf >= cc * 0.85f) ||
+                                     (p.agree > ca && p.conf >= cc * 0.92f));
+                if (!better) continue;
+                fbpm_h[(size_t)i] = p.bpm;
+                fconf_h[(size_t)i] = p.conf;
+                res[(size_t)idx[(size_t)R[(size_t)i]]].perc_used = 1;
+                perc_took[(size_t)i] = 1;
+                changed = true;
+                if (cfg_.emit_tempogram_candidates)
+                    perc_cands[(size_t)i].assign(pc_h.begin() + (long)((size_t)k * (size_t)pin.cand_cap * 4),
+                                                 pc_h.begin() + (long)((size_t)k * (size_t)pin.cand_cap * 4 +
+                                                                       (size_t)p.n_cands * 4));
+            }
+            if (changed) {
+                SDSP_HIP_CHECK(hipMemcpyAsync(d_fbpm, c_.keep_bytes(fbpm_h), (size_t)NR * sizeof(float),
+                                              hipMemcpyHostToDevice, st));
+                SDSP_HIP_CHECK(hipMemcpyAsync(d_fconf, c_.keep_bytes(fconf_h), (size_t)NR * sizeof(float),
+                                              hipMemcpyHostToDevice, st));
+            }
+        }
+        htr("C perc");
+    }
     tm.mark(4);
     // ---------------- D: beat grid ----------------
     std::vector<int> ident((size_t)NR);
@@ -1472,7 +1650,14 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
             r.downs.assign(downs_h.begin() + (long)od, downs_h.begin() + (long)(od + b.n_down));
             r.stability = b.stability;
         }
-        if (cfg_.emit_tempogram_candidates && best[(size_t)i].ok) {
+        if (cfg_.emit_tempogram_candidates && perc_took[(size_t)i]) {  // chosen_cands = p_cands (:661-664)
+            r.has_cands = true;
+            const std::vector<float>& pc = perc_cands[(size_t)i];
+            for (size_t k = 0; k + 4 <= pc.size(); k += 4) {
+                sdsp_tempo_candidate tc{pc[k], pc[k + 1], pc[k + 2], pc[k + 3], (uint8_t)(sd_absf(pc[k] - r.bpm) < 0.75f)};
+                r.cands.push_back(tc);
+            }
+        } else if (cfg_.emit_tempogram_candidates && best[(size_t)i].ok) {
             r.has_cands = true;
             int n = best[(size_t)i].n_cands;
             if (mr_on && r.mr_used == 1) n = std::min(n, (int)std::max<uint64_t>(cfg_.tempogram_multi_res_top_k, 1));
