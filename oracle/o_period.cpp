@@ -1058,3 +1058,42 @@ extern "C" int32_t sdsp_oracle_find_best(const float* bpm, const float* val, int
     return 1;
 }
 
+
+// ctypes entry point for the legacy-estimator unit tests (tests/test_oracle_legacy.py).
+// which: 0 autocorrelation candidates (autocorrelation.rs:90-216), 1 comb-filter candidates
+// (comb_filter.rs:96-215), 2 the estimate (mod.rs:196-404; g7 = guardrails or null), 3
+// merge_bpm_candidates (candidate_filter.rs:147-442) of in[0..n_ac) and in[n_ac..n_ac+n_comb).
+// Returns the number of entries written, or -(AnalysisError code).
+extern "C" int64_t sdsp_oracle_legacy(int32_t which, const uint64_t* on, uint64_t n, uint32_t sr, uint64_t hop,
+                                      float min_bpm, float max_bpm, float res, const float* in_bpm,
+                                      const float* in_conf, uint64_t n_ac, uint64_t n_comb, const float* g7,
+                                      float* out_bpm, float* out_conf, uint32_t* out_agree, uint64_t cap) {
+    using namespace orc;
+    std::vector<size_t> o(on, on + n);
+    std::vector<BpmEstimate> est;
+    try {
+        if (which == 0 || which == 1) {
+            auto c = which == 0 ? legacy_autocorr(o, sr, (size_t)hop, min_bpm, max_bpm)
+                                : legacy_comb(o, sr, min_bpm, max_bpm, res);
+            for (auto& x : c) est.push_back({x.bpm, x.confidence, 0});
+        } else if (which == 2) {
+            BpmEstimate e{};
+            Guardrails g{};
+            if (g7) g = {g7[0], g7[1], g7[2], g7[3], g7[4], g7[5], g7[6]};
+            if (estimate_bpm_legacy(o, sr, (size_t)hop, min_bpm, max_bpm, res, g7 ? &g : nullptr, &e)) est.push_back(e);
+        } else {
+            std::vector<BpmCandidate> a, c;
+            for (uint64_t i = 0; i < n_ac; i++) a.push_back({in_bpm[i], in_conf[i]});
+            for (uint64_t i = 0; i < n_comb; i++) c.push_back({in_bpm[n_ac + i], in_conf[n_ac + i]});
+            est = merge_candidates(a, c, 50.0f);
+        }
+    } catch (const AErr& e) {
+        return -(int64_t)e.code;
+    }
+    for (size_t i = 0; i < est.size() && i < cap; i++) {
+        out_bpm[i] = est[i].bpm;
+        out_conf[i] = est[i].confidence;
+        out_agree[i] = est[i].method_agreement;
+    }
+    return (int64_t)est.size();
+}

@@ -65,6 +65,10 @@ def lib():
         L.sdsp_oracle_tuning.restype = C.c_float
         L.sdsp_oracle_key_hpss.argtypes = [fp, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64,
                                            C.c_uint64, C.c_float]
+        L.sdsp_oracle_legacy.argtypes = [C.c_int32, C.POINTER(C.c_uint64), C.c_uint64, C.c_uint32, C.c_uint64,
+                                          C.c_float, C.c_float, C.c_float, fp, fp, C.c_uint64, C.c_uint64, fp, fp, fp,
+                                          C.POINTER(C.c_uint32), C.c_uint64]
+        L.sdsp_oracle_legacy.restype = C.c_int64
         L.sdsp_oracle_hpss.argtypes = [fp, C.c_uint64, C.c_uint64, C.c_uint64, fp, fp]
         L.sdsp_oracle_hpss.restype = C.c_int32
         L.sdsp_oracle_hpss_onsets.argtypes = [fp, C.c_uint64, C.c_uint64, C.c_float, C.POINTER(C.c_uint64),
@@ -197,6 +201,29 @@ def key_hpss(spec, sample_rate=44100, fft_size=8192, step=4, time_margin=8, freq
     lib().sdsp_oracle_key_hpss(_fp(s), s.shape[0], s.shape[1], sample_rate, fft_size, step, time_margin, freq_margin,
                                C.c_float(power))
     return s
+
+
+def legacy(which, onsets=(), sample_rate=44100, hop=512, min_bpm=40.0, max_bpm=240.0, res=1.0, guardrails=None,
+           autocorr=(), comb=()):
+    """Legacy BPM estimator pieces (src/features/period): which = "autocorr" | "comb" | "estimate" |
+    "merge".  Returns a list of (bpm, confidence, method_agreement), or -(AnalysisError code)."""
+    w = {"autocorr": 0, "comb": 1, "estimate": 2, "merge": 3}[which]
+    on = np.ascontiguousarray(onsets, dtype=np.uint64)
+    cands = list(autocorr) + list(comb)
+    ib = np.ascontiguousarray([c[0] for c in cands] or [0.0], dtype=np.float32)
+    ic = np.ascontiguousarray([c[1] for c in cands] or [0.0], dtype=np.float32)
+    g = None if guardrails is None else np.ascontiguousarray(guardrails, dtype=np.float32)
+    cap = 8192
+    ob = np.zeros(cap, np.float32)
+    oc = np.zeros(cap, np.float32)
+    oa = np.zeros(cap, np.uint32)
+    n = lib().sdsp_oracle_legacy(w, on.ctypes.data_as(C.POINTER(C.c_uint64)), on.size, sample_rate, hop,
+                                 C.c_float(min_bpm), C.c_float(max_bpm), C.c_float(res), _fp(ib), _fp(ic),
+                                 len(autocorr), len(comb), _fp(g) if g is not None else None, _fp(ob), _fp(oc),
+                                 oa.ctypes.data_as(C.POINTER(C.c_uint32)), cap)
+    if n < 0:
+        return int(n)
+    return [(float(ob[i]), float(oc[i]), int(oa[i])) for i in range(min(n, cap))]
 
 
 def hpss(spec, margin):
