@@ -178,6 +178,20 @@ struct HpssLaunch {
 };
 constexpr int HPSS_HM_FRAMES = 256, HPSS_VM_FRAMES = 32, HPSS_COLS = 256, HPSS_ROW_FRAMES = 256;
 
+// ---- k_legacy (estimate_bpm_with_guardrails / estimate_bpm, period/mod.rs:196-404) ----
+struct LegacyParams {
+    int sr, hop;
+    float min_bpm, max_bpm, res;
+    int guard;   // enable_legacy_bpm_guardrails
+    float g[7];  // clamp_sane'd guardrails: preferred min/max, soft min/max, mul preferred/soft/extreme
+};
+struct LegacyOut {
+    int ok;  // 1 estimate, 0 none, -1 "Signal too short for autocorrelation", -2 scratch too small
+    float bpm, conf;
+    int agree;
+};
+constexpr int LG_COMB_MAX = 2048, LG_AC_MAX = 512;  // comb candidates; autocorrelation peaks
+
 // ---- launchers ----
 void launch_stft(int nfft, bool frame_max, const float* samples, const uint64_t* frame_pfx, int n_tracks,
                  uint64_t total_frames, const uint64_t* src_off, const float* gain, int hop, const float* window,
@@ -251,6 +265,9 @@ void launch_key_hpss(float* mags, const uint64_t* frame_pfx, const uint64_t* mti
                      const uint64_t* atile_pfx, uint64_t n_atiles, const uint64_t* mask_off, const int* tracks,
                      int n_items, const KeyHpssParams& P, float* mask, hipStream_t st);
 void launch_hpss(const HpssLaunch& L, hipStream_t st);
+void launch_legacy(const uint32_t* onsets, const uint64_t* on_off, const int* on_n, int n_items, const uint64_t* scr_off,
+                   const uint64_t* scr_cap, cx* scratch, const cx* tw, int tw_M, const LegacyParams& P, LegacyOut* out,
+                   hipStream_t st);
 void launch_hpss_rows(const float* p, const uint64_t* row0, const uint64_t* fpfx, const uint64_t* tile_pfx,
                       uint64_t n_tiles, int n_items, int stride, int B, float* energy, float* fmax, hipStream_t st);
 void launch_beat_sync(const int* tracks, int n_items, const uint64_t* frame_pfx, const float* fchroma,

@@ -515,15 +515,24 @@ struct TrackRes {
 };
 
 // Configuration support (everything the default path and its numeric knobs need).
-std::string unsupported(const sdsp_config& c) {
+std::string unsupported(const sdsp_config& c, uint32_t sr) {
     if (c.enable_normalization && c.normalization != SDSP_NORM_PEAK && c.normalization != SDSP_NORM_RMS &&
         c.normalization != SDSP_NORM_LOUDNESS)
         return "unknown normalization method";
     if (c.frame_size != 2048) return "frame_size other than 2048";
     if (c.hop_size == 0 || c.hop_size > 8192) return "hop_size outside 1..8192";
     if ((c.enable_hpss_onsets || c.enable_tempogram_percussive_fallback) && c.hpss_margin > 16) return "hpss_margin > 16";
-    if (c.force_legacy_bpm || c.enable_bpm_fusion) return "legacy-BPM output paths (force_legacy_bpm / enable_bpm_fusion)";
     if (!(c.min_bpm > 0.0f && c.max_bpm > c.min_bpm && c.bpm_resolution > 0.0f)) return "BPM range/resolution";
+    if (c.force_legacy_bpm || c.enable_bpm_fusion) {  // k_legacy's fixed LDS lists
+        int nc = 0;
+        for (float b = c.min_bpm; b <= c.max_bpm + EPS && nc <= LG_COMB_MAX; b += c.bpm_resolution) nc++;
+        if (nc > LG_COMB_MAX) return "legacy BPM: more than 2048 comb-filter candidates";
+        const uint64_t hop = c.hop_size ? c.hop_size : 1;
+        const float lmin = std::ceil((60.0f * (float)sr) / (c.max_bpm * (float)hop));
+        const float lmax = std::floor((60.0f * (float)sr) / (c.min_bpm * (float)hop));
+        if (lmax - lmin > (float)(2 * LG_AC_MAX - 4)) return "legacy BPM: autocorrelation lag range above 1020";
+        if ((60.0f * (float)sr) / c.max_bpm < 1.0f) return "legacy BPM: period below one sample";
+    }
     if (c.tempogram_superflux_max_filter_bins > (uint64_t)FT_KMAX) return "superflux_max_filter_bins > 8";
     if (c.enable_tempogram_mel_novelty && std::max<uint64_t>(c.tempogram_mel_n_mels, 4) > (uint64_t)FT_MELMAX)
         return "tempogram_mel_n_mels > 48";
@@ -603,13 +612,16 @@ class Pipeline {
     void sub_batch(const float* d_samples, const std::vector<uint64_t>& in_off, const std::vector<uint64_t>& n_raw,
                    const std::vector<int>& idx, std::vector<TrackRes>& res);
     void tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPassOut& out);
+    void legacy_select(const TempoPassIn& bin, const uint32_t* d_onsets, const uint64_t* d_on_off, const int* d_on_n,
+                       const std::vector<int>& R, const std::vector<int>& idx, std::vector<TrackRes>& res,
+                       std::vector<float>& fbpm_h, std::vector<float>& fconf_h, float* d_fbpm, float* d_fconf);
 };
 
 void Pipeline::run(const float* d_samples, const std::vector<uint64_t>& in_off, const std::vector<uint64_t>& n_raw,
                    std::vector<TrackRes>& res) {
     const size_t T = n_raw.size();
     res.assign(T, TrackRes{});
-    std::string why = unsupported(cfg_);
+    std::string why = unsupported(cfg_, sr_);
     if (why.empty()) why = unsupported_sr(cfg_, sr_);
     for (size_t i = 0; i < T; i++) {
         if (n_raw[i] == 0) {
@@ -717,6 +729,96 @@ void Pipeline::loudness_prepass(const float* d_samples, const std::vector<uint64
         loud_gain_[at[(size_t)k]] = g[(size_t)k];
         loud_stat_[at[(size_t)k]] = st[(size_t)k];
     }
+}
+
+// The legacy estimate of every track from its beat-tracking onsets (on_legacy == on_beat,
+// src/lib.rs:176-291), then force_legacy_bpm / enable_bpm_fusion's choice (src/lib.rs:814-892).
+// ACF scratch: M = next_pow2(2L) complex per buffer, L <= (n_trim - 1) / hop + 1.
+void Pipeline::legacy_select(const TempoPassIn& bin, const uint32_t* d_onsets, const uint64_t* d_on_off,
+                             const int* d_on_n, const std::vector<int>& R, const std::vector<int>& idx,
+                             std::vector<TrackRes>& res, std::vector<float>& fbpm_h, std::vector<float>& fconf_h,
+                             float* d_fbpm, float* d_fconf) {
+    hipStream_t st = d_.stream;
+    const int NR = (int)R.size();
+    const uint64_t hop = (uint64_t)bin.hop;
+    std::vector<uint64_t> soff((size_t)NR), scap((size_t)NR);
+    uint64_t tot = 0, mmax = 4;
+    for (int i = 0; i < NR; i++) {
+        const uint64_t n = bin.n_trim[(size_t)i];
+        const uint64_t L = (n ? n - 1 : 0) / hop + 1;
+        uint64_t M = 1;
+        while (M < 2 * L) M <<= 1;
+        scap[(size_t)i] = M;
+        soff[(size_t)i] = tot;
+        tot += 2 * M;
+        mmax = std::max(mmax, M);
+    }
+    LegacyParams P{};
+    P.sr = (int)sr_;
+    P.hop = (int)hop;
+    P.min_bpm = cfg_.min_bpm;
+    P.max_bpm = cfg_.max_bpm;
+    P.res = cfg_.bpm_resolution;
+    P.guard = cfg_.enable_legacy_bpm_guardrails ? 1 : 0;
+    {  // LegacyBpmGuardrails::clamp_sane (period/mod.rs:88-121)
+        const float pmn = cfg_.legacy_bpm_preferred_min, pmx = cfg_.legacy_bpm_preferred_max;
+        const float smn = cfg_.legacy_bpm_soft_min, smx = cfg_.legacy_bpm_soft_max;
+        P.g[0] = sd_minf(pmn, pmx);
+        P.g[1] = sd_maxf(pmn, pmx);
+        P.g[2] = sd_minf(sd_minf(smn, smx), P.g[0]);
+        P.g[3] = sd_maxf(sd_maxf(smn, smx), P.g[1]);
+        const float mul[3] = {cfg_.legacy_bpm_conf_mul_preferred, cfg_.legacy_bpm_conf_mul_soft,
+                              cfg_.legacy_bpm_conf_mul_extreme};
+        for (int k = 0; k < 3; k++) P.g[4 + k] = sd_isfinite_f(mul[k]) ? sd_maxf(mul[k], 0.0f) : 0.0f;
+    }
+    FftTables& tb = d_.tables((int)(2 * mmax), false);
+    cx* scr = c_.dev<cx>("G.acf", tot);
+    LegacyOut* d_lo = c_.dev<LegacyOut>("G.out", (size_t)NR);
+    launch_legacy(d_onsets, d_on_off, d_on_n, NR, c_.up("G.soff", soff), c_.up("G.scap", scap), scr, tb.tw.as<cx>(),
+                  (int)mmax, P, d_lo, st);
+    SDSP_HIP_CHECK(hipGetLastError());
+    const std::vector<LegacyOut> lo = c_.down(d_lo, (size_t)NR);
+    for (int i = 0; i < NR; i++) {
+        TrackRes& r = res[(size_t)idx[(size_t)R[(size_t)i]]];
+        const LegacyOut& l = lo[(size_t)i];
+        if (l.ok < 0) {  // estimate_bpm_with_guardrails(...)? propagates (src/lib.rs:315, 324)
+            r.status = SDSP_ERR_PROCESSING;
+            r.err = l.ok == -1 ? "Processing error: Signal too short for autocorrelation"
+                               : "Processing error: legacy BPM scratch too small";
+            continue;
+        }
+        const bool has = l.ok > 0;
+        float& bpm = fbpm_h[(size_t)i];
+        float& conf = fconf_h[(size_t)i];
+        if (cfg_.force_legacy_bpm) {
+            bpm = has ? l.bpm : 0.0f;
+            conf = has ? l.conf : 0.0f;
+            continue;
+        }
+        // fusion: the tempogram BPM is kept; legacy only moves its confidence
+        const float t_bpm = bpm, t_conf = conf;
+        const float l_bpm = has ? l.bpm : 0.0f;
+        const float l_conf = sd_clampf(has ? l.conf : 0.0f, 0.0f, 1.0f);
+        if (t_bpm <= 0.0f) {
+            bpm = has ? l.bpm : 0.0f;
+            conf = has ? l.conf : 0.0f;
+            continue;
+        }
+        float c = sd_clampf(t_conf, 0.0f, 1.0f);
+        bool agree = false;
+        if (l_bpm > 0.0f) {
+            const float d[5] = {sd_absf(l_bpm - t_bpm), sd_absf(l_bpm - (t_bpm * 0.5f)), sd_absf(l_bpm - (t_bpm * 2.0f)),
+                                sd_absf(l_bpm - (t_bpm * (2.0f / 3.0f))), sd_absf(l_bpm - (t_bpm * (3.0f / 2.0f)))};
+            for (float v : d) agree |= v <= 2.0f;
+        }
+        if (agree)
+            c = sd_clampf(c + 0.12f * l_conf, 0.0f, 1.0f);
+        else if (l_bpm > 0.0f)
+            c = sd_clampf(c * 0.90f, 0.0f, 1.0f);
+        conf = c;
+    }
+    SDSP_HIP_CHECK(hipMemcpyAsync(d_fbpm, c_.keep_bytes(fbpm_h), (size_t)NR * sizeof(float), hipMemcpyHostToDevice, st));
+    SDSP_HIP_CHECK(hipMemcpyAsync(d_fconf, c_.keep_bytes(fconf_h), (size_t)NR * sizeof(float), hipMemcpyHostToDevice, st));
 }
 
 void Pipeline::tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPassOut& o) {
@@ -1042,7 +1144,10 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     const int NR = (int)R.size();
     if (NR == 0) return;
     // ---------------- B: base tempo pass (hop = config hop) + onsets ----------------
-    const bool mr_on = cfg_.enable_tempogram_multi_resolution;
+    // force_legacy_bpm skips the tempogram estimate (src/lib.rs:337): no escalation, no
+    // candidates, the flags stay None; the hop-512 pass still feeds the onset detectors
+    const bool tg_on = !cfg_.force_legacy_bpm;
+    const bool mr_on = cfg_.enable_tempogram_multi_resolution && tg_on;
     const int base_top_n =
         (int)std::max<uint64_t>(std::max<uint64_t>(cfg_.tempogram_candidates_top_n, cfg_.tempogram_multi_res_top_k), 10);
     TempoPassIn bin;
@@ -1363,7 +1468,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         TrackRes& r = res[(size_t)idx[(size_t)R[(size_t)i]]];
         const TempoEst& e = best[(size_t)i];
         r.onset_consensus = en_h[(size_t)i] > 0 ? 1.0f : 0.0f;
-        if (!e.ok) continue;
+        if (!e.ok || !tg_on) continue;
         fbpm[(size_t)i] = e.bpm;
         fconf[(size_t)i] = e.conf;
         if (mr_on) {
@@ -1542,6 +1647,9 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         }
         htr("C perc");
     }
+    // ---------------- C'': legacy estimator (src/lib.rs:294-329) and the BPM choice (:814-900) ------
+    if (cfg_.force_legacy_bpm || cfg_.enable_bpm_fusion)
+        legacy_select(bin, d_chosen, d_coff, d_cn, R, idx, res, fbpm_h, fconf_h, d_fbpm, d_fconf);
     tm.mark(4);
     // ---------------- D: beat grid ----------------
     std::vector<int> ident((size_t)NR);
@@ -1636,6 +1744,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     times_.beat_ms += tm.ms(4, 5);
     for (int i = 0; i < NR; i++) {
         TrackRes& r = res[(size_t)idx[(size_t)R[(size_t)i]]];
+        if (r.status != SDSP_OK) continue;  // a legacy-estimator error propagated
         r.bpm = fbpm_h[(size_t)i];
         r.bpm_conf = fconf_h[(size_t)i];
         const BeatOut& b = bout[(size_t)i];
@@ -1657,7 +1766,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
                 sdsp_tempo_candidate tc{pc[k], pc[k + 1], pc[k + 2], pc[k + 3], (uint8_t)(sd_absf(pc[k] - r.bpm) < 0.75f)};
                 r.cands.push_back(tc);
             }
-        } else if (cfg_.emit_tempogram_candidates && best[(size_t)i].ok) {
+        } else if (cfg_.emit_tempogram_candidates && best[(size_t)i].ok && tg_on) {
             r.has_cands = true;
             int n = best[(size_t)i].n_cands;
             if (mr_on && r.mr_used == 1) n = std::min(n, (int)std::max<uint64_t>(cfg_.tempogram_multi_res_top_k, 1));
