@@ -1,9 +1,8 @@
 // o_analyze.cpp — analyze_audio orchestration + the oracle's C API (TEST INFRASTRUCTURE).
 //
 // Follows src/lib.rs:86-1635 with AnalysisConfig::default() (src/config.rs:594-744) and the opt-in
-// branches restated so far (normalisation methods, key scoring options, chroma front-ends).
-// Branches not restated yet (HPSS onsets / percussive fallback / key HPSS, the legacy-BPM output
-// paths) raise NotImplemented here, as they do in the engine.
+// branches (normalisation methods, HPSS onsets and the percussive fallback, the legacy-BPM output
+// paths, key scoring options, chroma front-ends).  Only degenerate sizes raise NotImplemented.
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
