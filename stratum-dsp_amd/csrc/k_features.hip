@@ -31,8 +31,7 @@ namespace sdsp {
 // the chunk's windows are read once into registers and every bin's window max is taken from
 // them; KK = 0: runtime P.K with the per-bin window loop.
 template <int CW, int W, int KK>
-__global__ __launch_bounds__(FT_FRAMES) void k_features(const float* __restrict__ mags,
-                                                        const float* __restrict__ fmax,
+__global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
                                                         const uint64_t* __restrict__ frame_pfx,
                                                         const uint64_t* __restrict__ tile_pfx, int T, FeatParams P,
                                                         const MelPlan* __restrict__ mel, float* __restrict__ E,
@@ -63,29 +62,47 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const float* __restrict_
     float e[4] = {0, 0, 0, 0}, h[4] = {0, 0, 0, 0}, sx[4] = {0, 0, 0, 0}, so = 0.0f;
     float accA = 0.0f, accB = 0.0f;
     int mA = 0;
-    const float mx_c = valid ? fmax[g] : 0.0f;
-    const float mx_p = has_prev ? fmax[g - 1] : 0.0f;
+    // frame f of this track lives in row (f even ? A : B) r0 + (f >> 1) * step (RowMap)
+    const uint64_t ra0 = rm.rowA0[trk], rb0 = rm.rowB0 ? rm.rowB0[trk] : ra0 + (uint64_t)rm.offB;
+    auto row_of = [&](int64_t fr, bool* odd) {
+        *odd = fr & 1;
+        return (*odd ? rb0 + (uint64_t)(fr >> 1) * (uint64_t)rm.stepB : ra0 + (uint64_t)(fr >> 1) * (uint64_t)rm.stepA);
+    };
+    auto fmax_of = [&](int64_t fr) {
+        bool odd;
+        const uint64_t r = row_of(fr, &odd);
+        return odd ? rm.fmaxB[r] : rm.fmaxA[r];
+    };
+    const float mx_c = valid ? fmax_of(f) : 0.0f;
+    const float mx_p = has_prev ? fmax_of(f - 1) : 0.0f;
     const bool cn = mx_c > EPS, pn = mx_p > EPS;
 
     // rows f0-1 .. f0+FT_FRAMES-1 of the track; row r <-> frame f0-1+r
     const int64_t r_lo = f0 >= 1 ? 0 : 1;
     const int64_t r_hi = F - f0 + 1 < ROWS ? F - f0 + 1 : ROWS;  // rows [r_lo, r_hi) exist
-    const float* base = mags + (g0 + (uint64_t)f0) * (uint64_t)P.stride;  // row r at base + (r-1)*stride
     const int sub = i / CW, jj = i % CW;
 
     // stage bins [b0, b0+CW) (columns beyond B or rows outside the track read as 0), in two
     // halves so the loads of the next step are in flight while the current step is walked
     constexpr int RSTEP = FT_FRAMES / CW;
     constexpr int NLD = (ROWS + RSTEP - 1) / RSTEP;
+    const float* rowp[NLD];  // this thread's staged rows
+#pragma unroll
+    for (int u = 0; u < NLD; u++) {
+        const int r = sub + u * RSTEP;
+        rowp[u] = nullptr;
+        if (r >= r_lo && r < r_hi) {
+            bool odd;
+            const uint64_t row = row_of(f0 - 1 + r, &odd);
+            rowp[u] = (odd ? rm.magsB : rm.magsA) + row * (uint64_t)P.stride;
+        }
+    }
     float nx[NLD];
     auto load = [&](int b0) {
         const int b = b0 + jj;
         const bool col_ok = b < B;
 #pragma unroll
-        for (int u = 0; u < NLD; u++) {
-            const int r = sub + u * RSTEP;
-            nx[u] = (col_ok && r >= r_lo && r < r_hi) ? base[(int64_t)(r - 1) * P.stride + b] : 0.0f;
-        }
+        for (int u = 0; u < NLD; u++) nx[u] = (col_ok && rowp[u]) ? rowp[u][b] : 0.0f;
     };
     auto commit = [&](int b0) {
         const int slot = (b0 + jj) & (W - 1);
@@ -220,19 +237,19 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const float* __restrict_
     }
 }
 
-void launch_features(const float* mags, const float* fmax, const uint64_t* frame_pfx, const uint64_t* tile_pfx,
+void launch_features(const RowMap& mags, const uint64_t* frame_pfx, const uint64_t* tile_pfx,
                      int T, uint64_t n_tiles, const FeatParams& P, const MelPlan* mel, float* E, float* H, float* SFX,
                      float* SFO, float* MEL, uint64_t total, hipStream_t st) {
     if (n_tiles == 0) return;
     // window must hold [c0-K, c0+CW+K): CW + 2K <= W
     if (P.K == 4)
-        hipLaunchKernelGGL((k_features<8, 16, 4>), dim3((unsigned)n_tiles), dim3(FT_FRAMES), 0, st, mags, fmax,
+        hipLaunchKernelGGL((k_features<8, 16, 4>), dim3((unsigned)n_tiles), dim3(FT_FRAMES), 0, st, mags,
                            frame_pfx, tile_pfx, T, P, mel, E, H, SFX, SFO, MEL, total);
     else if (P.K <= 4)
-        hipLaunchKernelGGL((k_features<8, 16, 0>), dim3((unsigned)n_tiles), dim3(FT_FRAMES), 0, st, mags, fmax,
+        hipLaunchKernelGGL((k_features<8, 16, 0>), dim3((unsigned)n_tiles), dim3(FT_FRAMES), 0, st, mags,
                            frame_pfx, tile_pfx, T, P, mel, E, H, SFX, SFO, MEL, total);
     else
-        hipLaunchKernelGGL((k_features<16, 32, 0>), dim3((unsigned)n_tiles), dim3(FT_FRAMES), 0, st, mags, fmax,
+        hipLaunchKernelGGL((k_features<16, 32, 0>), dim3((unsigned)n_tiles), dim3(FT_FRAMES), 0, st, mags,
                            frame_pfx, tile_pfx, T, P, mel, E, H, SFX, SFO, MEL, total);
 }
 

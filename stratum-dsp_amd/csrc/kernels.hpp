@@ -30,6 +30,15 @@ struct MelPlan {
 };
 constexpr int PK_CH = 16384;  // samples per k_peak_abs workgroup
 constexpr int FT_FRAMES = 256;
+// Where k_features finds frame f of item k: row (f even ? A : B) r0 + (f >> 1) * step, with
+// rB0 = rowB0[k] or rowA0[k] + offB.  Compact spectrogram: A = B, rowA0 = frame prefix, offB = 1,
+// steps 2.  The escalation hops reuse the hop-512 rows: hop 1024 frame v is hop-512 frame 2v;
+// hop 256 frame 2u is hop-512 frame u (the odd hop-256 frames are computed on their own).
+struct RowMap {
+    const float *magsA, *magsB, *fmaxA, *fmaxB;
+    const uint64_t *rowA0, *rowB0;
+    int offB, stepA, stepB;
+};
 constexpr int FT_KMAX = 8;
 constexpr int FT_MELMAX = 48;
 
@@ -226,7 +235,7 @@ void launch_consensus(const uint32_t* energy, const uint64_t* e_off, const int* 
                       const uint64_t* f_off, const int* f_n, uint64_t kind_stride, int T, uint32_t tol, int enable,
                       const int* has_mags, uint32_t* chosen, const uint64_t* c_off, int* c_n, uint32_t* scratch,
                       hipStream_t st, int hpss = 0);
-void launch_features(const float* mags, const float* fmax, const uint64_t* frame_pfx, const uint64_t* tile_pfx,
+void launch_features(const RowMap& mags, const uint64_t* frame_pfx, const uint64_t* tile_pfx,
                      int T, uint64_t n_tiles, const FeatParams& P, const MelPlan* mel, float* E, float* H, float* SFX,
                      float* SFO, float* MEL, uint64_t total, hipStream_t st);
 void launch_novelty(const float* E, const float* H, const float* SFX, const uint64_t* frame_pfx, int T, uint64_t total,

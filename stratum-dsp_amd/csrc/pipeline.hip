@@ -569,6 +569,12 @@ struct TempoPassIn {
     // maxima: the STFT is skipped (the percussive tempogram fallback runs on the HPSS output)
     const float* mags_in = nullptr;
     const float* fmax_in = nullptr;
+    // escalation hops over the hop-512 spectrogram (rows base_row0[t] + frame): 1 = hop 1024, every
+    // frame is a hop-512 row (2v); 2 = hop 256, even frames are hop-512 rows, odd ones are computed
+    int reuse = 0;
+    const float* base_mags = nullptr;
+    const float* base_fmax = nullptr;
+    std::vector<uint64_t> base_row0;
 };
 struct TempoPassOut {
     std::vector<uint64_t> fpfx;  // frame prefix over the pass's tracks
@@ -847,22 +853,46 @@ void Pipeline::tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPa
     Timers tm;
     tm.init(d_);
     tm.mark(0);
+    RowMap rm{};
+    uint64_t stft_frames = 0;
     if (in.mags_in) {
         o.mags = const_cast<float*>(in.mags_in);
         o.fmax = const_cast<float*>(in.fmax_in);
+    } else if (in.reuse == 1) {  // hop 1024: nothing to compute
+        o.mags = nullptr;
+        o.fmax = nullptr;
+        rm = RowMap{in.base_mags, in.base_mags, in.base_fmax, in.base_fmax, c_.up(tag + "brow", in.base_row0), nullptr,
+                    2, 4, 4};
+    } else if (in.reuse == 2) {  // hop 256: the odd frames, as a hop-512 STFT from sample 256
+        std::vector<uint64_t> opfx((size_t)P_T + 1, 0), osrc((size_t)P_T);
+        for (int t = 0; t < P_T; t++) {
+            opfx[(size_t)t + 1] = opfx[(size_t)t] + (o.fpfx[(size_t)t + 1] - o.fpfx[(size_t)t]) / 2;
+            osrc[(size_t)t] = in.src_off[(size_t)t] + (uint64_t)hop;
+        }
+        stft_frames = opfx[(size_t)P_T];
+        o.mags = c_.dev<float>(tag + "mags", std::max<uint64_t>(stft_frames, 1) * STRIDE2);
+        o.fmax = c_.dev<float>(tag + "fmax", std::max<uint64_t>(stft_frames, 1));
+        uint64_t* d_opfx = c_.up(tag + "opfx", opfx);
+        launch_stft(FS, true, in.samples, d_opfx, P_T, stft_frames, c_.up(tag + "osrc", osrc), d_gain, 2 * hop,
+                    tb.window.as<float>(), tb.stft_tw.as<cx>(), tb.stft_rt.as<cx>(), o.mags, d_opfx, STRIDE2, o.fmax,
+                    d_.stream);
+        SDSP_HIP_CHECK(hipGetLastError());
+        rm = RowMap{in.base_mags, o.mags, in.base_fmax, o.fmax, c_.up(tag + "brow", in.base_row0), d_opfx, 0, 1, 1};
     } else {
         o.mags = c_.dev<float>(tag + "mags", total * STRIDE2);
         o.fmax = c_.dev<float>(tag + "fmax", total);
         launch_stft(FS, true, in.samples, o.d_fpfx, P_T, total, d_src, d_gain, hop, tb.window.as<float>(),
                     tb.stft_tw.as<cx>(), tb.stft_rt.as<cx>(), o.mags, o.d_fpfx, STRIDE2, o.fmax, d_.stream);
         SDSP_HIP_CHECK(hipGetLastError());
+        stft_frames = total;
     }
+    if (in.mags_in || in.reuse == 0) rm = RowMap{o.mags, o.mags, o.fmax, o.fmax, o.d_fpfx, nullptr, 1, 2, 2};
     tm.mark(1);
-    o.stft_launch = (total && !in.mags_in) ? 1 : 0;
-    if (!in.mags_in) {
+    o.stft_launch = stft_frames ? 1 : 0;
+    if (stft_frames) {
         double inb = 0;
         for (int t = 0; t < P_T; t++) inb += 4.0 * (double)in.n_trim[(size_t)t];
-        o.stft_bytes = inb + 4.0 * (double)total * 1025.0;
+        o.stft_bytes = inb + 4.0 * (double)stft_frames * 1025.0;
     }
     // features
     const int B = 1025;
@@ -904,7 +934,7 @@ void Pipeline::tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPa
     o.SFX = c_.dev<float>(tag + "SFX", 4 * total);
     o.SFO = c_.dev<float>(tag + "SFO", total);
     o.MEL = c_.dev<float>(tag + "MEL", std::max<uint64_t>(total * (uint64_t)std::max(fp.n_mels, 1), 1));
-    launch_features(o.mags, o.fmax, o.d_fpfx, d_tpfx, P_T, tpfx[(size_t)P_T], fp, d_mplan, o.E, o.H, o.SFX, o.SFO,
+    launch_features(rm, o.d_fpfx, d_tpfx, P_T, tpfx[(size_t)P_T], fp, d_mplan, o.E, o.H, o.SFX, o.SFO,
                     o.MEL, total, d_.stream);
     SDSP_HIP_CHECK(hipGetLastError());
     // novelty
@@ -1495,13 +1525,20 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
             ein.n_trim.push_back(bin.n_trim[(size_t)i]);
         }
         ein.want_onsets = false;
+        ein.base_mags = bo.mags;
+        ein.base_fmax = bo.fmax;
+        for (int i : E) ein.base_row0.push_back(bo.fpfx[(size_t)i]);
         ein.top_n = aux_k;
         ein.cand_cap = aux_k;
         ein.gate = 0;
         TempoPassOut o256, o1024;
+        // multi-resolution runs only at hop 512 (unsupported()); SDSP_NO_ROW_REUSE: A/B switch
+        static const bool reuse_on = std::getenv("SDSP_NO_ROW_REUSE") == nullptr;
         ein.hop = 256;
+        ein.reuse = (HOP == 512 && reuse_on) ? 2 : 0;
         tempo_pass("C256.", ein, o256);
         ein.hop = 1024;
+        ein.reuse = (HOP == 512 && reuse_on) ? 1 : 0;
         tempo_pass("C1024.", ein, o1024);
         for (TempoPassOut* o : {&o256, &o1024}) {
             times_.stft2048_ms += o->stft_ms;
