@@ -3,15 +3,16 @@
 // original magnitudes, stopped per track once no element moves by 1e-6.  It feeds the HPSS onsets
 // (src/lib.rs:222-236, hpss.rs:290-372) and the percussive tempogram fallback (src/lib.rs:587-683).
 //
-//   k_hpss_hmed     HF = time-median(H), one thread per (bin, chunk of HM_CH frames)
-//   k_hpss_vmed     PF = frequency-median(P) fused with the re-partition and the change maximum
+//   k_hpss_round    one round: frequency medians of P (LDS tile), time medians of H (registers),
+//                   the re-partition and the change maximum, per 32-frame x 256-bin tile
 //   k_hpss_conv     per-track convergence flags between rounds
 //   k_hpss_rows     per-frame sum of squares (bin order) and max of the final P
 //
 // Medians: each thread slides a window along its row/column and keeps it sorted in registers.
 // Inserting x into a sorted array b is c[j] = min(max(b[j-1], x), b[j]); deleting y (present) is
-// d[j] = c[j] < y ? c[j] : c[j+1] (+inf pads the tail, -inf the head).  Both are 2 ops per slot on
-// statically indexed registers.  The median of n values is s[n/2] for odd n and
+// d[j] = c[j] < y ? c[j] : c[j+1] (+inf pads the tail).  Both are 2 ops per slot on statically
+// indexed registers.  The leaving value is deleted before the entering one is inserted, so the
+// array never holds more than 2m + 1 <= W values.  The median of n values is s[n/2] for odd n and
 // (s[n/2-1] + s[n/2]) * 0.5 for even n (the reference's windows shrink at the edges).
 //
 // Buffers ping-pong: round `it` reads H[it%2], P[it%2] (round 0: the spectrogram itself) and
@@ -37,9 +38,13 @@ __device__ __forceinline__ void sw_delete(float (&a)[W], float y) {
     for (int j = 0; j < W - 1; j++) a[j] = a[j] < y ? a[j] : a[j + 1];
     a[W - 1] = __builtin_inff();
 }
-template <int W>
+// MM >= 0: the margin is the compile-time MM (the full-window median is register a[MM]);
+// MM < 0: runtime m (a select chain).
+template <int W, int MM>
 __device__ __forceinline__ float sw_median(const float (&a)[W], int n, int m) {
-    if (n == 2 * m + 1) {  // full window (static slot when W == 2m + 1)
+    if constexpr (MM >= 0) {
+        if (n == 2 * MM + 1) return a[MM];
+    } else if (n == 2 * m + 1) {
         float v = a[0];
 #pragma unroll
         for (int j = 0; j < W; j++)
@@ -60,88 +65,50 @@ __device__ __forceinline__ float sw_median(const float (&a)[W], int n, int m) {
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------
-// Horizontal median: lanes are adjacent bins (coalesced row segments), each thread walks HM_CH
-// frames of its bin.
-constexpr int HM_CH = 256;
-template <int W>
-__global__ __launch_bounds__(256) void k_hpss_hmed(const float* __restrict__ hin, const uint64_t* __restrict__ in_row0,
-                                                   float* __restrict__ hf, const uint64_t* __restrict__ out_row0,
-                                                   const uint64_t* __restrict__ fpfx, const uint64_t* __restrict__ tile_pfx,
-                                                   const int* __restrict__ last_it, int it, int n_items, HpssParams P) {
-    const uint64_t gb = blockIdx.x;
-    const int k = find_track(tile_pfx, n_items, gb);
-    if (last_it[k] < it) return;  // converged in an earlier round
-    const int64_t F = (int64_t)(fpfx[k + 1] - fpfx[k]);
-    const int nbb = (P.B + 255) / 256;
-    const int64_t lt = (int64_t)(gb - tile_pfx[k]);
-    const int64_t t0 = (lt / nbb) * HM_CH;
-    const int b = (int)(lt % nbb) * 256 + (int)threadIdx.x;
-    if (b >= P.B) return;
-    const int m = P.m;
-    const float* src = hin + in_row0[k] * (uint64_t)P.stride + b;
-    float* dst = hf + out_row0[k] * (uint64_t)P.stride + b;
-    float a[W];
-#pragma unroll
-    for (int j = 0; j < W; j++) a[j] = __builtin_inff();
-    const int64_t w0 = t0 >= m ? t0 - m : 0, w1 = t0 + m + 1 < F ? t0 + m + 1 : F;
-    for (int64_t t = w0; t < w1; t++) sw_insert<W>(a, src[(uint64_t)t * P.stride]);
-    int n = (int)(w1 - w0);
-    const int64_t t1 = t0 + HM_CH < F ? t0 + HM_CH : F;
-    for (int64_t t = t0; t < t1; t++) {
-        dst[(uint64_t)t * P.stride] = sw_median<W>(a, n, m);
-        // delete before insert: the window never holds more than 2m + 1 <= W values
-        const int64_t tin = t + m + 1, tout = t - m;
-        if (tout >= 0) {
-            sw_delete<W>(a, src[(uint64_t)tout * P.stride]);
-            n--;
-        }
-        if (tin < F) {
-            sw_insert<W>(a, src[(uint64_t)tin * P.stride]);
-            n++;
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
-// Vertical median + re-partition.  A workgroup owns VM_ROWS frames x VM_COLS bins: the P tile
-// with its +-m halo is staged in LDS, each thread slides a window along VM_SEG bins of one frame
-// (results in registers), the medians replace the tile centre, and a coalesced pass re-partitions
-// every element: total = h + p; H', P' = orig * h/total, orig * p/total (or orig * 0.5 each when
-// total <= 1e-10), and the round's change max(|H' - H|, |P' - P|) goes to the track's maximum.
-constexpr int VM_ROWS = 32, VM_SEG = 32, VM_COLS = 256, VM_MAXM = 16;
+// One round, fused.  A workgroup owns VM_ROWS frames x VM_COLS bins of one track:
+//  1. the P tile with its +-m bin halo is staged in LDS; thread (row, segment) slides the
+//     frequency median along VM_SEG bins of its row (results in registers);
+//  2. thread b slides the time median of bin b down the tile's rows, reading H straight from
+//     global memory (lanes are adjacent bins: coalesced rows; the +-m halo rows come from L2);
+//  3. the frequency medians replace the tile centre and thread b re-partitions its column:
+//     total = h + p; H', P' = orig * h/total, orig * p/total (or orig * 0.5 each when total <=
+//     1e-10), and the round's change max(|H' - H|, |P' - P|) goes to the track's maximum.
+// Per round the spectrogram-sized streams are H (+ halo), P, orig read and H', P' written.
+constexpr int VM_ROWS = HPSS_VM_FRAMES, VM_SEG = 32, VM_COLS = HPSS_COLS, VM_MAXM = 16;
 constexpr int VM_LD = VM_COLS + 2 * VM_MAXM + 1;
-template <int W>
-__global__ __launch_bounds__(256) void k_hpss_vmed(const float* __restrict__ orig, const uint64_t* __restrict__ o_row0,
-                                                   const float* __restrict__ hold, const float* __restrict__ pold,
-                                                   const uint64_t* __restrict__ in_row0, float* __restrict__ hnew,
-                                                   float* __restrict__ pnew, const uint64_t* __restrict__ out_row0,
-                                                   const uint64_t* __restrict__ fpfx, const uint64_t* __restrict__ tile_pfx,
-                                                   const int* __restrict__ last_it, int it, int n_items, HpssParams P,
-                                                   unsigned int* __restrict__ change) {
+static_assert(VM_ROWS * (VM_COLS / VM_SEG) == 256 && VM_COLS == 256, "thread maps of k_hpss_round");
+template <int W, int MM>
+__global__ __launch_bounds__(256) void k_hpss_round(const float* __restrict__ orig, const uint64_t* __restrict__ o_row0,
+                                                    const float* __restrict__ hin, const float* __restrict__ pin,
+                                                    const uint64_t* __restrict__ in_row0, float* __restrict__ hout,
+                                                    float* __restrict__ pout, const uint64_t* __restrict__ out_row0,
+                                                    const uint64_t* __restrict__ fpfx, const uint64_t* __restrict__ tile_pfx,
+                                                    const int* __restrict__ last_it, int it, int n_items, HpssParams P,
+                                                    unsigned int* __restrict__ change) {
     __shared__ float tl[VM_ROWS][VM_LD];
     __shared__ float red[4];
     const uint64_t gb = blockIdx.x;
     const int k = find_track(tile_pfx, n_items, gb);
-    if (last_it[k] < it) return;
+    if (last_it[k] < it) return;  // converged in an earlier round
     const int64_t F = (int64_t)(fpfx[k + 1] - fpfx[k]);
     const int ncb = (P.B + VM_COLS - 1) / VM_COLS;
     const int64_t lt = (int64_t)(gb - tile_pfx[k]);
     const int64_t r0 = (lt / ncb) * VM_ROWS;
     const int c0 = (int)(lt % ncb) * VM_COLS;
-    const int m = P.m, B = P.B;
+    const int m = MM >= 0 ? MM : P.m, B = P.B;
+    const uint64_t stride = (uint64_t)P.stride;
     const uint64_t ir = in_row0[k], orr = out_row0[k], oo = o_row0[k];
-    // stage P rows r0.., bins c0-m .. c0+VM_COLS+m
+    // 1. stage P rows r0.., bins c0-m .. c0+VM_COLS+m; frequency medians
     const int cols = VM_COLS + 2 * m;
     for (int e = threadIdx.x; e < VM_ROWS * cols; e += 256) {
         const int r = e / cols, c = e % cols;
         const int64_t t = r0 + r;
         const int b = c0 - m + c;
         float v = 0.0f;
-        if (t < F && b >= 0 && b < B) v = pold[(ir + (uint64_t)t) * P.stride + b];
+        if (t < F && b >= 0 && b < B) v = pin[(ir + (uint64_t)t) * stride + b];
         tl[r][c] = v;
     }
     __syncthreads();
-    // sliding medians: thread -> (row, segment)
     const int r = threadIdx.x % VM_ROWS, sg = threadIdx.x / VM_ROWS;
     const int bs = c0 + sg * VM_SEG;
     float pf[VM_SEG];
@@ -155,7 +122,7 @@ __global__ __launch_bounds__(256) void k_hpss_vmed(const float* __restrict__ ori
 #pragma unroll
         for (int j = 0; j < VM_SEG; j++) {
             const int b = bs + j;
-            pf[j] = b < B ? sw_median<W>(a, n, m) : 0.0f;
+            pf[j] = b < B ? sw_median<W, MM>(a, n, m) : 0.0f;
             if (j + 1 == VM_SEG || b + 1 >= B) continue;  // no further median in this segment
             const int bin = b + m + 1, bout = b - m;
             if (bout >= 0) {
@@ -168,34 +135,67 @@ __global__ __launch_bounds__(256) void k_hpss_vmed(const float* __restrict__ ori
             }
         }
     }
+    // 2. time medians of bin b over the tile's rows
+    const int b = c0 + (int)threadIdx.x;
+    const bool col = b < B;
+    float hf[VM_ROWS];
+    if (col) {
+        const float* src = hin + ir * stride + b;
+        float a[W];
+#pragma unroll
+        for (int j = 0; j < W; j++) a[j] = __builtin_inff();
+        const int64_t w0 = r0 >= m ? r0 - m : 0, w1 = r0 + m + 1 < F ? r0 + m + 1 : F;
+        for (int64_t t = w0; t < w1; t++) sw_insert<W>(a, src[(uint64_t)t * stride]);
+        int n = (int)(w1 - w0);
+#pragma unroll
+        for (int j = 0; j < VM_ROWS; j++) {
+            const int64_t t = r0 + j;
+            hf[j] = 0.0f;
+            if (t < F) {
+                hf[j] = sw_median<W, MM>(a, n, m);
+                const int64_t tin = t + m + 1, tout = t - m;
+                if (tout >= 0) {
+                    sw_delete<W>(a, src[(uint64_t)tout * stride]);
+                    n--;
+                }
+                if (tin < F) {
+                    sw_insert<W>(a, src[(uint64_t)tin * stride]);
+                    n++;
+                }
+            }
+        }
+    }
+    // 3. re-partition, one column per thread
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < VM_SEG; j++) tl[r][sg * VM_SEG + j + m] = pf[j];
     __syncthreads();
-    // re-partition, coalesced
     float mx = 0.0f;
-    for (int e = threadIdx.x; e < VM_ROWS * VM_COLS; e += 256) {
-        const int rr = e / VM_COLS, c = e % VM_COLS;
-        const int64_t t = r0 + rr;
-        const int b = c0 + c;
-        if (t >= F || b >= B) continue;
-        const uint64_t io = (ir + (uint64_t)t) * P.stride + b;
-        const uint64_t ou = (orr + (uint64_t)t) * P.stride + b;
-        const float x = orig[(oo + (uint64_t)t) * P.stride + b];
-        const float h = hnew[ou];  // the horizontal median of this round
-        const float p = tl[rr][c + m];
-        const float total = h + p;
-        float hn, pn;
-        if (total > 1e-10f) {
-            hn = x * (h / total);
-            pn = x * (p / total);
-        } else {
-            hn = x * 0.5f;
-            pn = x * 0.5f;
+    if (col) {
+#pragma unroll
+        for (int j = 0; j < VM_ROWS; j++) {
+            const int64_t t = r0 + j;
+            if (t >= F) break;
+            const float x = orig[(oo + (uint64_t)t) * stride + b];
+            const float h = hf[j];
+            const float p = tl[j][threadIdx.x + m];
+            const float total = h + p;
+            float hn, pn;
+            if (total > 1e-10f) {
+                hn = x * (h / total);
+                pn = x * (p / total);
+            } else {
+                hn = x * 0.5f;
+                pn = x * 0.5f;
+            }
+            const uint64_t ou = (orr + (uint64_t)t) * stride + b;
+            hout[ou] = hn;
+            pout[ou] = pn;
+            if (it > 0) {
+                const uint64_t io = (ir + (uint64_t)t) * stride + b;
+                mx = sd_maxf(sd_maxf(mx, sd_absf(hn - hin[io])), sd_absf(pn - pin[io]));
+            }
         }
-        hnew[ou] = hn;
-        pnew[ou] = pn;
-        if (it > 0) mx = sd_maxf(sd_maxf(mx, sd_absf(hn - hold[io])), sd_absf(pn - pold[io]));
     }
     if (it > 0) {
         mx = block_max(mx, red);
@@ -264,7 +264,7 @@ __global__ __launch_bounds__(RW_T) void k_hpss_rows(const float* __restrict__ p,
 }
 
 // ---- launcher: the whole decomposition ----
-template <int W>
+template <int W, int MM>
 static void hpss_rounds(const HpssLaunch& L, hipStream_t st) {
     const HpssParams& P = L.P;
     for (int it = 0; it < 10; it++) {
@@ -273,10 +273,8 @@ static void hpss_rounds(const HpssLaunch& L, hipStream_t st) {
         const uint64_t* irow = it == 0 ? L.orig_row0 : L.row0;
         float* hout = L.h[(it + 1) % 2];
         float* pout = L.p[(it + 1) % 2];
-        hipLaunchKernelGGL(k_hpss_hmed<W>, dim3((unsigned)L.n_htiles), dim3(256), 0, st, hin, irow, hout, L.row0,
-                           L.fpfx, L.htile_pfx, L.last_it, it, L.n_items, P);
-        hipLaunchKernelGGL(k_hpss_vmed<W>, dim3((unsigned)L.n_vtiles), dim3(256), 0, st, L.orig, L.orig_row0, hin, pin,
-                           irow, hout, pout, L.row0, L.fpfx, L.vtile_pfx, L.last_it, it, L.n_items, P, L.change);
+        hipLaunchKernelGGL((k_hpss_round<W, MM>), dim3((unsigned)L.n_vtiles), dim3(256), 0, st, L.orig, L.orig_row0, hin,
+                           pin, irow, hout, pout, L.row0, L.fpfx, L.vtile_pfx, L.last_it, it, L.n_items, P, L.change);
         hipLaunchKernelGGL(k_hpss_conv, dim3((L.n_items + 255) / 256), dim3(256), 0, st, L.n_items, it, L.change,
                            L.last_it);
     }
@@ -288,12 +286,12 @@ static void hpss_rounds(const HpssLaunch& L, hipStream_t st) {
 void launch_hpss(const HpssLaunch& L, hipStream_t st) {
     if (L.n_items == 0) return;
     (void)hipMemsetAsync(L.change, 0, (size_t)L.n_items * sizeof(unsigned int), st);
-    if (L.P.m == 10)
-        hpss_rounds<21>(L, st);
+    if (L.P.m == 10)  // the default margin
+        hpss_rounds<21, 10>(L, st);
     else if (L.P.m <= 4)
-        hpss_rounds<9>(L, st);
+        hpss_rounds<9, -1>(L, st);
     else
-        hpss_rounds<2 * VM_MAXM + 1>(L, st);
+        hpss_rounds<2 * VM_MAXM + 1, -1>(L, st);
 }
 
 void launch_hpss_rows(const float* p, const uint64_t* row0, const uint64_t* fpfx, const uint64_t* tile_pfx,

@@ -177,15 +177,13 @@ struct HpssLaunch {
     float* p[2];                 // ping-pong percussive buffers (the result ends in p[0])
     const uint64_t* row0;        // per item: first row in h / p (== fpfx: compact)
     const uint64_t* fpfx;        // frame prefix over the items
-    const uint64_t* htile_pfx;   // k_hpss_hmed tiles: ceil(F / 256) * ceil(B / 256) per item
-    uint64_t n_htiles;
-    const uint64_t* vtile_pfx;   // k_hpss_vmed tiles: ceil(F / 32) * ceil(B / 256) per item
+    const uint64_t* vtile_pfx;   // k_hpss_round tiles: ceil(F / 32) * ceil(B / 256) per item
     uint64_t n_vtiles;
     int* last_it;                // per item: last round run (init 9)
     unsigned int* change;        // per item: the round's largest change (f32 bits)
     int n_items;
 };
-constexpr int HPSS_HM_FRAMES = 256, HPSS_VM_FRAMES = 32, HPSS_COLS = 256, HPSS_ROW_FRAMES = 256;
+constexpr int HPSS_VM_FRAMES = 32, HPSS_COLS = 256, HPSS_ROW_FRAMES = 256;
 
 // ---- k_legacy (estimate_bpm_with_guardrails / estimate_bpm, period/mod.rs:196-404) ----
 struct LegacyParams {

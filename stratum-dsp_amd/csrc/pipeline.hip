@@ -1407,12 +1407,11 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         const int NS = (int)S.size();
         const uint64_t totS = hpfx.back();
         if (NS > 0 && totS > 0) {
-            std::vector<uint64_t> orow, ht(1, 0), vt(1, 0), rt(1, 0);
+            std::vector<uint64_t> orow, vt(1, 0), rt(1, 0);
             const uint64_t ncb = (1025 + HPSS_COLS - 1) / HPSS_COLS;
             for (int k = 0; k < NS; k++) {
                 const uint64_t F = hpfx[(size_t)k + 1] - hpfx[(size_t)k];
                 orow.push_back(bo.fpfx[(size_t)S[(size_t)k]]);
-                ht.push_back(ht.back() + (F + HPSS_HM_FRAMES - 1) / HPSS_HM_FRAMES * ncb);
                 vt.push_back(vt.back() + (F + HPSS_VM_FRAMES - 1) / HPSS_VM_FRAMES * ncb);
                 rt.push_back(rt.back() + (F + HPSS_ROW_FRAMES - 1) / HPSS_ROW_FRAMES);
             }
@@ -1429,8 +1428,6 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
             uint64_t* d_hpfx = c_.up("H.hpfx", hpfx);
             L.row0 = d_hpfx;
             L.fpfx = d_hpfx;
-            L.htile_pfx = c_.up("H.ht", ht);
-            L.n_htiles = ht.back();
             L.vtile_pfx = c_.up("H.vt", vt);
             L.n_vtiles = vt.back();
             L.last_it = c_.up("H.last", std::vector<int>((size_t)NS, 9));

@@ -28,6 +28,11 @@ CASES = {
     "key_ensemble": dict(enable_key_ensemble=1),
     "key_mode_heuristic": dict(enable_key_mode_heuristic=1, enable_key_minor_harmonic_bonus=1),
     "key_multi_scale": dict(enable_key_multi_scale=1),
+    "hpss_onsets": dict(enable_hpss_onsets=1),
+    "percussive_fallback": dict(enable_tempogram_percussive_fallback=1),
+    "force_legacy": dict(force_legacy_bpm=1),
+    "bpm_fusion": dict(enable_bpm_fusion=1),
+    "key_hpss": dict(enable_key_hpss_harmonic=1),
 }
 
 
