@@ -6,9 +6,15 @@ pass of the whole pipeline over one batch of `--tracks` tracks per GPU (BASELINE
 per GPU; config 3 = 8 GPUs x 1024).  Tracks are generated on the device before the timed region
 (inputs resident in HBM); every step re-runs everything, results are copied back to the host.
 
-Multi-GPU: one process per GPU (torch.distributed.run), tracks sharded with no data-path
-collective (`scaling: weak`); a gloo (CPU) process group provides the barrier and the max over
-ranks.  The engine's own HIP runtime is loaded before torch so no second GPU runtime is touched.
+Multi-GPU: one process per GPU, tracks sharded with no data-path collective (`scaling: weak`); a
+gloo (CPU) process group provides the barrier and the max over ranks.  Under torch.distributed.run
+the ranks come from the environment; `python bench.py --gpus N` without it spawns the N rank
+processes itself (before anything touches a GPU) and exits with their status.  The engine's own
+HIP runtime is loaded before torch so no second GPU runtime is touched.
+
+Workloads (BASELINE.json configs): `config2` (default) 1024 x 3-min tracks per GPU, full analysis;
+`mixed` (config 4) lengths uniform on whole seconds in [30, 600]; `bpm-only` (config 5) 4096
+tracks per GPU with an escalation-heavy BPM mix, stages a1-a19 only.
 
 Also reported: the dominant STFT kernel's HBM roofline (algorithmic bytes / HIP-event kernel time
 vs 8 TB/s) and the CPU restatement (oracle) timed on this box's host cores on a bounded sample.
@@ -17,6 +23,8 @@ import argparse
 import concurrent.futures as cf
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -38,13 +46,21 @@ class Engine:
         sdsp.lib()
         self.dev = dev
 
-    def generate(self, n, L, sr, seed0, bpm_mode):
-        buf = sdsp.DeviceBuffer(n * L, device=self.dev)
-        sdsp.generate_synthetic(buf.ptr, n, L, sr, seed0=seed0, bpm_mode=bpm_mode, device=self.dev)
-        return buf
+    def generate(self, lens, sr, seed0, bpm_mode):
+        """Track i (seed seed0 + i) of lens[i] samples at offs[i] of one HBM buffer."""
+        lens = np.asarray(lens, dtype=np.uint64)
+        offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+        buf = sdsp.DeviceBuffer(int(lens.sum()), device=self.dev)
+        if np.all(lens == lens[0]):
+            sdsp.generate_synthetic(buf.ptr, len(lens), int(lens[0]), sr, seed0=seed0, bpm_mode=bpm_mode, device=self.dev)
+        else:
+            for i, (o, ln) in enumerate(zip(offs, lens)):
+                sdsp.generate_synthetic(buf.ptr + 4 * int(o), 1, int(ln), sr, seed0=seed0 + i, bpm_mode=bpm_mode,
+                                        device=self.dev)
+        return buf, offs
 
-    def analyze(self, buf, offs, lens, sr):
-        return sdsp.analyze_batch_device(buf.ptr, offs, lens, sr, device=self.dev, raw=True)
+    def analyze(self, buf, offs, lens, sr, stages=0):
+        return sdsp.analyze_batch_device(buf.ptr, offs, lens, sr, device=self.dev, raw=True, stages=stages)
 
     def stage_times(self):
         return sdsp.stage_times(self.dev)
@@ -67,10 +83,11 @@ class DryEngine:
     def __init__(self, dev):
         self.dev = dev
 
-    def generate(self, n, L, sr, seed0, bpm_mode):
-        return {"n": n, "seed0": seed0}
+    def generate(self, lens, sr, seed0, bpm_mode):
+        lens = np.asarray(lens, dtype=np.uint64)
+        return {"n": len(lens), "seed0": seed0}, np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
 
-    def analyze(self, buf, offs, lens, sr):
+    def analyze(self, buf, offs, lens, sr, stages=0):
         time.sleep(0.001 * len(lens))
         return DryEngine._Res(len(lens))
 
@@ -98,23 +115,70 @@ def max_over_ranks(dt, tdist):
     return float(t.item())
 
 
+WORKLOADS = {
+    # name: (BASELINE config, default tracks per GPU, synthetic BPM mix, stages)
+    "config2": (2, 1024, 0, 0),
+    "mixed": (4, 1024, 0, 0),
+    "bpm-only": (5, 4096, 1, 1),
+}
+
+
+def track_lengths(workload, n, seconds, sr, seed0):
+    """Per-track sample counts.  mixed (config 4): whole seconds uniform on [30, 600], seeded by
+    the rank's first track so ranks draw disjoint, reproducible lengths."""
+    if workload == "mixed":
+        rng = np.random.default_rng(0x5EED0000 + seed0)
+        return (rng.integers(30, 601, size=n) * sr).astype(np.uint64)
+    return np.full(n, int(seconds * sr), dtype=np.uint64)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` outside torch.distributed.run: start N fresh rank processes (rank r on
+    GPU r) with the torchrun environment and wait for them.  This process touches no GPU; rank 0
+    prints the JSON line.  Returns the worst exit status."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE=str(n),
+               LOCAL_WORLD_SIZE=str(n))
+    procs = []
+    for r in range(n):
+        e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=e))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--tracks", type=int, default=1024, help="tracks per GPU per step")
-    ap.add_argument("--seconds", type=float, default=180.0)
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, os.cpu_count())")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="config2")
+    ap.add_argument("--tracks", type=int, default=0, help="tracks per GPU per step (0 = the workload's)")
+    ap.add_argument("--seconds", type=float, default=180.0, help="track length (config2 / bpm-only)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, usable host cores)")
     ap.add_argument("--cpu-tracks", type=int, default=0, help="0 = 2 per thread")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--bpm-mode", type=int, default=0, help="1 = config-5 escalation-heavy BPM mix")
+    ap.add_argument("--bpm-mode", type=int, default=-1, help="synthetic BPM mix (-1 = the workload's; 1 = config 5)")
     ap.add_argument("--dry-run", action="store_true", help="host-logic rehearsal without a GPU (tests)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    cfg_no, n_default, mix_default, stage_mask = WORKLOADS[args.workload]
+    bpm_mode = mix_default if args.bpm_mode < 0 else args.bpm_mode
     eng = (DryEngine if args.dry_run else Engine)(local)
     tdist = None
     if world > 1:
@@ -127,25 +191,27 @@ def main():
             tdist.barrier()
 
     sr = 44100
-    n = args.tracks
-    L = int(args.seconds * sr)
-    buf = eng.generate(n, L, sr, shard_seed0(rank, n), args.bpm_mode)
-    offs = np.arange(n, dtype=np.uint64) * np.uint64(L)
-    lens = np.full(n, L, dtype=np.uint64)
+    n = args.tracks or n_default
+    seed0 = shard_seed0(rank, n)
+    lens = track_lengths(args.workload, n, args.seconds, sr, seed0)
+    buf, offs = eng.generate(lens, sr, seed0, bpm_mode)
 
     # results stay native (C-ABI structs, as a Rust/C caller receives them); the parity sample
     # below converts the tracks it checks
     for _ in range(args.warmup):
-        eng.analyze(buf, offs, lens, sr).free()
+        eng.analyze(buf, offs, lens, sr, stage_mask).free()
     barrier()
     eng.synchronize()
     t0 = time.perf_counter()
     stft = {"ms8": 0.0, "b8": 0.0, "l8": 0, "ms2": 0.0, "b2": 0.0, "l2": 0}
+    step_s = []
     res = None
     for _ in range(args.steps):
         if res is not None:
             res.free()
-        res = eng.analyze(buf, offs, lens, sr)
+        ts = time.perf_counter()
+        res = eng.analyze(buf, offs, lens, sr, stage_mask)  # returns with the results on the host
+        step_s.append(time.perf_counter() - ts)
         st = eng.stage_times()
         stft["ms8"] += st["stft8192_ms"]
         stft["b8"] += st["stft8192_bytes"]
@@ -160,14 +226,17 @@ def main():
     total_tracks = n * world * args.steps
     value = total_tracks / dt
     stages = eng.stage_times()
-    # roofline of the dominant STFT kernel (k_stft_mag<8192>): algorithmic bytes per launch
-    # (4*N_in + 4*F*(nfft/2+1)) / average launch time (HIP events on the engine stream)
-    l8 = max(stft["l8"], 1)
-    bytes_per_launch = stft["b8"] / l8
-    ms_per_launch = stft["ms8"] / l8
+    # roofline of the dominant STFT kernel: k_stft_mag<8192> (the key STFT), or k_stft_mag<2048>
+    # when the key path does not run (bpm-only).  Algorithmic bytes per launch (4*N_in +
+    # 4*F*(nfft/2+1)) / average launch time (HIP events on the kernel's stream).
+    key_k = stft["l8"] > 0
+    tag = "8" if key_k else "2"
+    nl = max(stft["l" + tag], 1)
+    bytes_per_launch = stft["b" + tag] / nl
+    ms_per_launch = stft["ms" + tag] / nl
     achieved = bytes_per_launch / (ms_per_launch * 1e-3) / 1e9 if ms_per_launch > 0 else 0.0
     traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_stft8192.json")
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_stft8192.json" if key_k else "pmc_stft2048.json")
     if os.path.exists(pmc_path):
         # rocprofv3 PMC passes (profiles/README.md): measured HBM bytes / algorithmic bytes for
         # this kernel; scales to the per-launch traffic of whatever batch this run used
@@ -177,7 +246,7 @@ def main():
             traffic = round(ratio * bytes_per_launch)
     roofline = {
         "bound": "hbm",
-        "kernel": "k_stft_mag<8192> (key STFT, 8192/512)",
+        "kernel": "k_stft_mag<8192> (key STFT, 8192/512)" if key_k else "k_stft_mag<2048> (tempo STFT, 2048/512)",
         "achieved": round(achieved, 2),
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
@@ -193,15 +262,31 @@ def main():
     cpu = None
     parity = None
     extras = {}
+    ss = sorted(step_s)
+    extras["step_ms"] = {"median": round(1e3 * ss[len(ss) // 2], 3), "min": round(1e3 * ss[0], 3),
+                         "max": round(1e3 * ss[-1], 3), "all": [round(1e3 * t, 3) for t in step_s]}
     if not args.dry_run:
         # fraction of this rank's tracks whose base estimate escalated to multi-resolution
         # (src/lib.rs:410-459; BASELINE.md asks for the escalation rate beside the throughput)
         extras["escalation_rate"] = round(res.count("tempogram_multi_res_triggered") / max(n, 1), 4)
+        if stage_mask == 1:
+            extras["bpm_only_vs_full"] = bpm_only_check(eng, buf, offs, lens, sr, res, min(n, 64))
+    if args.workload == "mixed":
+        extras["mean_track_seconds"] = round(float(lens.mean()) / sr, 2)
+        extras["audio_seconds_per_s"] = round(float(lens.sum()) / sr * world * args.steps / dt, 1)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.dry_run:
-        cpu, parity = cpu_baseline(buf, res, n, L, sr, args)
+        cpu, parity = cpu_baseline(buf, offs, lens, res, n, sr, args)
         extras["sine_30s"] = sine_30s(sr)
 
     if rank == 0:
+        wl = {
+            "config2": f"batch of {n} synthetic {args.seconds:g}-s 44.1 kHz mono tracks per GPU, "
+                       "AnalysisConfig::default(), full BPM + key + beat grid",
+            "mixed": f"mixed-length batch of {n} synthetic tracks per GPU, whole seconds uniform in [30, 600] s, "
+                     "AnalysisConfig::default(), full BPM + key + beat grid",
+            "bpm-only": f"BPM-only path (stages a1-a19, multi-resolution escalation on) over {n} synthetic "
+                        f"{args.seconds:g}-s tracks per GPU, BPMs 1/3 in [55,80], 1/3 in [170,200], 1/3 in [80,170]",
+        }[args.workload]
         out = {
             "metric": "tracks/sec full analyze_audio(), 3-min 44.1 kHz mono, at 1/2/4/8 MI355X",
             "value": round(value, 3),
@@ -214,15 +299,16 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (seeded on-device generator: kick/hat/triad/diatonic line, 3-min 44.1 kHz mono)"
+            "data": "synthetic (seeded on-device generator: kick/hat/triad/diatonic line, 44.1 kHz mono)"
             + (" [DRY RUN: no GPU, not a measurement]" if args.dry_run else ""),
             "config": {
-                "workload": f"batch of {n} synthetic {args.seconds:g}-s 44.1 kHz mono tracks per GPU, "
-                            "AnalysisConfig::default(), full BPM + key + beat grid",
+                "workload": wl,
+                "baseline_config": cfg_no if world == 1 or cfg_no != 2 else 3,
                 "tracks_per_gpu": n,
-                "seconds_per_track": args.seconds,
+                "seconds_per_track": args.seconds if args.workload != "mixed" else "30-600",
                 "sample_rate": sr,
-                "bpm_mode": args.bpm_mode,
+                "bpm_mode": bpm_mode,
+                "stages": "bpm-only (a1-a19)" if stage_mask == 1 else "full",
                 "parallelism": f"track-sharded x{world} (no collectives)",
             },
             "errors": n_err,
@@ -237,25 +323,67 @@ def main():
         tdist.destroy_process_group()
 
 
-def cpu_baseline(buf, res, n, L, sr, args):
+def bpm_only_check(eng, buf, offs, lens, sr, res, k):
+    """BASELINE config 5: the BPM-only stages must give a full run's bpm, bpm_confidence and
+    multi-resolution flags.  Runs the full pipeline on the first k tracks and compares bitwise."""
+    full = eng.analyze(buf, offs[:k], lens[:k], sr, 0)
+    same = 0
+    for i in range(k):
+        a, b = res[i], full[i]
+        if isinstance(a, Exception) or isinstance(b, Exception):
+            same += int(type(a) is type(b))
+            continue
+        keys = ("bpm", "bpm_confidence")
+        flags = ("tempogram_multi_res_triggered", "tempogram_multi_res_used")
+        ok = all(np.float32(a[x]).tobytes() == np.float32(b[x]).tobytes() for x in keys)
+        ok = ok and all(a["metadata"].get(f) == b["metadata"].get(f) for f in flags)
+        same += int(ok)
+    full.free()
+    return {"checked": k, "identical": same}
+
+
+def host_cpu():
+    """The host the CPU baseline ran on: logical CPUs, the ones this process may use, the model."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count()
+    return {"nproc": os.cpu_count(), "usable": usable, "model": model}
+
+
+def cpu_baseline(buf, offs, lens, res, n, sr, args):
     """The oracle (C++ restatement, single-threaded per track, one track per thread as
     examples/analyze_batch.rs:239-268 does with rayon) on a bounded sample of the same tracks."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     import parity
 
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    host = host_cpu()
+    threads = args.cpu_threads or min(16, host["usable"] or 1)
     k = min(n, args.cpu_tracks or 2 * threads)
-    xs = [buf.to_host(i * L, L) for i in range(k)]
+    xs = [buf.to_host(int(offs[i]), int(lens[i])) for i in range(k)]
     oracle.lib()
 
     def one(x):
-        return oracle.analyze(x, sr)
+        t = time.perf_counter()
+        r = oracle.analyze(x, sr)  # ctypes releases the GIL: the threads run in parallel
+        return r, time.perf_counter() - t
 
     t0 = time.perf_counter()
     with cf.ThreadPoolExecutor(threads) as ex:
         outs = list(ex.map(one, xs))
     dt = time.perf_counter() - t0
+    per_track = [o[1] for o in outs]
+    outs = [o[0] for o in outs]
     match = sum(1 for i, (st, ref) in enumerate(outs) if st == 0 and not parity.diff_results(res[i], ref))
     exact = sum(1 for i, (st, ref) in enumerate(outs) if st == 0 and parity.exact_fraction(res[i], ref) == 1.0)
     cpu = {
@@ -263,15 +391,21 @@ def cpu_baseline(buf, res, n, L, sr, args):
         "unit": "tracks/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{k} of the benchmark's own {args.seconds:g}-s tracks, one track per thread, "
-                  f"{dt:.1f} s wall ({dt * threads:.0f} thread-s); C++ restatement -O3, FFT per sdsp_fft_spec.h",
+        "host": host,
+        "sample": f"{k} of the benchmark's own tracks, one track per thread on {threads} threads, "
+                  f"{dt:.1f} s wall ({sum(per_track):.0f} thread-s); C++ restatement -O3, FFT per sdsp_fft_spec.h "
+                  "(scalar radix-4; rustfft is SIMD)",
+        # one thread's rate over the same k tracks, each timed inside its own thread (while the
+        # other threads ran): k / the summed per-track seconds
+        "value_1thread_loaded": round(k / sum(per_track), 4),
     }
-    # one thread, the same tracks (report 1 thread and all cores)
+    # one thread alone, the first tracks again
     k1 = min(k, 2)
     t0 = time.perf_counter()
     for x in xs[:k1]:
         one(x)
     cpu["value_1thread"] = round(k1 / (time.perf_counter() - t0), 4)
+    cpu["value_1thread_sample"] = f"{k1} tracks, alone on one thread"
     par = {"checked": k, "within_tolerance": match, "bit_exact": exact}
     return cpu, par
 

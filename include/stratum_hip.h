@@ -273,6 +273,19 @@ int32_t sdsp_analyze_batch_device(const float* d_samples, const uint64_t* offset
                                   const sdsp_config* cfg, int32_t device, void* stream,
                                   sdsp_result* outs);
 
+/*
+ * Stage selection for the device-resident batch (new; the reference has no such switch).
+ * SDSP_STAGES_BPM_ONLY runs the tempo path alone -- src/lib.rs:86-910, SURVEY.md rows a1-a19:
+ * normalisation, trim, onsets, tempogram, multi-resolution escalation, BPM choice.  bpm,
+ * bpm_confidence, duration and the tempogram_* flags equal a full run's; the key fields keep their
+ * defaults (C major, 0) and the beat grid is empty.  BASELINE config 5 is quoted in this mode.
+ */
+enum sdsp_stages { SDSP_STAGES_FULL = 0, SDSP_STAGES_BPM_ONLY = 1 };
+int32_t sdsp_analyze_batch_device_ex(const float* d_samples, const uint64_t* offsets,
+                                     const uint64_t* lens, uint64_t n_tracks, uint32_t sample_rate,
+                                     const sdsp_config* cfg, int32_t device, void* stream,
+                                     int32_t stages, sdsp_result* outs);
+
 /* Frees the arrays owned by one result (beats, downbeats, bars, warnings, candidates). */
 void sdsp_result_free(sdsp_result* r);
 

@@ -124,13 +124,11 @@ int main(int argc, char** argv) {
             lens.push_back(items[i].samples.size());
         }
         std::vector<sdsp_result> outs(idx.size());
-        const int32_t st = sdsp_analyze_batch(ptrs.data(), lens.data(), idx.size(), kv.first, &cfg, devices, outs.data());
+        // a non-OK return means some chunk failed; every track's own status says which (tracks the
+        // library did not analyse carry an error status), so each result is read and freed
+        (void)sdsp_analyze_batch(ptrs.data(), lens.data(), idx.size(), kv.first, &cfg, devices, outs.data());
         for (size_t k = 0; k < idx.size(); k++) {
             Item& it = items[idx[k]];
-            if (st != 0 && outs[k].status == 0) {
-                it.error = "analysis failed: batch failed";
-                continue;
-            }
             const sdsp_result& r = outs[k];
             if (r.status != 0) {
                 it.error = std::string("analysis failed: ") + r.error_message;

@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "../../include/sdsp_fft_spec.h"
+#include "batch_sched.hpp"
 #include "kernels.hpp"
 #include "sdsp_runtime.hpp"
 
@@ -596,7 +597,8 @@ struct TempoPassOut {
 // ---------------------------------------------------------------------------------------
 class Pipeline {
    public:
-    Pipeline(DeviceCtx& d, const sdsp_config& cfg, uint32_t sr) : c_(d), d_(d), cfg_(cfg), sr_(sr) {}
+    Pipeline(DeviceCtx& d, const sdsp_config& cfg, uint32_t sr, int stages = SDSP_STAGES_FULL)
+        : c_(d), d_(d), cfg_(cfg), sr_(sr), bpm_only_(stages == SDSP_STAGES_BPM_ONLY) {}
 
     void run(const float* d_samples, const std::vector<uint64_t>& in_off, const std::vector<uint64_t>& n_raw,
              std::vector<TrackRes>& res);
@@ -606,6 +608,9 @@ class Pipeline {
     DeviceCtx& d_;
     const sdsp_config& cfg_;
     uint32_t sr_;
+    // SDSP_STAGES_BPM_ONLY: the tempo path alone (src/lib.rs:86-910); the key
+    // stream and the beat grid are not run, their result fields keep their defaults
+    bool bpm_only_ = false;
     sdsp_stage_times times_{};
     // RMS / LUFS: gains (and LUFS status) of every track, folded once for the whole batch
     // before the sub-batches (the fold is a per-track sequential latency, not a throughput)
@@ -673,11 +678,11 @@ void Pipeline::run(const float* d_samples, const std::vector<uint64_t>& in_off, 
     for (size_t i = 0; i < T; i++) {
         if (res[i].status != SDSP_OK) continue;
         const double n = (double)n_raw[i];
-        need[i] = n / hop * (STRIDE2 * 4.0 * 1.3 + 4 * 70.0) + n / khop * STRIDE8 * 4.0 +
+        need[i] = n / hop * (STRIDE2 * 4.0 * 1.3 + 4 * 70.0) + (bpm_only_ ? 0.0 : n / khop * STRIDE8 * 4.0) +
                   (n / 256 + n / 1024) * STRIDE2 * 4.0 + 1e6;
         if (cfg_.enable_hpss_onsets || cfg_.enable_tempogram_percussive_fallback)  // H, P ping-pong + a copy
             need[i] += n / hop * STRIDE2 * 4.0 * 5.0;
-        if (cfg_.enable_key_hpss_harmonic) need[i] += n / khop * 1024.0 * 4.0;
+        if (cfg_.enable_key_hpss_harmonic && !bpm_only_) need[i] += n / khop * 1024.0 * 4.0;
         total_need += need[i];
     }
     const double parts = std::max(1.0, std::ceil(total_need / budget));
@@ -1223,6 +1228,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     double key_in_bytes = 0;
     for (int i = 0; i < NR; i++) {
         const uint64_t n = bin.n_trim[(size_t)i];
+        if (bpm_only_) break;  // SDSP_STAGES_BPM_ONLY: stages a1-a19 only, no key path
         if (n < (uint64_t)FS || n < (uint64_t)KFS) continue;  // key skipped or empty key spectrogram -> default key
         const uint64_t F8 = (n - KFS) / (uint64_t)KHOP + 1;
         K.push_back(i);
@@ -1328,6 +1334,9 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
             std::vector<HarmEntry> ht =
                 harm_table(B8, sr_, KFS, cfg_.soft_mapping_sigma, hp.hmax, cfg_.key_hpcp_harmonic_decay);
             HarmEntry* d_ht = c_.up("E.harm", ht);
+            // the table upload is queued on the main stream: order the key stream after it
+            kt.mark(10);
+            SDSP_HIP_CHECK(hipStreamWaitEvent(st2, kt.ev[10], 0));
             launch_hpcp(mags8, d_kpfx, d_ktile, d_kid, NK, ktile.back(), hp, d_ht, d_chroma, d_energy, st2);
         } else {  // :1169-1197 (the tuned variant only when |offset| > 1e-6)
             const ChromaParams cp = chroma_params(cfg_, sr_, 0, B8, fres8);
@@ -1530,7 +1539,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         ein.gate = 0;
         TempoPassOut o256, o1024;
         // multi-resolution runs only at hop 512 (unsupported()); SDSP_NO_ROW_REUSE: A/B switch
-        static const bool reuse_on = std::getenv("SDSP_NO_ROW_REUSE") == nullptr;
+        const bool reuse_on = std::getenv("SDSP_NO_ROW_REUSE") == nullptr;  // read per call (tests flip it)
         ein.hop = 256;
         ein.reuse = (HOP == 512 && reuse_on) ? 2 : 0;
         tempo_pass("C256.", ein, o256);
@@ -1685,6 +1694,16 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     if (cfg_.force_legacy_bpm || cfg_.enable_bpm_fusion)
         legacy_select(bin, d_chosen, d_coff, d_cn, R, idx, res, fbpm_h, fconf_h, d_fbpm, d_fconf);
     tm.mark(4);
+    if (bpm_only_) {
+        for (int i = 0; i < NR; i++) {
+            TrackRes& r = res[(size_t)idx[(size_t)R[(size_t)i]]];
+            if (r.status != SDSP_OK) continue;
+            r.bpm = fbpm_h[(size_t)i];
+            r.bpm_conf = fconf_h[(size_t)i];
+        }
+        htr("results (bpm only)");
+        return;
+    }
     // ---------------- D: beat grid ----------------
     std::vector<int> ident((size_t)NR);
     std::vector<uint64_t> boff((size_t)NR + 1, 0);
@@ -1892,8 +1911,12 @@ void fill_result(const TrackRes& r, uint32_t sr, float ms, sdsp_result* o) {
     o->tempogram_percussive_used = r.perc_used;
 }
 
+// One device-resident batch on `device`.  The engine's main stream first waits for `user_stream`
+// (everything queued on it so far) and for `wait_ev` (a copy's completion), whichever are given.
 int32_t run_device(int device, const float* d_samples, const uint64_t* offsets, const uint64_t* lens, uint64_t n,
-                   uint32_t sr, const sdsp_config* cfg, void* user_stream, sdsp_result* outs) {
+                   uint32_t sr, const sdsp_config* cfg, void* user_stream, sdsp_result* outs,
+                   int stages = SDSP_STAGES_FULL, hipEvent_t wait_ev = nullptr) {
+    if (stages != SDSP_STAGES_FULL && stages != SDSP_STAGES_BPM_ONLY) throw HipError("unknown stage mask");
     DeviceCtx& d = device_ctx(device);
     std::lock_guard<std::mutex> lk(d.mu);
     SDSP_HIP_CHECK(hipSetDevice(device));
@@ -1904,10 +1927,11 @@ int32_t run_device(int device, const float* d_samples, const uint64_t* offsets, 
         SDSP_HIP_CHECK(hipStreamWaitEvent(d.stream, ev, 0));
         SDSP_HIP_CHECK(hipEventDestroy(ev));
     }
+    if (wait_ev) SDSP_HIP_CHECK(hipStreamWaitEvent(d.stream, wait_ev, 0));
     auto t0 = std::chrono::steady_clock::now();
     std::vector<uint64_t> off(offsets, offsets + n), ln(lens, lens + n);
     std::vector<TrackRes> res;
-    Pipeline p(d, *cfg, sr);
+    Pipeline p(d, *cfg, sr, stages);
     p.run(d_samples, off, ln, res);
     const float ms = (float)(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() /
                              (double)std::max<uint64_t>(n, 1));
@@ -1925,8 +1949,15 @@ extern "C" {
 int32_t sdsp_analyze_batch_device(const float* d_samples, const uint64_t* offsets, const uint64_t* lens,
                                   uint64_t n_tracks, uint32_t sample_rate, const sdsp_config* cfg, int32_t device,
                                   void* stream, sdsp_result* outs) {
+    return sdsp_analyze_batch_device_ex(d_samples, offsets, lens, n_tracks, sample_rate, cfg, device, stream,
+                                        SDSP_STAGES_FULL, outs);
+}
+
+int32_t sdsp_analyze_batch_device_ex(const float* d_samples, const uint64_t* offsets, const uint64_t* lens,
+                                     uint64_t n_tracks, uint32_t sample_rate, const sdsp_config* cfg, int32_t device,
+                                     void* stream, int32_t stages, sdsp_result* outs) {
     try {
-        return run_device(device, d_samples, offsets, lens, n_tracks, sample_rate, cfg, stream, outs);
+        return run_device(device, d_samples, offsets, lens, n_tracks, sample_rate, cfg, stream, outs, stages);
     } catch (const std::exception& e) {
         std::fprintf(stderr, "sdsp_analyze_batch_device: %s\n", e.what());
         for (uint64_t i = 0; i < n_tracks; i++) {
@@ -1938,15 +1969,32 @@ int32_t sdsp_analyze_batch_device(const float* d_samples, const uint64_t* offset
     }
 }
 
-// Host buffers: the batch is cut into chunks of whole tracks (up to
-// SDSP_BATCH_CHUNK_TRACKS tracks, default 512, and about 8 GB) that one host thread per device
-// pulls from a shared counter, so escalation-heavy chunks do not leave the other GPUs idle.  Per
-// device a copier thread stages the next chunk into the second of two HBM slots while the
-// device analyses the current one, so PCIe transfers overlap the kernels.
+// Host buffers: chunks of whole tracks (up to SDSP_BATCH_CHUNK_TRACKS tracks, default
+// 512, and about 8 GB) pulled from a shared counter by one worker per device; per device a copier
+// thread stages the next chunk into the second of two HBM slots (its own stream, completion
+// signalled by an event the engine's stream waits on) while the device analyses the current one.
+// The queue itself is batch_sched.hpp (host-only, tested with fake devices).
 namespace {
 struct Slot {
     float* d = nullptr;
     uint64_t cap = 0;  // floats
+    hipEvent_t ready = nullptr;
+};
+struct DeviceStage {
+    int dev = 0;
+    hipStream_t copy = nullptr;
+    Slot slot[2];
+    ~DeviceStage() {
+        if (copy) {
+            (void)hipSetDevice(dev);
+            (void)hipStreamSynchronize(copy);
+        }
+        for (auto& sl : slot) {
+            if (sl.d) (void)hipFree(sl.d);
+            if (sl.ready) (void)hipEventDestroy(sl.ready);
+        }
+        if (copy) (void)hipStreamDestroy(copy);
+    }
 };
 }  // namespace
 
@@ -1965,98 +2013,51 @@ int32_t sdsp_analyze_batch(const float* const* tracks, const uint64_t* lens, uin
     for (int d = 0; d < ndev && d < 32; d++)
         if (device_mask == 0 ? d == 0 : ((device_mask >> d) & 1u)) devs.push_back(d);
     if (devs.empty()) devs.push_back(0);
-    // chunk boundaries: whole tracks, bounded in count and bytes
     uint64_t max_tracks = 512;
     if (const char* e = std::getenv("SDSP_BATCH_CHUNK_TRACKS")) max_tracks = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
-    const uint64_t max_floats = (uint64_t)2 << 30;  // 8 GB
-    std::vector<uint64_t> cb(1, 0);
-    uint64_t acc = 0;
-    for (uint64_t i = 0; i < n_tracks; i++) {
-        if (i > cb.back() && (i - cb.back() >= max_tracks || acc + lens[i] > max_floats)) {
-            cb.push_back(i);
-            acc = 0;
-        }
-        acc += lens[i];
-    }
-    cb.push_back(n_tracks);
-    const size_t n_chunks = n_tracks ? cb.size() - 1 : 0;
+    const std::vector<uint64_t> cb = plan_chunks(lens, n_tracks, max_tracks, (uint64_t)2 << 30 /* 8 GB of f32 */);
+    const size_t n_chunks = cb.size() - 1;
     // every result starts as an error; run_device overwrites the tracks it analyses
-    for (uint64_t i = 0; i < n_tracks; i++) {
-        std::memset(&outs[i], 0, sizeof(outs[i]));
-        outs[i].status = SDSP_ERR_PROCESSING;
-        std::snprintf(outs[i].error_message, sizeof outs[i].error_message, "Processing error: track not analysed");
-    }
-    std::atomic<size_t> next{0};
-    std::vector<int32_t> rc(devs.size(), SDSP_OK);
-    auto fail_chunk = [&](size_t c, const char* what) {
+    auto mark_failed = [&](size_t c, const std::string& what) {
         for (uint64_t i = cb[c]; i < cb[c + 1]; i++) {
             std::memset(&outs[i], 0, sizeof(outs[i]));
             outs[i].status = SDSP_ERR_PROCESSING;
-            std::snprintf(outs[i].error_message, sizeof outs[i].error_message, "Processing error: %s", what);
+            std::snprintf(outs[i].error_message, sizeof outs[i].error_message, "Processing error: %s", what.c_str());
         }
     };
-    auto device_worker = [&](size_t k) {
-        const int dev = devs[k];
-        Slot slot[2];
-        std::mutex mu;
-        std::condition_variable cv;
-        // ready[s]: chunk index staged in slot s (-1 = free); done: the copier has finished
-        long ready[2] = {-1, -1};
-        bool done = false;
-        std::string copy_err;
-        auto copier = [&]() {
-            int s = 0;
-            try {
-                SDSP_HIP_CHECK(hipSetDevice(dev));
-                for (;;) {
-                    const size_t c = next++;
-                    if (c >= n_chunks) break;
-                    {
-                        std::unique_lock<std::mutex> lk(mu);
-                        cv.wait(lk, [&] { return ready[s] < 0; });
-                    }
-                    uint64_t tot = 0;
-                    for (uint64_t i = cb[c]; i < cb[c + 1]; i++) tot += lens[i];
-                    if (slot[s].cap < tot) {
-                        if (slot[s].d) SDSP_HIP_CHECK(hipFree(slot[s].d));
-                        slot[s].d = nullptr;
-                        slot[s].cap = std::max<uint64_t>(tot, 1);
-                        SDSP_HIP_CHECK(hipMalloc(&slot[s].d, slot[s].cap * sizeof(float)));
-                    }
-                    uint64_t o = 0;
-                    for (uint64_t i = cb[c]; i < cb[c + 1]; i++) {
-                        if (lens[i])
-                            SDSP_HIP_CHECK(hipMemcpy(slot[s].d + o, tracks[i], lens[i] * sizeof(float), hipMemcpyHostToDevice));
-                        o += lens[i];
-                    }
-                    {
-                        std::lock_guard<std::mutex> lk(mu);
-                        ready[s] = (long)c;
-                    }
-                    cv.notify_all();
-                    s ^= 1;
-                }
-            } catch (const std::exception& e) {
-                std::lock_guard<std::mutex> lk(mu);
-                copy_err = e.what();
+    for (size_t c = 0; c < n_chunks; c++) mark_failed(c, "track not analysed");
+    std::vector<std::unique_ptr<DeviceStage>> stg;
+    std::vector<ChunkDevice> cds;
+    for (int dev : devs) {
+        stg.emplace_back(new DeviceStage());
+        DeviceStage* ds = stg.back().get();
+        ds->dev = dev;
+        ChunkDevice cd;
+        cd.stage = [ds, &cb, tracks, lens](int s, size_t c) {
+            SDSP_HIP_CHECK(hipSetDevice(ds->dev));
+            if (!ds->copy) SDSP_HIP_CHECK(hipStreamCreateWithFlags(&ds->copy, hipStreamNonBlocking));
+            Slot& sl = ds->slot[s];
+            if (!sl.ready) SDSP_HIP_CHECK(hipEventCreateWithFlags(&sl.ready, hipEventDisableTiming));
+            uint64_t tot = 0;
+            for (uint64_t i = cb[c]; i < cb[c + 1]; i++) tot += lens[i];
+            if (sl.cap < tot) {
+                if (sl.d) SDSP_HIP_CHECK(hipFree(sl.d));
+                sl.d = nullptr;
+                sl.cap = 0;
+                SDSP_HIP_CHECK(hipMalloc(&sl.d, std::max<uint64_t>(tot, 1) * sizeof(float)));
+                sl.cap = std::max<uint64_t>(tot, 1);
             }
-            {
-                std::lock_guard<std::mutex> lk(mu);
-                done = true;
+            uint64_t o = 0;
+            for (uint64_t i = cb[c]; i < cb[c + 1]; i++) {
+                if (lens[i])
+                    SDSP_HIP_CHECK(hipMemcpyAsync(sl.d + o, tracks[i], lens[i] * sizeof(float), hipMemcpyHostToDevice,
+                                                  ds->copy));
+                o += lens[i];
             }
-            cv.notify_all();
+            SDSP_HIP_CHECK(hipEventRecord(sl.ready, ds->copy));
         };
-        std::thread cp(copier);
-        int s = 0;
-        for (;;) {
-            long c;
-            {
-                std::unique_lock<std::mutex> lk(mu);
-                cv.wait(lk, [&] { return ready[s] >= 0 || (done && ready[0] < 0 && ready[1] < 0); });
-                if (ready[s] < 0) break;  // copier finished and nothing staged
-                c = ready[s];
-            }
-            const uint64_t a = cb[(size_t)c], b = cb[(size_t)c + 1];
+        cd.analyze = [ds, &cb, lens, sample_rate, cfg, outs](int s, size_t c) {
+            const uint64_t a = cb[c], b = cb[c + 1];
             std::vector<uint64_t> off(b - a), ln(b - a);
             uint64_t tot = 0;
             for (uint64_t i = a; i < b; i++) {
@@ -2064,39 +2065,21 @@ int32_t sdsp_analyze_batch(const float* const* tracks, const uint64_t* lens, uin
                 ln[i - a] = lens[i];
                 tot += lens[i];
             }
-            try {
-                const int32_t r = run_device(dev, slot[s].d, off.data(), ln.data(), b - a, sample_rate, cfg, nullptr, outs + a);
-                if (r != SDSP_OK) rc[k] = r;
-            } catch (const std::exception& e) {
-                std::fprintf(stderr, "sdsp_analyze_batch: %s\n", e.what());
-                fail_chunk((size_t)c, e.what());
-                rc[k] = SDSP_ERR_PROCESSING;
-            }
-            {
-                std::lock_guard<std::mutex> lk(mu);
-                ready[s] = -1;
-            }
-            cv.notify_all();
-            s ^= 1;
-        }
-        cp.join();
-        if (!copy_err.empty()) {
-            std::fprintf(stderr, "sdsp_analyze_batch: %s\n", copy_err.c_str());
-            rc[k] = SDSP_ERR_PROCESSING;
-        }
-        for (auto& sl : slot)
-            if (sl.d) (void)hipFree(sl.d);
-    };
-    if (devs.size() == 1) {
-        device_worker(0);
-    } else {
-        std::vector<std::thread> th;
-        for (size_t k = 0; k < devs.size(); k++) th.emplace_back(device_worker, k);
-        for (auto& t : th) t.join();
+            run_device(ds->dev, ds->slot[s].d, off.data(), ln.data(), b - a, sample_rate, cfg, nullptr, outs + a,
+                       SDSP_STAGES_FULL, ds->slot[s].ready);
+        };
+        cd.drain = [ds]() {  // after a failed chunk: nothing may still read the slot it reuses
+            SDSP_HIP_CHECK(hipSetDevice(ds->dev));
+            SDSP_HIP_CHECK(hipDeviceSynchronize());
+        };
+        cds.push_back(cd);
     }
-    for (auto v : rc)
-        if (v != SDSP_OK) return v;
-    return SDSP_OK;
+    const size_t failed = run_chunked(n_chunks, cds, [&](size_t c, const std::string& what) {
+        std::fprintf(stderr, "sdsp_analyze_batch: %s\n", what.c_str());
+        mark_failed(c, what);
+    });
+    stg.clear();
+    return failed ? SDSP_ERR_PROCESSING : SDSP_OK;
 }
 
 int32_t sdsp_analyze_audio(const float* samples, uint64_t n_samples, uint32_t sample_rate, const sdsp_config* cfg,

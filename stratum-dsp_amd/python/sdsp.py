@@ -52,6 +52,10 @@ def lib():
         L.sdsp_analyze_batch_device.argtypes = [C.c_void_p, u64p, u64p, C.c_uint64, C.c_uint32, C.POINTER(SdspConfig),
                                                 C.c_int32, C.c_void_p, C.POINTER(SdspResult)]
         L.sdsp_analyze_batch_device.restype = C.c_int32
+        L.sdsp_analyze_batch_device_ex.argtypes = [C.c_void_p, u64p, u64p, C.c_uint64, C.c_uint32,
+                                                   C.POINTER(SdspConfig), C.c_int32, C.c_void_p, C.c_int32,
+                                                   C.POINTER(SdspResult)]
+        L.sdsp_analyze_batch_device_ex.restype = C.c_int32
         L.sdsp_result_free.argtypes = [C.POINTER(SdspResult)]
         L.sdsp_generate_synthetic.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64, C.c_int32,
                                               C.c_int32, C.c_void_p, fp, C.POINTER(C.c_int32)]
@@ -218,17 +222,23 @@ class ResultBatch:
             pass
 
 
-def analyze_batch_device(d_ptr, offsets, lens, sample_rate=44100, config=None, device=0, stream=None, raw=False):
+STAGES_FULL = 0
+STAGES_BPM_ONLY = 1  # stages a1-a19 (src/lib.rs:86-910): no key path, no beat grid
+
+
+def analyze_batch_device(d_ptr, offsets, lens, sample_rate=44100, config=None, device=0, stream=None, raw=False,
+                         stages=STAGES_FULL):
     """Tracks already resident in HBM (d_ptr: device address).  Returns a list of results
-    (dicts / AnalysisError), or with raw=True the native ResultBatch."""
+    (dicts / AnalysisError), or with raw=True the native ResultBatch.  stages=STAGES_BPM_ONLY runs
+    the tempo path alone (sdsp_analyze_batch_device_ex)."""
     offs = np.ascontiguousarray(offsets, dtype=np.uint64)
     ln = np.ascontiguousarray(lens, dtype=np.uint64)
     n = ln.size
     outs = (SdspResult * n)()
     cfg = config if config is not None else default_config()
-    st = lib().sdsp_analyze_batch_device(C.c_void_p(d_ptr), offs.ctypes.data_as(C.POINTER(C.c_uint64)),
-                                         ln.ctypes.data_as(C.POINTER(C.c_uint64)), n, sample_rate, C.byref(cfg),
-                                         device, C.c_void_p(stream or 0), outs)
+    st = lib().sdsp_analyze_batch_device_ex(C.c_void_p(d_ptr), offs.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                            ln.ctypes.data_as(C.POINTER(C.c_uint64)), n, sample_rate, C.byref(cfg),
+                                            device, C.c_void_p(stream or 0), stages, outs)
     if st != 0:
         raise AnalysisError(st, _batch_error(outs, n, "device batch failed"))
     batch = ResultBatch(outs, n)

@@ -64,3 +64,48 @@ def test_bench_launcher_world2_dry_run():
     assert d["scaling"] == "weak" and d["higher_is_better"] is True
     assert abs(d["value"] - 4 * 2 * 2 / (d["ms_per_step"] * 2 / 1000.0)) / d["value"] < 1e-2
     assert d["config"]["parallelism"].startswith("track-sharded x2")
+
+
+def _bench_json(cmd):
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout  # rank 0 only
+    return json.loads(lines[0])
+
+
+def test_bench_spawns_ranks_without_torchrun():
+    """`python bench.py --gpus 2` (the driver's plain invocation) starts its own 2 rank processes."""
+    d = _bench_json([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+                     "--tracks", "3", "--seconds", "1", "--dry-run"])
+    assert d["n_gpus"] == 2 and d["steps"] == 2
+    assert d["config"]["parallelism"].startswith("track-sharded x2")
+    assert d["config"]["baseline_config"] == 3
+    assert abs(d["value"] - 3 * 2 * 2 / (d["ms_per_step"] * 2 / 1000.0)) / d["value"] < 1e-2
+    assert len(d["step_ms"]["all"]) == 2
+
+
+@pytest.mark.parametrize("workload,cfg", [("mixed", 4), ("bpm-only", 5)])
+def test_bench_workloads_dry_run(workload, cfg):
+    d = _bench_json([sys.executable, os.path.join(ROOT, "bench.py"), "--workload", workload, "--steps", "1",
+                     "--warmup", "0", "--tracks", "5", "--dry-run"])
+    assert d["n_gpus"] == 1 and d["config"]["baseline_config"] == cfg
+    assert d["config"]["stages"] == ("bpm-only (a1-a19)" if workload == "bpm-only" else "full")
+
+
+def test_mixed_lengths_are_config4():
+    sys.path.insert(0, ROOT)
+    import bench
+
+    a = bench.track_lengths("mixed", 2000, 180.0, 44100, 0)
+    assert a.min() >= 30 * 44100 and a.max() <= 600 * 44100 and (a % 44100 == 0).all()
+    assert len(set((a // 44100).tolist())) > 400  # spread over the whole range
+    b = bench.track_lengths("mixed", 2000, 180.0, 44100, 2000)
+    assert not (a == b).all()  # ranks draw different tracks
+
+
+def test_gpus_world_mismatch_is_an_error():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run", "--tracks", "2",
+                          "--seconds", "1"], capture_output=True, text=True, timeout=120, cwd=ROOT, env=env)
+    assert out.returncode != 0 and "WORLD_SIZE" in out.stderr
