@@ -29,6 +29,23 @@
  *        X[k] = E + rt[k] * O,  rt[k] = e^{-2 pi i k/N}
  *     |X[k]| = sqrt(X.re*X.re + X.im*X.im);  power = X.re*X.re + X.im*X.im.
  *
+ * STFT section (round 2; the spectrogram FFTs of compute_stft only -- the tempogram and
+ * autocorrelation FFTs keep the general section above).  Same Stockham radix-4 (+ radix-2)
+ * stages and tables, with
+ *   - complex products in FMA form: (w * z) = (fma(w.re, z.re, -(w.im*z.im)),
+ *                                             fma(w.re, z.im, w.im*z.re));
+ *   - no products for the p = 0 butterflies (W^0 = 1): y1 = amc + jbmd, y2 = apc - bpd,
+ *     y3 = amc - jbmd;
+ *   - post-processing for k = 0..M, with Zk = Z[k mod M], Zr = Z[(M-k) mod M]:
+ *        S = (Zk.re + Zr.re, Zk.im - Zr.im)              (Zk + conj(Zr))
+ *        D' = (Zk.im + Zr.im, -(Zk.re - Zr.re))          (-i (Zk - conj(Zr)))
+ *        Y.re = fma(rt.re, D'.re, fma(-rt.im, D'.im, S.re))
+ *        Y.im = fma(rt.re, D'.im, fma(rt.im, D'.re, S.im))
+ *        |X[k]| = 0.5 * sqrt(fma(Y.re, Y.re, Y.im * Y.im))    (X = Y / 2; sqrt correctly rounded)
+ * FMA is a single rounding on both sides (gfx950 v_fma_f32 / x86 vfmadd), so the STFT stays
+ * bit-identical between the CPU restatement and the kernels, at about two thirds of the
+ * general section's arithmetic.  tests/test_spec.py checks it against numpy float64 too.
+ *
  * Twiddles are cos/sin evaluated in double by sdsp_libm and rounded once to f32.  Both the
  * CPU restatement (oracle/) and the HIP kernels implement exactly this operation order, so
  * their spectra agree bit for bit; tests/test_oracle_fft.py checks the specification

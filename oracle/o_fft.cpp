@@ -1,7 +1,11 @@
 // o_fft.cpp — FFTs and the STFT of the reference path (TEST INFRASTRUCTURE, see oracle_internal.hpp).
 //
 // compute_stft follows src/features/chroma/extractor.rs:301-359; the FFT arithmetic is the
-// sdsp specification (include/sdsp_fft_spec.h) standing in for rustfft "6.2".
+// sdsp specification (include/sdsp_fft_spec.h) standing in for rustfft "6.2": its STFT section
+// for the spectrogram (stft_mag), its general section for the tempogram / autocorrelation FFTs
+// (fft_complex, rfft).
+#include <cmath>
+#include <cstring>
 #include <map>
 #include <mutex>
 
@@ -107,6 +111,79 @@ void rfft(const float* x, size_t n, std::vector<Cx>& out) {
     }
 }
 
+// ---- STFT section of sdsp_fft_spec.h (the spectrogram FFTs only) ----
+static inline Cx cmulf(Cx w, Cx z) {
+    return {std::fma(w.re, z.re, -(w.im * z.im)), std::fma(w.re, z.im, w.im * z.re)};
+}
+
+// Stockham radix-4 (+ one radix-2) DIF with FMA complex products; the p = 0 butterflies carry
+// no products (W^0 = 1).
+static void stft_fft_complex(std::vector<Cx>& x, std::vector<Cx>& y) {
+    const size_t M = x.size();
+    if (M <= 1) return;
+    if (M & (M - 1)) throw std::runtime_error("fft size must be a power of two");
+    const std::vector<Cx>& tw = twiddles(M);
+    y.resize(M);
+    Cx* src = x.data();
+    Cx* dst = y.data();
+    size_t n = M, s = 1;
+    while (n >= 4) {
+        const size_t m = n / 4;
+        const size_t tstep = M / n;
+        for (size_t p = 0; p < m; p++) {
+            const Cx w1 = tw[1 * p * tstep];
+            const Cx w2 = tw[2 * p * tstep];
+            const Cx w3 = tw[3 * p * tstep];
+            for (size_t q = 0; q < s; q++) {
+                const Cx a = src[q + s * (p)];
+                const Cx b = src[q + s * (p + m)];
+                const Cx c = src[q + s * (p + 2 * m)];
+                const Cx d = src[q + s * (p + 3 * m)];
+                const Cx apc = cadd(a, c), amc = csub(a, c), bpd = cadd(b, d), bmd = csub(b, d);
+                const Cx t1 = {amc.re + bmd.im, amc.im - bmd.re};  // amc + (-i)(b - d)
+                const Cx t2 = csub(apc, bpd);
+                const Cx t3 = {amc.re - bmd.im, amc.im + bmd.re};  // amc - (-i)(b - d)
+                dst[q + s * (4 * p + 0)] = cadd(apc, bpd);
+                dst[q + s * (4 * p + 1)] = p ? cmulf(w1, t1) : t1;
+                dst[q + s * (4 * p + 2)] = p ? cmulf(w2, t2) : t2;
+                dst[q + s * (4 * p + 3)] = p ? cmulf(w3, t3) : t3;
+            }
+        }
+        n = m;
+        s *= 4;
+        std::swap(src, dst);
+    }
+    if (n == 2) {
+        for (size_t q = 0; q < s; q++) {
+            const Cx a = src[q], b = src[q + s];
+            dst[q] = cadd(a, b);
+            dst[q + s] = csub(a, b);
+        }
+        std::swap(src, dst);
+    }
+    if (src != x.data()) std::memcpy(x.data(), src, M * sizeof(Cx));
+}
+
+// |X[k]|, k = 0..n/2, of a real frame of n samples: z[j] = (x[2j], x[2j+1]), Z = FFT_M(z),
+// S = Z[k] + conj(Z[M-k]), D' = -i (Z[k] - conj(Z[M-k])), Y = S + rt[k] D' (two FMAs per
+// component), |X[k]| = 0.5 * sqrt(fma(Y.re, Y.re, Y.im * Y.im)).
+static void stft_mag(const float* x, size_t n, float* mag, std::vector<Cx>& z, std::vector<Cx>& tmp) {
+    const size_t M = n / 2;
+    z.resize(M);
+    for (size_t j = 0; j < M; j++) z[j] = {x[2 * j], x[2 * j + 1]};
+    stft_fft_complex(z, tmp);
+    const std::vector<Cx>& rt = rtwiddles(n);
+    for (size_t k = 0; k <= M; k++) {
+        const Cx Zk = z[k % M];
+        const Cx Zr = z[(M - k) % M];
+        const float sre = Zk.re + Zr.re, sim = Zk.im - Zr.im;
+        const float dre = Zk.im + Zr.im, dim = -(Zk.re - Zr.re);
+        const float yre = std::fma(rt[k].re, dre, std::fma(-rt[k].im, dim, sre));
+        const float yim = std::fma(rt[k].re, dim, std::fma(rt[k].im, dre, sim));
+        mag[k] = 0.5f * std::sqrt(std::fma(yre, yre, yim * yim));
+    }
+}
+
 // extractor.rs:301-359
 Spec compute_stft(const float* s, size_t n_samples, size_t frame_size, size_t hop) {
     Spec out;
@@ -119,13 +196,11 @@ Spec compute_stft(const float* s, size_t n_samples, size_t frame_size, size_t ho
     out.bins = n_bins;
     out.d.resize(n_frames * n_bins);
     std::vector<float> buf(frame_size);
-    std::vector<Cx> X;
+    std::vector<Cx> z, tmp;
     for (size_t f = 0; f < n_frames; f++) {
         const float* fr = s + f * hop;
         for (size_t i = 0; i < frame_size; i++) buf[i] = fr[i] * window[i];
-        rfft(buf.data(), frame_size, X);
-        float* row = out.row(f);
-        for (size_t k = 0; k < n_bins; k++) row[k] = __builtin_sqrtf(X[k].re * X[k].re + X[k].im * X[k].im);
+        stft_mag(buf.data(), frame_size, out.row(f), z, tmp);
     }
     return out;
 }

@@ -1,24 +1,30 @@
 // k_stft.hip — batched real-input STFT magnitudes for gfx950 (replaces compute_stft,
 // reference src/features/chroma/extractor.rs:301-359, whose FFT is rustfft).
 //
-// Arithmetic: exactly sdsp_fft_spec.h (Stockham radix-4 DIF stages, real-FFT post-twiddle),
-// so the spectra are bit-identical to the CPU restatement.  Data movement: two consecutive
-// radix-4 stages touch a closed set of 16 elements (stage (n, s) butterflies
-// p = p' + j'*n/16, j' = 0..3, feed stage (n/4, 4s) butterflies q + s*jA), so each thread
-// runs both stages on 16 values held in registers ("radix-16 pass"): one LDS round trip per
-// two stages instead of one per stage.
+// Arithmetic: exactly the STFT section of sdsp_fft_spec.h (Stockham radix-4 DIF stages with FMA
+// complex products and no W^0 products, then the real-FFT post-processing in FMA form), so the
+// spectra are bit-identical to the CPU restatement.  Data movement: two consecutive radix-4
+// stages touch a closed set of 16 elements (stage (n, s) butterflies p = p' + j'*n/16,
+// j' = 0..3, feed stage (n/4, 4s) butterflies q + s*jA), so each thread runs both stages on 16
+// values held in registers ("radix-16 pass"): one LDS round trip per two stages instead of one
+// per stage.
 //
 //   N = 8192 (M = 4096 = 16^3):       3 radix-16 passes, 256 threads per frame
 //   N = 2048 (M = 1024 = 16^2 * 4):   2 radix-16 passes + 1 radix-4 pass, 64 threads (one
 //                                     wave) per frame, 4 frames per workgroup
 //
 // Instruction economy (the kernel is VALU-bound):
-//  * complex values are 2-wide vectors, so every complex add / scale is one v_pk_* op and
-//    the -i rotation and conjugations fold into the packed ops' swizzle / negate modifiers;
+//  * complex values are pairs of scalar f32 registers.  gfx950's packed f32 ops (v_pk_*) issue
+//    at the same flop rate as scalar ones but add a wait state between dependent packed ops, and
+//    the -i rotations / conjugations cost extra moves in packed form; scalar code folds them into
+//    the adds.  A complex product is 2 v_mul + 2 v_fma;
+//  * the W^0 products the spec omits are skipped at compile time where the twiddle is
+//    wave-uniform (the last pass); where it is per lane (lanes with p = 0 in passes 1-2) the
+//    per-thread table holds exactly (1, +0), whose FMA product equals the operand;
 //  * the frame, the window and the per-thread twiddle tables are read with buffer loads
 //    whose per-element offsets are scalar (SGPR) constants, so no VALU address arithmetic;
 //  * every LDS index is (per-thread base) + (compile-time constant);
-//  * bins k and M-k share one LDS read and one E/O evaluation; |X| uses the exact fast sqrt.
+//  * bins k and M-k share one LDS read and one S/D evaluation; |X| uses the exact fast sqrt.
 // The twiddle values are those of sdsp_fft_spec.h, re-laid out per thread on the host
 // (stft_tables below).  LDS index padding i + i/16 keeps the strided pass-1 stores
 // near conflict-free.
@@ -33,10 +39,13 @@
 
 namespace sdsp {
 
-typedef float f2 __attribute__((ext_vector_type(2)));
+// one complex value: two scalar registers; 8-byte aligned so LDS moves are ds_*_b64
+struct __attribute__((aligned(8))) c2 {
+    float x, y;
+};
 
-__device__ __forceinline__ f2 ld_f2(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
-    return __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+__device__ __forceinline__ c2 ld_c2(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+    return __builtin_bit_cast(c2, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
 }
 // buffer resource over [p, p+bytes) for a wave-uniform pointer
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p, uint32_t bytes) {
@@ -46,22 +55,29 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p, uint32_
     return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, bytes, 0x00020000);
 }
 
-// complex ops on (re, im) pairs; the same IEEE operations in the same order as cadd/csub/cmul
-__device__ __forceinline__ f2 vmul(f2 w, f2 z) {  // (w.re z.re - w.im z.im, w.re z.im + w.im z.re)
-    const f2 t1 = w.xx * z;
-    const f2 t2 = w.yy * z.yx;
-    return t1 + f2{-t2.x, t2.y};
+// the spec's complex product: (fma(w.re, z.re, -(w.im z.im)), fma(w.re, z.im, w.im z.re))
+__device__ __forceinline__ c2 cmulf(c2 w, c2 z) {
+    return {__builtin_fmaf(w.x, z.x, -(w.y * z.y)), __builtin_fmaf(w.x, z.y, w.y * z.x)};
 }
 
-// radix-4 butterfly of sdsp_fft_spec.h
-__device__ __forceinline__ void bfly4(f2 a, f2 b, f2 c, f2 d, f2 w1, f2 w2, f2 w3, f2& y0, f2& y1, f2& y2, f2& y3) {
-    const f2 apc = a + c, amc = a - c;
-    const f2 bpd = b + d, bmd = b - d;
-    const f2 jbmd = {bmd.y, -bmd.x};  // -i (b - d)
-    y0 = apc + bpd;
-    y1 = vmul(w1, amc + jbmd);
-    y2 = vmul(w2, apc - bpd);
-    y3 = vmul(w3, amc - jbmd);
+// radix-4 butterfly of sdsp_fft_spec.h; TW = false: p = 0, no products
+template <bool TW>
+__device__ __forceinline__ void bfly4(c2 a, c2 b, c2 c, c2 d, c2 w1, c2 w2, c2 w3, c2& y0, c2& y1, c2& y2, c2& y3) {
+    const c2 apc = {a.x + c.x, a.y + c.y}, amc = {a.x - c.x, a.y - c.y};
+    const c2 bpd = {b.x + d.x, b.y + d.y}, bmd = {b.x - d.x, b.y - d.y};
+    const c2 t1 = {amc.x + bmd.y, amc.y - bmd.x};  // amc + (-i)(b - d)
+    const c2 t2 = {apc.x - bpd.x, apc.y - bpd.y};
+    const c2 t3 = {amc.x - bmd.y, amc.y + bmd.x};  // amc - (-i)(b - d)
+    y0 = {apc.x + bpd.x, apc.y + bpd.y};
+    if constexpr (TW) {
+        y1 = cmulf(w1, t1);
+        y2 = cmulf(w2, t2);
+        y3 = cmulf(w3, t3);
+    } else {
+        y1 = t1;
+        y2 = t2;
+        y3 = t3;
+    }
 }
 
 #ifdef SDSP_EXP_NOPAD
@@ -114,16 +130,23 @@ __device__ __forceinline__ float sqrt_cr(float x) {
 // Two radix-4 stages, (n, s) then (n/4, 4s), on v[j' + 4j] = x[q + s(p' + (n/16)(j' + 4j))].
 // On return v[jA + 4jB] = z[q + 16 s p' + s(jA + 4jB)].  w[0..11] = stage-A twiddles
 // W^{jA (p' + j' n/16) M/n} at index 3 j' + jA - 1, w[12..14] = stage-B W^{jB p' 4M/n}.
-__device__ __forceinline__ void radix16(f2 v[16], const f2 w[15]) {
-    f2 u[16];
+// LAST (p' = 0 for every lane, the last pass): stage A's j' = 0 butterfly and all of stage B
+// have p = 0, so they carry no products.
+template <bool LAST>
+__device__ __forceinline__ void radix16(c2 v[16], const c2 w[15]) {
+    c2 u[16];
 #pragma unroll
-    for (int jp = 0; jp < 4; jp++)
-        bfly4(v[jp], v[jp + 4], v[jp + 8], v[jp + 12], w[3 * jp + 0], w[3 * jp + 1], w[3 * jp + 2], u[jp * 4 + 0],
-              u[jp * 4 + 1], u[jp * 4 + 2], u[jp * 4 + 3]);
+    for (int jp = 0; jp < 4; jp++) {
+        if (LAST && jp == 0)
+            bfly4<false>(v[0], v[4], v[8], v[12], w[0], w[0], w[0], u[0], u[1], u[2], u[3]);
+        else
+            bfly4<true>(v[jp], v[jp + 4], v[jp + 8], v[jp + 12], w[3 * jp + 0], w[3 * jp + 1], w[3 * jp + 2],
+                        u[jp * 4 + 0], u[jp * 4 + 1], u[jp * 4 + 2], u[jp * 4 + 3]);
+    }
 #pragma unroll
     for (int ja = 0; ja < 4; ja++)
-        bfly4(u[0 * 4 + ja], u[1 * 4 + ja], u[2 * 4 + ja], u[3 * 4 + ja], w[12], w[13], w[14], v[ja + 0], v[ja + 4],
-              v[ja + 8], v[ja + 12]);
+        bfly4<!LAST>(u[0 * 4 + ja], u[1 * 4 + ja], u[2 * 4 + ja], u[3 * 4 + ja], w[12], w[13], w[14], v[ja + 0],
+                     v[ja + 4], v[ja + 8], v[ja + 12]);
 }
 
 template <int M>
@@ -149,7 +172,7 @@ __global__ __launch_bounds__(256) STFT_ATTR void k_stft_mag(const float* __restr
     constexpr int FPB = 256 / TPF;    // frames per workgroup
     constexpr int PADM = M + PADSHIFT * M / 16;  // padded LDS slots per frame
     static_assert(S::NPASS > 0, "supported sizes: N = 2048, 8192");
-    __shared__ f2 lds[FPB * PADM];
+    __shared__ c2 lds[FPB * PADM];
     __shared__ float red[4];
 
     const int lt = threadIdx.x % TPF;  // thread within frame
@@ -160,24 +183,24 @@ __global__ __launch_bounds__(256) STFT_ATTR void k_stft_mag(const float* __restr
     const int trk = find_track(frame_pfx, n_tracks, gg);
     const uint64_t f = gg - frame_pfx[trk];
     const float gn = gain[trk];
-    f2* buf = lds + fl * PADM;
+    c2* buf = lds + fl * PADM;
     const __amdgpu_buffer_rsrc_t rx = rsrc_of(samples + src_off[trk] + f * (uint64_t)hop, 4u * NFFT);
     const __amdgpu_buffer_rsrc_t rw = rsrc_of(window, 4u * NFFT);
     const __amdgpu_buffer_rsrc_t rtw = rsrc_of(twp, 8u * 15u * (TPF + TPF / 16 + 1));
     const __amdgpu_buffer_rsrc_t rrt = rsrc_of(rtp, 8u * (S::RT_SPECIAL + 4));
     const int vo = 8 * lt;  // every table below is [item][lane] with 8-byte entries
 
-    f2 v[16], w[15];
+    c2 v[16], w[15];
     // pass 1 (n = M, s = 1, p' = lt): z[idx] = (x[2idx], x[2idx+1]) * gain * window, idx = lt + TPF k
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        const f2 xs = ld_f2(rx, vo, 8 * TPF * k);
-        const f2 ws = ld_f2(rw, vo, 8 * TPF * k);
-        v[k] = (xs * gn) * ws;
+        const c2 xs = ld_c2(rx, vo, 8 * TPF * k);
+        const c2 ws = ld_c2(rw, vo, 8 * TPF * k);
+        v[k] = {(xs.x * gn) * ws.x, (xs.y * gn) * ws.y};
     }
 #pragma unroll
-    for (int j = 0; j < 15; j++) w[j] = ld_f2(rtw, vo, 8 * TPF * j);
-    radix16(v, w);
+    for (int j = 0; j < 15; j++) w[j] = ld_c2(rtw, vo, 8 * TPF * j);
+    radix16<false>(v, w);
     {
         const int b0 = P17 * lt;  // lpad(16 lt + k) = 17 lt + k
 #pragma unroll
@@ -197,16 +220,19 @@ __global__ __launch_bounds__(256) STFT_ATTR void k_stft_mag(const float* __restr
             // pass 1: one entry per p' (TPF/16 of them, shared by 16 lanes); pass 2: p' = 0 for
             // every lane, so the 15 twiddles are wave-uniform scalar loads
             if (pass == 1)
-                w[j] = ld_f2(rtw, 8 * pp, 8 * (15 * TPF + j * (TPF / 16)));
+                w[j] = ld_c2(rtw, 8 * pp, 8 * (15 * TPF + j * (TPF / 16)));
             else {
                 const cx t = twp[15 * TPF + 15 * (TPF / 16) + j];
-                w[j] = f2{t.re, t.im};
+                w[j] = c2{t.re, t.im};
             }
         }
 #pragma unroll
         for (int k = 0; k < 16; k++) v[k] = buf[rb + rs * k];
         frame_sync<TPF>();
-        radix16(v, w);
+        if (pass == 2)
+            radix16<true>(v, w);
+        else
+            radix16<false>(v, w);
         // writes z[q + 16 s pp + s k]:  s = 16 -> (q + 272 pp) + 17 k;  s = 256 (pp = 0) -> lpad(q) + 272 k
         if (s == 16) {
             const int wb = q + P272 * pp;
@@ -218,16 +244,15 @@ __global__ __launch_bounds__(256) STFT_ATTR void k_stft_mag(const float* __restr
         }
         frame_sync<TPF>();
     }
-    // trailing radix-4 stage (M = 16^2 * 4): n = 4, s = M/4, p = 0, twiddles tw[0]
+    // trailing radix-4 stage (M = 16^2 * 4): n = 4, s = M/4, p = 0 (no products)
     if constexpr (M == 1024) {
         constexpr int s = M / 4;
-        const f2 w0 = ld_f2(rrt, 0, 8 * (S::RT_SPECIAL + 3));
 #pragma unroll
         for (int r = 0; r < s / TPF; r++) {
             const int q = lt + TPF * r;
             const int b = lpad(q);  // lpad(q + j s) = b + 272 j (s = 256)
-            f2 y0, y1, y2, y3;
-            bfly4(buf[b], buf[b + P272], buf[b + 2 * P272], buf[b + 3 * P272], w0, w0, w0, y0, y1, y2, y3);
+            c2 y0, y1, y2, y3;
+            bfly4<false>(buf[b], buf[b + P272], buf[b + 2 * P272], buf[b + 3 * P272], c2{}, c2{}, c2{}, y0, y1, y2, y3);
             buf[b] = y0;
             buf[b + P272] = y1;
             buf[b + 2 * P272] = y2;
@@ -235,53 +260,54 @@ __global__ __launch_bounds__(256) STFT_ATTR void k_stft_mag(const float* __restr
         }
         frame_sync<TPF>();
     }
-    // real-FFT post-processing, |X[k]|, k = 0..M.  Bins k and M-k read the same pair
-    // (Z[k], Z[M-k]); the partner's E and O are the conjugates of this bin's (exactly, up to
-    // the sign of zero, which |X| cannot see), so each pair is read and combined once.
+    // real-FFT post-processing, |X[k]|, k = 0..M (sdsp_fft_spec.h, STFT section):
+    //   S = Z[k] + conj(Z[M-k]),  D = Z[k] - conj(Z[M-k]),  D' = (D.im, -D.re),
+    //   Y = S + rt[k] D' in FMA form,  |X[k]| = 0.5 * sqrt(fma(Y.re, Y.re, Y.im * Y.im)).
+    // Bins k and M-k read the same pair (Z[k], Z[M-k]); the partner's S and D' are the
+    // conjugates of this bin's (exactly, up to the sign of zero, which |X| cannot see), so each
+    // pair is read and combined once.
     float* out = mags + (mag_row0[trk] + f) * (uint64_t)stride;
     float mx = 0.0f;
-    auto mag_of = [&](f2 E, f2 O, f2 wt) {
-        const f2 X = E + vmul(wt, O);
-        const f2 sq = X * X;
-        return sqrt_cr(sq.x + sq.y);
+    auto mag_of = [&](float sx, float sy, float dx, float dy, c2 wt) {  // S = (sx, sy), D' = (dx, dy)
+        const float yx = __builtin_fmaf(wt.x, dx, __builtin_fmaf(-wt.y, dy, sx));
+        const float yy = __builtin_fmaf(wt.x, dy, __builtin_fmaf(wt.y, dx, sy));
+        return 0.5f * sqrt_cr(__builtin_fmaf(yx, yx, yy * yy));
     };
     auto put = [&](int k, float mag) {
         if (live) out[k] = mag;
         if (FRAME_MAX) mx = sd_maxf(mx, mag);
     };
-    auto pair_eo = [&](int ik, int ir, f2& E, f2& O) {  // LDS indices of Z[k], Z[M-k]
-        const f2 Zk = buf[ik];
-        const f2 Zr = buf[ir];
-        const f2 Zc = {Zr.x, -Zr.y};
-        E = (Zk + Zc) * 0.5f;
-        const f2 D = Zk - Zc;
-        O = f2{D.y * 0.5f, -(D.x * 0.5f)};
+    struct SD {
+        float sx, sy, dx, dy;
     };
-    f2 wk[S::NPAIR], wm[S::NPAIR];
+    auto pair_sd = [&](int ik, int ir) {  // LDS indices of Z[k], Z[M-k]
+        const c2 Zk = buf[ik];
+        const c2 Zr = buf[ir];
+        // S = Zk + conj(Zr);  D = Zk - conj(Zr);  D' = (D.im, -D.re)
+        return SD{Zk.x + Zr.x, Zk.y - Zr.y, Zk.y + Zr.y, -(Zk.x - Zr.x)};
+    };
+    c2 wk[S::NPAIR], wm[S::NPAIR];
 #pragma unroll
     for (int j = 0; j < S::NPAIR; j++) {
-        wk[j] = ld_f2(rrt, vo, 8 * TPF * (2 * j));
-        wm[j] = ld_f2(rrt, vo, 8 * TPF * (2 * j + 1));
+        wk[j] = ld_c2(rrt, vo, 8 * TPF * (2 * j));
+        wm[j] = ld_c2(rrt, vo, 8 * TPF * (2 * j + 1));
     }
 #pragma unroll
     for (int j = 0; j < S::NPAIR; j++) {
         const int k = 1 + lt + TPF * j;  // k < M/2 except possibly on the last j
         if (j + 1 < S::NPAIR || k < M / 2) {
-            f2 E, O;
-            pair_eo(lpad(k), lpad(M - k), E, O);
-            put(k, mag_of(E, O, wk[j]));
-            put(M - k, mag_of(f2{E.x, -E.y}, f2{O.x, -O.y}, wm[j]));
+            const SD a = pair_sd(lpad(k), lpad(M - k));
+            put(k, mag_of(a.sx, a.sy, a.dx, a.dy, wk[j]));
+            put(M - k, mag_of(a.sx, -a.sy, a.dx, -a.dy, wm[j]));
         }
     }
     if (lt == 0) {  // k = 0 and k = M both read (Z[0], Z[0]); k = M/2 reads (Z[M/2], Z[M/2])
-        f2 E, O;
-        pair_eo(0, 0, E, O);
-        put(0, mag_of(E, O, ld_f2(rrt, 0, 8 * S::RT_SPECIAL)));
-        put(M, mag_of(E, O, ld_f2(rrt, 0, 8 * (S::RT_SPECIAL + 1))));
+        const SD a = pair_sd(0, 0);
+        put(0, mag_of(a.sx, a.sy, a.dx, a.dy, ld_c2(rrt, 0, 8 * S::RT_SPECIAL)));
+        put(M, mag_of(a.sx, a.sy, a.dx, a.dy, ld_c2(rrt, 0, 8 * (S::RT_SPECIAL + 1))));
     } else if (lt == 1) {
-        f2 E, O;
-        pair_eo(lpad(M / 2), lpad(M / 2), E, O);
-        put(M / 2, mag_of(E, O, ld_f2(rrt, 0, 8 * (S::RT_SPECIAL + 2))));
+        const SD a = pair_sd(lpad(M / 2), lpad(M / 2));
+        put(M / 2, mag_of(a.sx, a.sy, a.dx, a.dy, ld_c2(rrt, 0, 8 * (S::RT_SPECIAL + 2))));
     }
     if (FRAME_MAX) {
         if constexpr (TPF == 64) {
@@ -315,6 +341,7 @@ void stft_tables(int N, const std::vector<float>& tw, const std::vector<float>& 
         (*v)[2 * i] = src[0];
         (*v)[2 * i + 1] = src[1];
     };
+    static const float one[2] = {1.0f, 0.0f};  // a p = 0 twiddle: the FMA product is the operand
     size_t len = 0;
     for (int pass = 0, s = 1; pass < npass; pass++, s *= 16) len += (size_t)15 * (TPF / s);
     twp->assign(2 * len, 0.0f);
@@ -324,9 +351,10 @@ void stft_tables(int N, const std::vector<float>& tw, const std::vector<float>& 
         for (int pp = 0; pp < npp; pp++) {
             for (int jp = 0; jp < 4; jp++)
                 for (int ja = 1; ja <= 3; ja++)
-                    put(twp, base + (size_t)(3 * jp + ja - 1) * npp + pp, &tw[2 * (size_t)(ja * (pp + jp * m1) * tA)]);
+                    put(twp, base + (size_t)(3 * jp + ja - 1) * npp + pp,
+                        pp + jp * m1 == 0 ? one : &tw[2 * (size_t)(ja * (pp + jp * m1) * tA)]);
             for (int jb = 1; jb <= 3; jb++)
-                put(twp, base + (size_t)(12 + jb - 1) * npp + pp, &tw[2 * (size_t)(jb * pp * tB)]);
+                put(twp, base + (size_t)(12 + jb - 1) * npp + pp, pp == 0 ? one : &tw[2 * (size_t)(jb * pp * tB)]);
         }
         base += (size_t)15 * npp;
     }

@@ -20,13 +20,13 @@ pytestmark = pytest.mark.gpu
 
 
 def _device_tracks(lens, seed0, bpm_mode=0):
+    """Track i is the first lens[i] samples of synthetic track seed0 + i (one generator call, so
+    bpm_mode 1 cycles through its three BPM ranges)."""
     lens = np.asarray(lens, dtype=np.uint64)
-    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
-    buf = sdsp.DeviceBuffer(int(lens.sum()))
-    for i, (o, n) in enumerate(zip(offs, lens)):
-        if n == 0:
-            continue
-        sdsp.generate_synthetic(buf.ptr + 4 * int(o), 1, int(n), seed0=seed0 + i, bpm_mode=bpm_mode)
+    Lmax = int(max(int(lens.max()), 1))
+    buf = sdsp.DeviceBuffer(len(lens) * Lmax)
+    sdsp.generate_synthetic(buf.ptr, len(lens), Lmax, seed0=seed0, bpm_mode=bpm_mode)
+    offs = (np.arange(len(lens)) * Lmax).astype(np.uint64)
     return buf, offs, lens
 
 

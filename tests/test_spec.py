@@ -77,8 +77,11 @@ def test_rfft(N):
     assert np.max(np.abs(got - want)) <= 2e-6 * np.max(np.abs(want)) * np.log2(N)
 
 
-@pytest.mark.parametrize("nfft,hop", [(2048, 512), (8192, 512), (2048, 256)])
+@pytest.mark.parametrize("nfft,hop", [(2048, 512), (8192, 512), (2048, 256), (512, 128), (1024, 256), (4096, 1024),
+                                      (16384, 4096)])
 def test_stft_magnitudes(nfft, hop):
+    """The STFT section of the spec (FMA complex products, no W^0 products, post-processing in
+    FMA form; radix-2 last stage when log2(N/2) is odd)."""
     x = (0.5 * np.sin(2 * np.pi * 440.0 * np.arange(nfft * 4) / 44100.0) + 0.1 * RNG.standard_normal(nfft * 4))
     x = x.astype(np.float32)
     got = oracle.stft(x, nfft, hop)
@@ -91,6 +94,17 @@ def test_stft_magnitudes(nfft, hop):
         seg = (x[f * hop:f * hop + nfft] * w).astype(np.float64)
         want = np.abs(np.fft.rfft(seg))
         assert np.max(np.abs(got[f] - want)) <= 2e-6 * np.max(want) * np.log2(nfft)
+
+
+def test_stft_silence_and_tiny_frames():
+    """Digital silence gives exact zeros; frames of subnormal-scale samples stay finite and
+    non-negative (the GPU's fast sqrt takes its general path there)."""
+    n = 8192 * 3
+    x = np.zeros(n, np.float32)
+    x[8192:16384] = (RNG.standard_normal(8192) * 1e-38).astype(np.float32)
+    for nfft in (2048, 8192):
+        got = oracle.stft(x, nfft, 512)
+        assert np.all(got[0] == 0.0) and np.all(np.isfinite(got)) and np.all(got >= 0.0)
 
 
 def test_stft_short_input():
