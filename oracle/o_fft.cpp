@@ -166,7 +166,8 @@ static void stft_fft_complex(std::vector<Cx>& x, std::vector<Cx>& y) {
 
 // |X[k]|, k = 0..n/2, of a real frame of n samples: z[j] = (x[2j], x[2j+1]), Z = FFT_M(z),
 // S = Z[k] + conj(Z[M-k]), D' = -i (Z[k] - conj(Z[M-k])), Y = S + rt[k] D' (two FMAs per
-// component), |X[k]| = 0.5 * sqrt(fma(Y.re, Y.re, Y.im * Y.im)).
+// component), |X[k]| = 0.5 * sqrt(fma(Y.re, Y.re, Y.im * Y.im)); the post twiddles are symmetric,
+// rt[M-k] = (-rt[k].re, rt[k].im) for 0 < k < M/2.
 static void stft_mag(const float* x, size_t n, float* mag, std::vector<Cx>& z, std::vector<Cx>& tmp) {
     const size_t M = n / 2;
     z.resize(M);
@@ -176,10 +177,12 @@ static void stft_mag(const float* x, size_t n, float* mag, std::vector<Cx>& z, s
     for (size_t k = 0; k <= M; k++) {
         const Cx Zk = z[k % M];
         const Cx Zr = z[(M - k) % M];
+        // symmetric post twiddles: rt[k] for k <= M/2 and k = M, rt[M-k] := (-rt[k].re, rt[k].im)
+        const Cx w = (k > M / 2 && k < M) ? Cx{-rt[M - k].re, rt[M - k].im} : rt[k];
         const float sre = Zk.re + Zr.re, sim = Zk.im - Zr.im;
         const float dre = Zk.im + Zr.im, dim = -(Zk.re - Zr.re);
-        const float yre = std::fma(rt[k].re, dre, std::fma(-rt[k].im, dim, sre));
-        const float yim = std::fma(rt[k].re, dim, std::fma(rt[k].im, dre, sim));
+        const float yre = std::fma(w.re, dre, std::fma(-w.im, dim, sre));
+        const float yim = std::fma(w.re, dim, std::fma(w.im, dre, sim));
         mag[k] = 0.5f * std::sqrt(std::fma(yre, yre, yim * yim));
     }
 }

@@ -134,6 +134,10 @@ __device__ __forceinline__ float sqrt_cr(float x) {
 // have p = 0, so they carry no products.
 template <bool LAST>
 __device__ __forceinline__ void radix16(c2 v[16], const c2 w[15]) {
+#ifdef SDSP_EXP_NOFFT  // ablation: data movement only
+    for (int k = 0; k < 16; k++) v[k].x += w[k % 15].y;
+    return;
+#endif
     c2 u[16];
 #pragma unroll
     for (int jp = 0; jp < 4; jp++) {
@@ -195,11 +199,20 @@ __global__ __launch_bounds__(256) STFT_ATTR void k_stft_mag(const float* __restr
 #pragma unroll
     for (int k = 0; k < 16; k++) {
         const c2 xs = ld_c2(rx, vo, 8 * TPF * k);
+#ifdef SDSP_EXP_NOTAB  // ablation: no window / twiddle table reads
+        const c2 ws = {1.0f + k, 0.5f};
+#else
         const c2 ws = ld_c2(rw, vo, 8 * TPF * k);
+#endif
         v[k] = {(xs.x * gn) * ws.x, (xs.y * gn) * ws.y};
     }
 #pragma unroll
-    for (int j = 0; j < 15; j++) w[j] = ld_c2(rtw, vo, 8 * TPF * j);
+    for (int j = 0; j < 15; j++)
+#ifdef SDSP_EXP_NOTAB
+        w[j] = c2{0.25f * j, 1.0f - 0.5f * j};
+#else
+        w[j] = ld_c2(rtw, vo, 8 * TPF * j);
+#endif
     radix16<false>(v, w);
     {
         const int b0 = P17 * lt;  // lpad(16 lt + k) = 17 lt + k
@@ -220,7 +233,11 @@ __global__ __launch_bounds__(256) STFT_ATTR void k_stft_mag(const float* __restr
             // pass 1: one entry per p' (TPF/16 of them, shared by 16 lanes); pass 2: p' = 0 for
             // every lane, so the 15 twiddles are wave-uniform scalar loads
             if (pass == 1)
+#ifdef SDSP_EXP_NOTAB
+                w[j] = c2{0.125f * j, 1.0f - 0.25f * j};
+#else
                 w[j] = ld_c2(rtw, 8 * pp, 8 * (15 * TPF + j * (TPF / 16)));
+#endif
             else {
                 const cx t = twp[15 * TPF + 15 * (TPF / 16) + j];
                 w[j] = c2{t.re, t.im};
@@ -271,10 +288,18 @@ __global__ __launch_bounds__(256) STFT_ATTR void k_stft_mag(const float* __restr
     auto mag_of = [&](float sx, float sy, float dx, float dy, c2 wt) {  // S = (sx, sy), D' = (dx, dy)
         const float yx = __builtin_fmaf(wt.x, dx, __builtin_fmaf(-wt.y, dy, sx));
         const float yy = __builtin_fmaf(wt.x, dy, __builtin_fmaf(wt.y, dx, sy));
+#ifdef SDSP_EXP_NOSQRT  // ablation: hardware sqrt, not correctly rounded
+        return 0.5f * __builtin_amdgcn_sqrtf(__builtin_fmaf(yx, yx, yy * yy));
+#else
         return 0.5f * sqrt_cr(__builtin_fmaf(yx, yx, yy * yy));
+#endif
     };
     auto put = [&](int k, float mag) {
+#ifdef SDSP_EXP_NOSTORE  // ablation: no global stores
+        if (live && mag == 1234.5f) out[k] = mag;
+#else
         if (live) out[k] = mag;
+#endif
         if (FRAME_MAX) mx = sd_maxf(mx, mag);
     };
     struct SD {
@@ -289,8 +314,13 @@ __global__ __launch_bounds__(256) STFT_ATTR void k_stft_mag(const float* __restr
     c2 wk[S::NPAIR], wm[S::NPAIR];
 #pragma unroll
     for (int j = 0; j < S::NPAIR; j++) {
+#ifdef SDSP_EXP_NOTAB
+        wk[j] = c2{0.3f * j, 0.7f};
+        wm[j] = c2{0.7f, 0.3f * j};
+#else
         wk[j] = ld_c2(rrt, vo, 8 * TPF * (2 * j));
         wm[j] = ld_c2(rrt, vo, 8 * TPF * (2 * j + 1));
+#endif
     }
 #pragma unroll
     for (int j = 0; j < S::NPAIR; j++) {
@@ -324,6 +354,190 @@ __global__ __launch_bounds__(256) STFT_ATTR void k_stft_mag(const float* __restr
             }
         }
     }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Sliding-strip STFT (the pipeline's kernel for hops that are a multiple of 2*TPF complex
+// values: 8192/512, 8192/1024, 2048/256, 2048/512, 2048/1024).  Same arithmetic as k_stft_mag,
+// different data movement, because the isolated profile of k_stft_mag showed it bound by what it
+// re-reads per frame, not by its arithmetic (window + twiddle tables ~100 KB and
+// the 16x-overlapped samples 32 KB per 8192-point frame, all from L2):
+//  * a strip = up to STRIP_T consecutive frames of one track, processed in order by one
+//    frame-group (8192: the 256-thread workgroup; 2048: one wave);
+//  * window, pass-1 and pass-2 twiddles and post twiddles are loaded into registers once per strip;
+//  * thread lt holds z[lt + TPF k], k = 0..15, of the current frame in a register ring.  The
+//    next frame starts hop/2 = S*TPF complex values later, so its element k is the current
+//    element k + S: the ring shifts by S and only S new values per thread are loaded (prefetched
+//    one frame ahead);
+//  * two LDS buffers: pass 1 writes A, pass 2 reads A and writes B, the last pass runs in place
+//    in B (each thread rewrites the slots it read), the post-processing reads B.  Three barriers
+//    per frame and no barrier between a pass's reads and its writes;
+//  * the STFT post twiddles are the spec's symmetric ones, rt[M-k] = (-rt[k].re, rt[k].im), so
+//    bin M-k needs no table entry of its own.
+constexpr int STRIP_T = 64;
+
+template <int NFFT, int S, bool FRAME_MAX>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_stft_slide(
+    const float* __restrict__ samples, const uint64_t* __restrict__ frame_pfx, const uint64_t* __restrict__ strip_pfx,
+    int n_tracks, uint64_t n_strips, const uint64_t* __restrict__ src_off, const float* __restrict__ gain, int hop,
+    const float* __restrict__ window, const cx* __restrict__ twp, const cx* __restrict__ rtp, float* __restrict__ mags,
+    const uint64_t* __restrict__ mag_row0, int stride, float* __restrict__ frame_max) {
+    constexpr int M = NFFT / 2;
+    using SH = StftShape<M>;
+    constexpr int TPF = SH::TPF;
+    constexpr int FPB = 256 / TPF;               // frame groups (strips) per workgroup
+    constexpr int PADM = M + PADSHIFT * M / 16;  // padded LDS slots per frame buffer
+    static_assert(SH::NPASS > 0 && S >= 1 && S <= 16, "supported: N = 2048, 8192; hop = S * 2 * TPF");
+    __shared__ c2 lds[FPB * 2 * PADM];
+
+    const int lt = threadIdx.x % TPF;
+    const int fl = threadIdx.x / TPF;
+    const uint64_t strip = (uint64_t)xcd_block(blockIdx.x, gridDim.x) * FPB + fl;
+    if (strip >= n_strips) return;  // only whole frame groups: a wave (TPF = 64) or the workgroup (FPB = 1)
+    const int trk = find_track(strip_pfx, n_tracks, strip);
+    const uint64_t F = frame_pfx[trk + 1] - frame_pfx[trk];
+    const uint64_t f0 = (strip - strip_pfx[trk]) * (uint64_t)STRIP_T;
+    const int nf = (int)(F - f0 < (uint64_t)STRIP_T ? F - f0 : (uint64_t)STRIP_T);
+    const float gn = gain[trk];
+    c2* bufA = lds + fl * 2 * PADM;
+    c2* bufB = bufA + PADM;
+    const int vo = 8 * lt;
+    // the strip's samples: frame f0 + i starts at complex index (f0 + i) * hop / 2
+    const uint64_t cstart = f0 * (uint64_t)(hop / 2);
+    const uint64_t clen = (uint64_t)(nf - 1) * (uint64_t)(hop / 2) + (uint64_t)M;  // complex values the strip reads
+    const float* sbase = samples + src_off[trk] + 2 * cstart;
+    const __amdgpu_buffer_rsrc_t rx = rsrc_of(sbase, (uint32_t)(8u * clen));
+    const __amdgpu_buffer_rsrc_t rw = rsrc_of(window, 4u * NFFT);
+    const __amdgpu_buffer_rsrc_t rtw = rsrc_of(twp, 8u * 15u * (TPF + TPF / 16 + 1));
+    const __amdgpu_buffer_rsrc_t rrt = rsrc_of(rtp, 8u * (SH::RT_SPECIAL + 4));
+
+    // per-strip constants
+    c2 win[16], tw1[15], tw2[15], wk[SH::NPAIR];
+    c2 ring[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) ring[k] = ld_c2(rx, vo, 8 * TPF * k);
+#pragma unroll
+    for (int k = 0; k < 16; k++) win[k] = ld_c2(rw, vo, 8 * TPF * k);
+#pragma unroll
+    for (int j = 0; j < 15; j++) tw1[j] = ld_c2(rtw, vo, 8 * TPF * j);
+    const int pp2 = lt / 16;  // pass 2 (s = 16): p' = lt / 16
+#pragma unroll
+    for (int j = 0; j < 15; j++) tw2[j] = ld_c2(rtw, 8 * pp2, 8 * (15 * TPF + j * (TPF / 16)));
+#pragma unroll
+    for (int j = 0; j < SH::NPAIR; j++) wk[j] = ld_c2(rrt, vo, 8 * TPF * (2 * j));
+    c2 tw3[15];  // pass 3 (M = 4096): p' = 0, wave-uniform
+    if constexpr (M == 4096) {
+#pragma unroll
+        for (int j = 0; j < 15; j++) {
+            const cx t = twp[15 * TPF + 15 * (TPF / 16) + j];
+            tw3[j] = c2{t.re, t.im};
+        }
+    }
+    const c2 rt0 = ld_c2(rrt, 0, 8 * SH::RT_SPECIAL), rtM = ld_c2(rrt, 0, 8 * (SH::RT_SPECIAL + 1)),
+             rtH = ld_c2(rrt, 0, 8 * (SH::RT_SPECIAL + 2));
+
+    for (int i = 0; i < nf; i++) {
+        const uint64_t f = f0 + (uint64_t)i;
+        // prefetch the next frame's S new ring values: z[(i+1) h + lt + TPF (16 - S + s)]
+        c2 nxt[S];
+        if (i + 1 < nf) {
+#pragma unroll
+            for (int s2 = 0; s2 < S; s2++)
+                nxt[s2] = ld_c2(rx, vo, 8 * ((i + 1) * (hop / 2) + TPF * (16 - S + s2)));
+        }
+        c2 v[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) v[k] = {(ring[k].x * gn) * win[k].x, (ring[k].y * gn) * win[k].y};
+        // pass 1 (n = M, s = 1, p' = lt) -> A
+        radix16<false>(v, tw1);
+#pragma unroll
+        for (int k = 0; k < 16; k++) bufA[P17 * lt + k] = v[k];
+        frame_sync<TPF>();
+        // pass 2 (n = M/16, s = 16): A -> B
+        {
+            constexpr int s2 = 16, m1 = (M / 16) / 16;
+            const int q = lt % s2;
+            const int rb = lpad(q + s2 * pp2), rs = s2 * m1 + PADSHIFT * (s2 * m1) / 16;
+#pragma unroll
+            for (int k = 0; k < 16; k++) v[k] = bufA[rb + rs * k];
+            radix16<false>(v, tw2);
+            const int wb = q + P272 * pp2;
+#pragma unroll
+            for (int k = 0; k < 16; k++) bufB[wb + P17 * k] = v[k];
+        }
+        frame_sync<TPF>();
+        if constexpr (M == 4096) {  // pass 3 (n = 16, s = 256, p' = 0), in place in B
+            const int rb = lpad(lt);
+#pragma unroll
+            for (int k = 0; k < 16; k++) v[k] = bufB[rb + P272 * k];
+            radix16<true>(v, tw3);
+#pragma unroll
+            for (int k = 0; k < 16; k++) bufB[rb + P272 * k] = v[k];
+        } else {  // trailing radix-4 (n = 4, s = M/4, p = 0), in place in B
+#pragma unroll
+            for (int r = 0; r < (M / 4) / TPF; r++) {
+                const int b = lpad(lt + TPF * r);
+                c2 y0, y1, y2, y3;
+                bfly4<false>(bufB[b], bufB[b + P272], bufB[b + 2 * P272], bufB[b + 3 * P272], c2{}, c2{}, c2{}, y0, y1,
+                             y2, y3);
+                bufB[b] = y0;
+                bufB[b + P272] = y1;
+                bufB[b + 2 * P272] = y2;
+                bufB[b + 3 * P272] = y3;
+            }
+        }
+        frame_sync<TPF>();
+        // post-processing from B (see k_stft_mag); rt[M-k] = (-rt[k].re, rt[k].im)
+        float* out = mags + (mag_row0[trk] + f) * (uint64_t)stride;
+        float mx = 0.0f;
+        auto sq = [](float yx, float yy) { return 0.5f * sqrt_cr(__builtin_fmaf(yx, yx, yy * yy)); };
+        auto put = [&](int k, float mag) {
+            out[k] = mag;
+            if (FRAME_MAX) mx = sd_maxf(mx, mag);
+        };
+#pragma unroll
+        for (int j = 0; j < SH::NPAIR; j++) {
+            const int k = 1 + lt + TPF * j;
+            if (j + 1 < SH::NPAIR || k < M / 2) {
+                const c2 Zk = bufB[lpad(k)], Zr = bufB[lpad(M - k)];
+                const float sx = Zk.x + Zr.x, sy = Zk.y - Zr.y, dx = Zk.y + Zr.y, dy = -(Zk.x - Zr.x);
+                const float a = wk[j].x, b = wk[j].y;
+                put(k, sq(__builtin_fmaf(a, dx, __builtin_fmaf(-b, dy, sx)), __builtin_fmaf(a, dy, __builtin_fmaf(b, dx, sy))));
+                // bin M-k: S' = conj(S), D'' = conj(D'), rt' = (-a, b)
+                put(M - k, sq(__builtin_fmaf(-a, dx, __builtin_fmaf(b, dy, sx)), __builtin_fmaf(a, dy, __builtin_fmaf(b, dx, -sy))));
+            }
+        }
+        if (lt == 0) {
+            const c2 Z0 = bufB[0];
+            const float sx = Z0.x + Z0.x, sy = Z0.y - Z0.y, dx = Z0.y + Z0.y, dy = -(Z0.x - Z0.x);
+            put(0, sq(__builtin_fmaf(rt0.x, dx, __builtin_fmaf(-rt0.y, dy, sx)), __builtin_fmaf(rt0.x, dy, __builtin_fmaf(rt0.y, dx, sy))));
+            put(M, sq(__builtin_fmaf(rtM.x, dx, __builtin_fmaf(-rtM.y, dy, sx)), __builtin_fmaf(rtM.x, dy, __builtin_fmaf(rtM.y, dx, sy))));
+        } else if (lt == 1) {
+            const c2 Zh = bufB[lpad(M / 2)];
+            const float sx = Zh.x + Zh.x, sy = Zh.y - Zh.y, dx = Zh.y + Zh.y, dy = -(Zh.x - Zh.x);
+            put(M / 2, sq(__builtin_fmaf(rtH.x, dx, __builtin_fmaf(-rtH.y, dy, sx)), __builtin_fmaf(rtH.x, dy, __builtin_fmaf(rtH.y, dx, sy))));
+        }
+        if constexpr (FRAME_MAX) {
+            static_assert(!FRAME_MAX || TPF == 64, "frame maxima: one wave per frame");
+            mx = wave_max(mx);
+            if (lt == 0) frame_max[mag_row0[trk] + f] = mx;
+        }
+        // slide the ring
+#pragma unroll
+        for (int k = 0; k < 16 - S; k++) ring[k] = ring[k + S];
+        if (i + 1 < nf) {
+#pragma unroll
+            for (int s2 = 0; s2 < S; s2++) ring[16 - S + s2] = nxt[s2];
+        }
+    }
+}
+
+// strips of STRIP_T frames per track: strip_pfx[t] = sum over tracks < t of ceil(F / STRIP_T)
+std::vector<uint64_t> stft_strips(const std::vector<uint64_t>& frame_pfx) {
+    std::vector<uint64_t> sp(frame_pfx.size(), 0);
+    for (size_t t = 0; t + 1 < frame_pfx.size(); t++)
+        sp[t + 1] = sp[t] + (frame_pfx[t + 1] - frame_pfx[t] + STRIP_T - 1) / STRIP_T;
+    return sp;
 }
 
 // Host: per-thread twiddle layouts for k_stft_mag, from the spec's tables (values unchanged).
@@ -365,7 +579,9 @@ void stft_tables(int N, const std::vector<float>& tw, const std::vector<float>& 
             const int k = 1 + lt + TPF * j;
             if (k >= M / 2) continue;
             put(rtp, (size_t)(2 * j) * TPF + lt, &rt[2 * (size_t)k]);
-            put(rtp, (size_t)(2 * j + 1) * TPF + lt, &rt[2 * (size_t)(M - k)]);
+            // the STFT section's symmetric post twiddles: rt[M-k] = (-rt[k].re, rt[k].im)
+            const float sym[2] = {-rt[2 * (size_t)k], rt[2 * (size_t)k + 1]};
+            put(rtp, (size_t)(2 * j + 1) * TPF + lt, sym);
         }
     put(rtp, (size_t)sp + 0, &rt[0]);
     put(rtp, (size_t)sp + 1, &rt[2 * (size_t)M]);
@@ -373,13 +589,50 @@ void stft_tables(int N, const std::vector<float>& tw, const std::vector<float>& 
     put(rtp, (size_t)sp + 3, &tw[0]);
 }
 
-// host launcher (the runtime owns all buffers; see runtime.hip)
+// hop = S * 2 * TPF complex values with a k_stft_slide instance
+bool stft_slide_ok(int nfft, int hop) {
+    if (nfft == 8192) return hop == 512 || hop == 1024;
+    if (nfft == 2048) return hop == 256 || hop == 512 || hop == 1024;
+    return false;
+}
+
+// host launcher (the runtime owns all buffers; see runtime.hip).  With strip_pfx (stft_strips of
+// the frame prefix, on the device) and a hop stft_slide_ok accepts, the sliding-strip kernel runs;
+// otherwise the frame-parallel one.
 void launch_stft(int nfft, bool frame_max, const float* samples, const uint64_t* frame_pfx, int n_tracks,
                  uint64_t total_frames, const uint64_t* src_off, const float* gain, int hop, const float* window,
                  const cx* twp, const cx* rtp, float* mags, const uint64_t* mag_row0, int stride, float* fmax,
-                 hipStream_t st) {
+                 hipStream_t st, const uint64_t* strip_pfx, uint64_t n_strips) {
     if (total_frames == 0) return;
     const dim3 block(256);
+    if (strip_pfx && n_strips && stft_slide_ok(nfft, hop)) {
+#define SDSP_SLIDE(N, S, FM)                                                                                      \
+    hipLaunchKernelGGL((k_stft_slide<N, S, FM>), dim3((unsigned)((n_strips + 256 / (N / 32) - 1) / (256 / (N / 32)))), \
+                       block, 0, st, samples, frame_pfx, strip_pfx, n_tracks, n_strips, src_off, gain, hop, window, twp, \
+                       rtp, mags, mag_row0, stride, fmax)
+        if (nfft == 8192) {
+            if (hop == 512)
+                SDSP_SLIDE(8192, 1, false);
+            else
+                SDSP_SLIDE(8192, 2, false);
+        } else if (frame_max) {
+            if (hop == 256)
+                SDSP_SLIDE(2048, 2, true);
+            else if (hop == 512)
+                SDSP_SLIDE(2048, 4, true);
+            else
+                SDSP_SLIDE(2048, 8, true);
+        } else {
+            if (hop == 256)
+                SDSP_SLIDE(2048, 2, false);
+            else if (hop == 512)
+                SDSP_SLIDE(2048, 4, false);
+            else
+                SDSP_SLIDE(2048, 8, false);
+        }
+#undef SDSP_SLIDE
+        return;
+    }
     if (nfft == 2048) {
         const dim3 grid((unsigned)((total_frames + 3) / 4));
         if (frame_max)

@@ -200,10 +200,7 @@ struct LegacyOut {
 constexpr int LG_COMB_MAX = 2048, LG_AC_MAX = 512;  // comb candidates; autocorrelation peaks
 
 // ---- launchers ----
-void launch_stft(int nfft, bool frame_max, const float* samples, const uint64_t* frame_pfx, int n_tracks,
-                 uint64_t total_frames, const uint64_t* src_off, const float* gain, int hop, const float* window,
-                 const cx* tw, const cx* rt, float* mags, const uint64_t* mag_row0, int stride, float* fmax,
-                 hipStream_t st);
+// launch_stft, stft_strips, stft_slide_ok: sdsp_runtime.hpp
 void launch_peak_gain(const float* x, const uint64_t* in_off, const uint64_t* n_raw, const uint64_t* chunk_pfx, int T,
                       uint64_t n_chunks, unsigned int* peak_bits, float target, int enable, float* gain,
                       hipStream_t st);

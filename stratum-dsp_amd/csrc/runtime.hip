@@ -254,6 +254,83 @@ int32_t sdsp_last_stage_times(int32_t device, sdsp_stage_times* out) {
     }
 }
 
+// Kernel probe (tools/stft_probe.py): times `reps` launches of the STFT kernel over n_tracks
+// device-resident noise tracks of len samples each (one magnitude buffer, the pipeline's row
+// stride), HIP events on the launch stream.  Writes the mean launch time and the algorithmic
+// bytes per launch (4 N_in + 4 F (nfft/2+1) per track).
+int32_t sdsp_probe_stft(int32_t device, uint64_t nfft, uint64_t hop, uint64_t n_tracks, uint64_t len, int32_t reps,
+                        int32_t stride, double* ms_per_launch, double* bytes_per_launch) {
+    try {
+        if (!(nfft == 2048 || nfft == 8192) || len < nfft || hop == 0 || n_tracks == 0 || reps <= 0)
+            return SDSP_ERR_INVALID_INPUT;
+        DeviceCtx& c = device_ctx(device);
+        std::lock_guard<std::mutex> lk(c.mu);
+        SDSP_HIP_CHECK(hipSetDevice(device));
+        const uint64_t F = (len - nfft) / hop + 1, total = F * n_tracks;
+        const int bins = (int)nfft / 2 + 1;
+        if (stride < bins) stride = (bins + 3) & ~3;
+        FftTables& tb = c.tables((int)nfft, true);
+        DevBuf x, pfx, off, g, row0, mags, fmax;
+        x.ensure(n_tracks * len * 4);
+        mags.ensure(total * (uint64_t)stride * 4);
+        fmax.ensure(total * 4);
+        std::vector<float> noise(len);
+        uint32_t st = 12345u;
+        for (auto& v : noise) {
+            st = st * 1664525u + 1013904223u;
+            v = ((float)(st >> 8) / 16777216.0f - 0.5f) * 0.6f;
+        }
+        SDSP_HIP_CHECK(hipMemcpy(x.p, noise.data(), len * 4, hipMemcpyHostToDevice));
+        for (uint64_t t = 1; t < n_tracks; t++)
+            SDSP_HIP_CHECK(hipMemcpy(x.as<float>() + t * len, x.p, len * 4, hipMemcpyDeviceToDevice));
+        std::vector<uint64_t> pf(n_tracks + 1), o(n_tracks), r0(n_tracks);
+        std::vector<float> gv(n_tracks, 0.8912509f);
+        for (uint64_t t = 0; t <= n_tracks; t++) pf[t] = t * F;
+        for (uint64_t t = 0; t < n_tracks; t++) {
+            o[t] = t * len;
+            r0[t] = t * F;
+        }
+        const bool frame_parallel = std::getenv("SDSP_STFT_FRAME_PARALLEL") != nullptr;  // A/B switch
+        const std::vector<uint64_t> sp = stft_strips(pf);
+        DevBuf strips;
+        strips.ensure(sp.size() * 8);
+        SDSP_HIP_CHECK(hipMemcpy(strips.p, sp.data(), sp.size() * 8, hipMemcpyHostToDevice));
+        pfx.ensure(pf.size() * 8);
+        off.ensure(o.size() * 8);
+        row0.ensure(r0.size() * 8);
+        g.ensure(gv.size() * 4);
+        SDSP_HIP_CHECK(hipMemcpy(pfx.p, pf.data(), pf.size() * 8, hipMemcpyHostToDevice));
+        SDSP_HIP_CHECK(hipMemcpy(off.p, o.data(), o.size() * 8, hipMemcpyHostToDevice));
+        SDSP_HIP_CHECK(hipMemcpy(row0.p, r0.data(), r0.size() * 8, hipMemcpyHostToDevice));
+        SDSP_HIP_CHECK(hipMemcpy(g.p, gv.data(), gv.size() * 4, hipMemcpyHostToDevice));
+        hipEvent_t e0, e1;
+        SDSP_HIP_CHECK(hipEventCreate(&e0));
+        SDSP_HIP_CHECK(hipEventCreate(&e1));
+        auto launch = [&]() {
+            launch_stft((int)nfft, nfft == 2048, x.as<float>(), pfx.as<uint64_t>(), (int)n_tracks, total,
+                        off.as<uint64_t>(), g.as<float>(), (int)hop, tb.window.as<float>(), tb.stft_tw.as<cx>(),
+                        tb.stft_rt.as<cx>(), mags.as<float>(), row0.as<uint64_t>(), stride, fmax.as<float>(), c.stream,
+                        frame_parallel ? nullptr : strips.as<uint64_t>(), sp.back());
+        };
+        launch();  // warm: first touch of the output pages
+        SDSP_HIP_CHECK(hipEventRecord(e0, c.stream));
+        for (int r = 0; r < reps; r++) launch();
+        SDSP_HIP_CHECK(hipEventRecord(e1, c.stream));
+        SDSP_HIP_CHECK(hipGetLastError());
+        SDSP_HIP_CHECK(hipEventSynchronize(e1));
+        float ms = 0;
+        SDSP_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        *ms_per_launch = ms / reps;
+        *bytes_per_launch = (double)n_tracks * (4.0 * (double)len + 4.0 * (double)F * (double)bins);
+        return SDSP_OK;
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "sdsp_probe_stft: %s\n", e.what());
+        return SDSP_ERR_PROCESSING;
+    }
+}
+
 // Stage probe: STFT magnitudes of one host buffer (x*gain framed at hop), frames x (nfft/2+1).
 int32_t sdsp_debug_stft(const float* host_x, uint64_t n, uint64_t nfft, uint64_t hop, float gain, float* host_out,
                         float* host_frame_max, int32_t device) {
@@ -275,6 +352,12 @@ int32_t sdsp_debug_stft(const float* host_x, uint64_t n, uint64_t nfft, uint64_t
         g.ensure(4);
         row0.ensure(8);
         const uint64_t pf[2] = {0, frames}, o0 = 0, r0 = 0;
+        const std::vector<uint64_t> sp = stft_strips(std::vector<uint64_t>{0, frames});
+        DevBuf strips;
+        strips.ensure(16);
+        SDSP_HIP_CHECK(hipMemcpy(strips.p, sp.data(), 16, hipMemcpyHostToDevice));
+        // SDSP_STFT_FRAME_PARALLEL=1: the frame-parallel kernel (k_stft_mag) for every hop
+        const bool frame_parallel = std::getenv("SDSP_STFT_FRAME_PARALLEL") != nullptr;
         SDSP_HIP_CHECK(hipMemcpy(x.p, host_x, n * 4, hipMemcpyHostToDevice));
         SDSP_HIP_CHECK(hipMemcpy(pfx.p, pf, 16, hipMemcpyHostToDevice));
         SDSP_HIP_CHECK(hipMemcpy(off.p, &o0, 8, hipMemcpyHostToDevice));
@@ -282,7 +365,8 @@ int32_t sdsp_debug_stft(const float* host_x, uint64_t n, uint64_t nfft, uint64_t
         SDSP_HIP_CHECK(hipMemcpy(row0.p, &r0, 8, hipMemcpyHostToDevice));
         launch_stft((int)nfft, nfft == 2048, x.as<float>(), pfx.as<uint64_t>(), 1, frames, off.as<uint64_t>(),
                     g.as<float>(), (int)hop, tb.window.as<float>(), tb.stft_tw.as<cx>(), tb.stft_rt.as<cx>(), mags.as<float>(),
-                    row0.as<uint64_t>(), stride, fmax.as<float>(), c.stream);
+                    row0.as<uint64_t>(), stride, fmax.as<float>(), c.stream, frame_parallel ? nullptr : strips.as<uint64_t>(),
+                    sp.back());
         SDSP_HIP_CHECK(hipGetLastError());
         SDSP_HIP_CHECK(hipStreamSynchronize(c.stream));
         SDSP_HIP_CHECK(hipMemcpy2D(host_out, (size_t)bins * 4, mags.p, (size_t)stride * 4, (size_t)bins * 4,

@@ -8,8 +8,16 @@ import sdsp
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("nfft,hop", [(2048, 512), (2048, 256), (2048, 1024), (8192, 512)])
-def test_stft_bit_exact(nfft, hop):
+@pytest.mark.parametrize("frame_parallel", [False, True])
+@pytest.mark.parametrize("nfft,hop", [(2048, 512), (2048, 256), (2048, 1024), (8192, 512), (8192, 1024), (2048, 300),
+                                      (8192, 256)])
+def test_stft_bit_exact(nfft, hop, frame_parallel, monkeypatch):
+    """The sliding-strip kernel (hops k_stft_slide serves; strips of 64 frames, a partial last
+    strip) and the frame-parallel kernel (every hop; SDSP_STFT_FRAME_PARALLEL=1 forces it)."""
+    if frame_parallel:
+        monkeypatch.setenv("SDSP_STFT_FRAME_PARALLEL", "1")
+    else:
+        monkeypatch.delenv("SDSP_STFT_FRAME_PARALLEL", raising=False)
     rng = np.random.default_rng(nfft + hop)
     x = (rng.standard_normal(44100 * 3) * 0.3).astype(np.float32)
     gain = np.float32(0.8912509)
