@@ -127,6 +127,30 @@ __device__ __forceinline__ float sqrt_cr(float x) {
     return __builtin_sqrtf(x);
 }
 
+// Correctly rounded f32 sqrt without compare masks or branches, for x = +0 and x in [2^-96, inf):
+// the same v_sqrt_f32 + +-1 ulp FMA-residual correction as sqrt_cr, with the two decisions taken
+// from the residuals' sign bits (rm <= 0 -> s - 1 ulp, rp > 0 -> s + 1 ulp; an exact zero residual
+// is +0, never -0).  x = +0 gives sm = NaN, whose residual's sign is unspecified: the final
+// signed max with 0 maps the possible -1 back to +0.  Inputs outside that set (subnormal-scale x,
+// inf, NaN) are recorded in lo / hi (min of bits - 1, max of bits) for the caller's fix-up pass.
+__device__ __forceinline__ float sqrt_fast(float x, uint32_t& lo, uint32_t& hi) {
+    const uint32_t u = __float_as_uint(x);
+    lo = min(lo, u - 1u);
+    hi = max(hi, u);
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const uint32_t si = __float_as_uint(s);
+    const float sm = __uint_as_float(si - 1u), sp = __uint_as_float(si + 1u);
+    const float rm = __builtin_fmaf(-sm, s, x);
+    const float rp = __builtin_fmaf(-sp, s, x);
+    const int dm = (int)(__float_as_uint(rm) - 1u) >> 31;  // -1 iff rm <= 0
+    const uint32_t up = (0u - __float_as_uint(rp)) >> 31;  // 1 iff rp > 0
+    return __int_as_float(max((int)(si + (uint32_t)dm + up), 0));
+}
+// true when some input of sqrt_fast was outside its exact range
+__device__ __forceinline__ bool sqrt_fast_missed(uint32_t lo, uint32_t hi) {
+    return lo < 0x0F7FFFFFu || hi >= 0x7F800000u;  // (0, 2^-96) or inf / NaN
+}
+
 // Two radix-4 stages, (n, s) then (n/4, 4s), on v[j' + 4j] = x[q + s(p' + (n/16)(j' + 4j))].
 // On return v[jA + 4jB] = z[q + 16 s p' + s(jA + 4jB)].  w[0..11] = stage-A twiddles
 // W^{jA (p' + j' n/16) M/n} at index 3 j' + jA - 1, w[12..14] = stage-B W^{jB p' 4M/n}.
@@ -376,6 +400,40 @@ __global__ __launch_bounds__(256) STFT_ATTR void k_stft_mag(const float* __restr
 //    bin M-k needs no table entry of its own.
 constexpr int STRIP_T = 64;
 
+// The post-processing of one thread's bins with the general sqrt (sqrt_cr), everything re-read
+// from LDS / the tables: k_stft_slide's fix-up for frames where sqrt_fast met an input outside
+// its exact range.  Out of line, so the rare path costs the main loop no registers.  Returns the
+// thread's magnitude maximum.
+template <int M>
+__device__ __noinline__ float stft_post_exact(const c2* bufB, int lt, const cx* rtp, float* out) {
+    using SH = StftShape<M>;
+    constexpr int TPF = SH::TPF;
+    float mx = 0.0f;
+    auto sq = [](float yx, float yy) { return 0.5f * sqrt_cr(__builtin_fmaf(yx, yx, yy * yy)); };
+    auto put = [&](int k, float m) {
+        out[k] = m;
+        mx = sd_maxf(mx, m);
+    };
+    auto one = [&](c2 Zk, c2 Zr, cx w, int k, bool partner) {
+        const float sx = Zk.x + Zr.x, sy = Zk.y - Zr.y, dx = Zk.y + Zr.y, dy = -(Zk.x - Zr.x);
+        put(k, sq(__builtin_fmaf(w.re, dx, __builtin_fmaf(-w.im, dy, sx)), __builtin_fmaf(w.re, dy, __builtin_fmaf(w.im, dx, sy))));
+        if (partner)
+            put(M - k, sq(__builtin_fmaf(-w.re, dx, __builtin_fmaf(w.im, dy, sx)),
+                          __builtin_fmaf(w.re, dy, __builtin_fmaf(w.im, dx, -sy))));
+    };
+    for (int j = 0; j < SH::NPAIR; j++) {
+        const int k = 1 + lt + TPF * j;
+        if (k < M / 2) one(bufB[lpad(k)], bufB[lpad(M - k)], rtp[(2 * j) * TPF + lt], k, true);
+    }
+    if (lt == 0) {
+        one(bufB[0], bufB[0], rtp[SH::RT_SPECIAL], 0, false);
+        one(bufB[0], bufB[0], rtp[SH::RT_SPECIAL + 1], M, false);
+    } else if (lt == 1) {
+        one(bufB[lpad(M / 2)], bufB[lpad(M / 2)], rtp[SH::RT_SPECIAL + 2], M / 2, false);
+    }
+    return mx;
+}
+
 template <int NFFT, int S, bool FRAME_MAX>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_stft_slide(
     const float* __restrict__ samples, const uint64_t* __restrict__ frame_pfx, const uint64_t* __restrict__ strip_pfx,
@@ -392,7 +450,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 
     const int lt = threadIdx.x % TPF;
     const int fl = threadIdx.x / TPF;
-    const uint64_t strip = (uint64_t)xcd_block(blockIdx.x, gridDim.x) * FPB + fl;
+    // wave-uniform by construction (a frame group is whole waves); readfirstlane lets the compiler
+    // keep the strip's scalars and buffer descriptors in SGPRs
+    const uint64_t strip =
+        (uint64_t)__builtin_amdgcn_readfirstlane((int)((uint64_t)xcd_block(blockIdx.x, gridDim.x) * FPB + fl));
     if (strip >= n_strips) return;  // only whole frame groups: a wave (TPF = 64) or the workgroup (FPB = 1)
     const int trk = find_track(strip_pfx, n_tracks, strip);
     const uint64_t F = frame_pfx[trk + 1] - frame_pfx[trk];
@@ -415,7 +476,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     c2 win[16], tw1[15], tw2[15], wk[SH::NPAIR];
     c2 ring[16];
 #pragma unroll
-    for (int k = 0; k < 16; k++) ring[k] = ld_c2(rx, vo, 8 * TPF * k);
+    for (int k = 0; k < 16; k++) {  // the ring holds x * gain (the normalised samples, src/lib.rs:124)
+        const c2 x = ld_c2(rx, vo, 8 * TPF * k);
+        ring[k] = {x.x * gn, x.y * gn};
+    }
 #pragma unroll
     for (int k = 0; k < 16; k++) win[k] = ld_c2(rw, vo, 8 * TPF * k);
 #pragma unroll
@@ -436,18 +500,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const c2 rt0 = ld_c2(rrt, 0, 8 * SH::RT_SPECIAL), rtM = ld_c2(rrt, 0, 8 * (SH::RT_SPECIAL + 1)),
              rtH = ld_c2(rrt, 0, 8 * (SH::RT_SPECIAL + 2));
 
+    // every per-strip load has landed before the frame loop: the loop header then carries no
+    // pending load, so the compiler does not wait there for the previous frame's stores
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     for (int i = 0; i < nf; i++) {
         const uint64_t f = f0 + (uint64_t)i;
-        // prefetch the next frame's S new ring values: z[(i+1) h + lt + TPF (16 - S + s)]
+        // prefetch the next frame's S new ring values: z[(i+1) h + lt + TPF (16 - S + s)].  After
+        // the strip's last frame the offsets are past the descriptor's range, where buffer loads
+        // return 0 without touching memory, so the load needs no branch (a conditional load
+        // makes the compiler wait for it at once).
         c2 nxt[S];
-        if (i + 1 < nf) {
 #pragma unroll
-            for (int s2 = 0; s2 < S; s2++)
-                nxt[s2] = ld_c2(rx, vo, 8 * ((i + 1) * (hop / 2) + TPF * (16 - S + s2)));
-        }
+        for (int s2 = 0; s2 < S; s2++) nxt[s2] = ld_c2(rx, vo, 8 * ((i + 1) * (hop / 2) + TPF * (16 - S + s2)));
         c2 v[16];
 #pragma unroll
-        for (int k = 0; k < 16; k++) v[k] = {(ring[k].x * gn) * win[k].x, (ring[k].y * gn) * win[k].y};
+        for (int k = 0; k < 16; k++) v[k] = {ring[k].x * win[k].x, ring[k].y * win[k].y};
         // pass 1 (n = M, s = 1, p' = lt) -> A
         radix16<false>(v, tw1);
 #pragma unroll
@@ -490,9 +557,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         // post-processing from B (see k_stft_mag); rt[M-k] = (-rt[k].re, rt[k].im)
         float* out = mags + (mag_row0[trk] + f) * (uint64_t)stride;
         float mx = 0.0f;
-        auto sq = [](float yx, float yy) { return 0.5f * sqrt_cr(__builtin_fmaf(yx, yx, yy * yy)); };
+        uint32_t lo = 0xFFFFFFFFu, hi = 0u;
+#ifdef SDSP_EXP_NOSQRT
+        auto sq = [&](float yx, float yy) { return 0.5f * __builtin_amdgcn_sqrtf(__builtin_fmaf(yx, yx, yy * yy)); };
+#else
+        auto sq = [&](float yx, float yy) { return 0.5f * sqrt_fast(__builtin_fmaf(yx, yx, yy * yy), lo, hi); };
+#endif
         auto put = [&](int k, float mag) {
+#ifdef SDSP_EXP_NOSTORE
+            if (mag == 1234.5f) out[k] = mag;
+#else
             out[k] = mag;
+#endif
             if (FRAME_MAX) mx = sd_maxf(mx, mag);
         };
 #pragma unroll
@@ -517,6 +593,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             const float sx = Zh.x + Zh.x, sy = Zh.y - Zh.y, dx = Zh.y + Zh.y, dy = -(Zh.x - Zh.x);
             put(M / 2, sq(__builtin_fmaf(rtH.x, dx, __builtin_fmaf(-rtH.y, dy, sx)), __builtin_fmaf(rtH.x, dy, __builtin_fmaf(rtH.y, dx, sy))));
         }
+#ifndef SDSP_EXP_NOSQRT
+        // a magnitude^2 of subnormal scale (or inf / NaN): redo this thread's bins with the general
+        // sqrt and store them again (same thread, same addresses: the later store wins).  B is
+        // intact until this thread reaches the next barrier.
+        if (__builtin_expect(sqrt_fast_missed(lo, hi), 0)) mx = stft_post_exact<M>(bufB, lt, rtp, out);
+#endif
         if constexpr (FRAME_MAX) {
             static_assert(!FRAME_MAX || TPF == 64, "frame maxima: one wave per frame");
             mx = wave_max(mx);
@@ -525,10 +607,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         // slide the ring
 #pragma unroll
         for (int k = 0; k < 16 - S; k++) ring[k] = ring[k + S];
-        if (i + 1 < nf) {
 #pragma unroll
-            for (int s2 = 0; s2 < S; s2++) ring[16 - S + s2] = nxt[s2];
-        }
+        for (int s2 = 0; s2 < S; s2++) ring[16 - S + s2] = {nxt[s2].x * gn, nxt[s2].y * gn};
     }
 }
 
