@@ -36,8 +36,8 @@
  *                                             fma(w.re, z.im, w.im*z.re));
  *   - no products for the p = 0 butterflies (W^0 = 1): y1 = amc + jbmd, y2 = apc - bpd,
  *     y3 = amc - jbmd;
- *   - post twiddles symmetric about M/2: rt[k] from the table for k <= M/2 and k = M, and
- *     rt[M-k] := (-rt[k].re, rt[k].im) for 0 < k < M/2 (e^{-i(pi - t)} = -conj(e^{-it}));
+ *   - post twiddles symmetric about M/2: rt[k] from the table for k <= M/2, and
+ *     rt[M-k] := (-rt[k].re, rt[k].im) for 0 <= k < M/2 (e^{-i(pi - t)} = -conj(e^{-it}));
  *   - post-processing for k = 0..M, with Zk = Z[k mod M], Zr = Z[(M-k) mod M]:
  *        S = (Zk.re + Zr.re, Zk.im - Zr.im)              (Zk + conj(Zr))
  *        D' = (Zk.im + Zr.im, -(Zk.re - Zr.re))          (-i (Zk - conj(Zr)))

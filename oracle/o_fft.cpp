@@ -167,7 +167,7 @@ static void stft_fft_complex(std::vector<Cx>& x, std::vector<Cx>& y) {
 // |X[k]|, k = 0..n/2, of a real frame of n samples: z[j] = (x[2j], x[2j+1]), Z = FFT_M(z),
 // S = Z[k] + conj(Z[M-k]), D' = -i (Z[k] - conj(Z[M-k])), Y = S + rt[k] D' (two FMAs per
 // component), |X[k]| = 0.5 * sqrt(fma(Y.re, Y.re, Y.im * Y.im)); the post twiddles are symmetric,
-// rt[M-k] = (-rt[k].re, rt[k].im) for 0 < k < M/2.
+// rt[M-k] = (-rt[k].re, rt[k].im) for 0 <= k < M/2.
 static void stft_mag(const float* x, size_t n, float* mag, std::vector<Cx>& z, std::vector<Cx>& tmp) {
     const size_t M = n / 2;
     z.resize(M);
@@ -177,8 +177,8 @@ static void stft_mag(const float* x, size_t n, float* mag, std::vector<Cx>& z, s
     for (size_t k = 0; k <= M; k++) {
         const Cx Zk = z[k % M];
         const Cx Zr = z[(M - k) % M];
-        // symmetric post twiddles: rt[k] for k <= M/2 and k = M, rt[M-k] := (-rt[k].re, rt[k].im)
-        const Cx w = (k > M / 2 && k < M) ? Cx{-rt[M - k].re, rt[M - k].im} : rt[k];
+        // symmetric post twiddles: rt[k] for k <= M/2, rt[M-k] := (-rt[k].re, rt[k].im) for k > M/2
+        const Cx w = k > M / 2 ? Cx{-rt[M - k].re, rt[M - k].im} : rt[k];
         const float sre = Zk.re + Zr.re, sim = Zk.im - Zr.im;
         const float dre = Zk.im + Zr.im, dim = -(Zk.re - Zr.re);
         const float yre = std::fma(w.re, dre, std::fma(-w.im, dim, sre));

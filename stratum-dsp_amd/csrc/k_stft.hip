@@ -185,15 +185,14 @@ struct StftShape {
     static constexpr int RT_SPECIAL = NPAIR * 2 * TPF;                  // rt[0], rt[M], rt[M/2], tw[0]
 };
 
+// one frame of k_stft_mag (frame group = the threads with the same threadIdx.x / TPF)
 template <int NFFT, bool FRAME_MAX>
-__global__ __launch_bounds__(256) STFT_ATTR void k_stft_mag(const float* __restrict__ samples,
-                                                  const uint64_t* __restrict__ frame_pfx, int n_tracks,
-                                                  uint64_t total_frames, const uint64_t* __restrict__ src_off,
-                                                  const float* __restrict__ gain, int hop,
-                                                  const float* __restrict__ window, const cx* __restrict__ twp,
-                                                  const cx* __restrict__ rtp, float* __restrict__ mags,
-                                                  const uint64_t* __restrict__ mag_row0, int stride,
-                                                  float* __restrict__ frame_max) {
+__device__ __forceinline__ void stft_mag_frame(const float* __restrict__ samples, const uint64_t* __restrict__ frame_pfx,
+                                               int n_tracks, uint64_t gg, bool live, const uint64_t* __restrict__ src_off,
+                                               const float* __restrict__ gain, int hop, const float* __restrict__ window,
+                                               const cx* __restrict__ twp, const cx* __restrict__ rtp,
+                                               float* __restrict__ mags, const uint64_t* __restrict__ mag_row0,
+                                               int stride, float* __restrict__ frame_max) {
     constexpr int M = NFFT / 2;
     using S = StftShape<M>;
     constexpr int TPF = S::TPF;
@@ -205,9 +204,6 @@ __global__ __launch_bounds__(256) STFT_ATTR void k_stft_mag(const float* __restr
 
     const int lt = threadIdx.x % TPF;  // thread within frame
     const int fl = threadIdx.x / TPF;  // frame within workgroup
-    const uint64_t g = (uint64_t)xcd_block(blockIdx.x, gridDim.x) * FPB + fl;
-    const bool live = g < total_frames;
-    const uint64_t gg = live ? g : total_frames - 1;  // dead lanes recompute the last frame
     const int trk = find_track(frame_pfx, n_tracks, gg);
     const uint64_t f = gg - frame_pfx[trk];
     const float gn = gain[trk];
@@ -380,6 +376,33 @@ __global__ __launch_bounds__(256) STFT_ATTR void k_stft_mag(const float* __restr
     }
 }
 
+// k_stft_mag: one frame per frame group (the general kernel: any hop).  With `redo` (the sliding
+// kernel's list: redo[0] = count, then global frame indices) it recomputes only the listed frames,
+// grid-striding over the list.
+template <int NFFT, bool FRAME_MAX>
+__global__ __launch_bounds__(256) STFT_ATTR void k_stft_mag(const float* __restrict__ samples,
+                                                  const uint64_t* __restrict__ frame_pfx, int n_tracks,
+                                                  uint64_t total_frames, const uint64_t* __restrict__ src_off,
+                                                  const float* __restrict__ gain, int hop,
+                                                  const float* __restrict__ window, const cx* __restrict__ twp,
+                                                  const cx* __restrict__ rtp, float* __restrict__ mags,
+                                                  const uint64_t* __restrict__ mag_row0, int stride,
+                                                  float* __restrict__ frame_max, const uint32_t* __restrict__ redo) {
+    if (redo) {
+        constexpr int FPB = 256 / StftShape<NFFT / 2>::TPF;
+        const uint32_t n = redo[0];
+        for (uint32_t e = blockIdx.x * FPB + threadIdx.x / StftShape<NFFT / 2>::TPF; e < n; e += gridDim.x * FPB)
+            stft_mag_frame<NFFT, FRAME_MAX>(samples, frame_pfx, n_tracks, (uint64_t)redo[1 + e], true, src_off, gain,
+                                            hop, window, twp, rtp, mags, mag_row0, stride, frame_max);
+        return;
+    }
+    const uint64_t g = (uint64_t)xcd_block(blockIdx.x, gridDim.x) * (256 / StftShape<NFFT / 2>::TPF) +
+                       threadIdx.x / StftShape<NFFT / 2>::TPF;
+    const bool live = g < total_frames;
+    stft_mag_frame<NFFT, FRAME_MAX>(samples, frame_pfx, n_tracks, live ? g : total_frames - 1, live, src_off, gain,
+                                    hop, window, twp, rtp, mags, mag_row0, stride, frame_max);
+}
+
 // ---------------------------------------------------------------------------------------------
 // Sliding-strip STFT (the pipeline's kernel for hops that are a multiple of 2*TPF complex
 // values: 8192/512, 8192/1024, 2048/256, 2048/512, 2048/1024).  Same arithmetic as k_stft_mag,
@@ -393,45 +416,52 @@ __global__ __launch_bounds__(256) STFT_ATTR void k_stft_mag(const float* __restr
 //    next frame starts hop/2 = S*TPF complex values later, so its element k is the current
 //    element k + S: the ring shifts by S and only S new values per thread are loaded (prefetched
 //    one frame ahead);
-//  * two LDS buffers: pass 1 writes A, pass 2 reads A and writes B, the last pass runs in place
-//    in B (each thread rewrites the slots it read), the post-processing reads B.  Three barriers
-//    per frame and no barrier between a pass's reads and its writes;
+//  * two LDS buffers: pass 1 writes A, pass 2 reads A and writes B, the last pass reads B into
+//    registers.  Its columns are assigned so that each real-FFT pair (k, M-k) meets in one thread
+//    (N = 2048) or in lanes l and l^32 of one wave, exchanged by ds_bpermute (N = 8192), so the
+//    post-processing runs from registers: two barriers per frame, no barrier between a pass's
+//    reads and its writes, and two LDS round trips instead of three;
 //  * the STFT post twiddles are the spec's symmetric ones, rt[M-k] = (-rt[k].re, rt[k].im), so
-//    bin M-k needs no table entry of its own.
+//    bin M-k needs no table entry of its own;
+//  * the correctly rounded sqrt is sqrt_fast; a frame where it met an input outside its exact
+//    range (magnitudes of subnormal scale, inf, NaN) is appended to a redo list that k_stft_mag
+//    recomputes right after (launch_stft).
 constexpr int STRIP_T = 64;
 
-// The post-processing of one thread's bins with the general sqrt (sqrt_cr), everything re-read
-// from LDS / the tables: k_stft_slide's fix-up for frames where sqrt_fast met an input outside
-// its exact range.  Out of line, so the rare path costs the main loop no registers.  Returns the
-// thread's magnitude maximum.
-template <int M>
-__device__ __noinline__ float stft_post_exact(const c2* bufB, int lt, const cx* rtp, float* out) {
-    using SH = StftShape<M>;
-    constexpr int TPF = SH::TPF;
-    float mx = 0.0f;
-    auto sq = [](float yx, float yy) { return 0.5f * sqrt_cr(__builtin_fmaf(yx, yx, yy * yy)); };
-    auto put = [&](int k, float m) {
-        out[k] = m;
-        mx = sd_maxf(mx, m);
-    };
-    auto one = [&](c2 Zk, c2 Zr, cx w, int k, bool partner) {
-        const float sx = Zk.x + Zr.x, sy = Zk.y - Zr.y, dx = Zk.y + Zr.y, dy = -(Zk.x - Zr.x);
-        put(k, sq(__builtin_fmaf(w.re, dx, __builtin_fmaf(-w.im, dy, sx)), __builtin_fmaf(w.re, dy, __builtin_fmaf(w.im, dx, sy))));
-        if (partner)
-            put(M - k, sq(__builtin_fmaf(-w.re, dx, __builtin_fmaf(w.im, dy, sx)),
-                          __builtin_fmaf(w.re, dy, __builtin_fmaf(w.im, dx, -sy))));
-    };
-    for (int j = 0; j < SH::NPAIR; j++) {
-        const int k = 1 + lt + TPF * j;
-        if (k < M / 2) one(bufB[lpad(k)], bufB[lpad(M - k)], rtp[(2 * j) * TPF + lt], k, true);
-    }
+// Last-pass columns of the sliding kernel, chosen so that the real-FFT pairs (k, M-k) meet in
+// registers.  Column c holds Z[c + 256 m]; its pairs lie in column 256 - c (mod 256).
+//  N = 8192 (16 per column, 256 threads): lanes l and l + 32 of a wave hold partner columns
+//    c = 32 w + l and 256 - c; wave 0's lanes 0 / 32 hold the self-paired columns 0 / 128.
+//  N = 2048 (4 per column, one wave): thread t holds columns (t, 256 - t) and (128 - t, 128 + t);
+//    thread 0 holds (0, 128) and (64, 192).
+__host__ __device__ inline int slide_col8(int lt) {
+    const int w = lt >> 6, l = lt & 63, base = 32 * w + (l & 31);
+    return l < 32 ? base : (base == 0 ? 128 : 256 - base);
+}
+__host__ __device__ inline void slide_cols2(int t, int* a, int* a2, int* b, int* b2) {
+    *a = t;
+    *a2 = t ? 256 - t : 128;
+    *b = t ? 128 - t : 64;
+    *b2 = t ? 128 + t : 192;
+}
+// The bin of each post slot (own bin k; the partner bin is M - k) of thread lt, slot j < 8.
+//  N = 8192: k = col + 256 j.  N = 2048: slots 0-3 pair (a, a2), 4-7 pair (b, b2), k = col + 256 j';
+//  thread 0's first four slots are {0, 256, 128, 384} (columns 0 and 128 pair within themselves).
+__host__ __device__ inline int slide_bin(int M, int lt, int j) {
+    if (M == 4096) return slide_col8(lt) + 256 * j;
+    int a, a2, b, b2;
+    slide_cols2(lt, &a, &a2, &b, &b2);
+    if (j >= 4) return b + 256 * (j - 4);
     if (lt == 0) {
-        one(bufB[0], bufB[0], rtp[SH::RT_SPECIAL], 0, false);
-        one(bufB[0], bufB[0], rtp[SH::RT_SPECIAL + 1], M, false);
-    } else if (lt == 1) {
-        one(bufB[lpad(M / 2)], bufB[lpad(M / 2)], rtp[SH::RT_SPECIAL + 2], M / 2, false);
+        const int t0[4] = {0, 256, 128, 384};
+        return t0[j];
     }
-    return mx;
+    return a + 256 * j;
+}
+// rtp offset of the sliding kernel's post table: [slot j][lane] rt(slide_bin), then rt(M/2)
+template <int M>
+constexpr int slide_rt_base() {
+    return StftShape<M>::RT_SPECIAL + 4;
 }
 
 template <int NFFT, int S, bool FRAME_MAX>
@@ -439,7 +469,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const float* __restrict__ samples, const uint64_t* __restrict__ frame_pfx, const uint64_t* __restrict__ strip_pfx,
     int n_tracks, uint64_t n_strips, const uint64_t* __restrict__ src_off, const float* __restrict__ gain, int hop,
     const float* __restrict__ window, const cx* __restrict__ twp, const cx* __restrict__ rtp, float* __restrict__ mags,
-    const uint64_t* __restrict__ mag_row0, int stride, float* __restrict__ frame_max) {
+    const uint64_t* __restrict__ mag_row0, int stride, float* __restrict__ frame_max, uint32_t* __restrict__ redo) {
     constexpr int M = NFFT / 2;
     using SH = StftShape<M>;
     constexpr int TPF = SH::TPF;
@@ -470,10 +500,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const __amdgpu_buffer_rsrc_t rx = rsrc_of(sbase, (uint32_t)(8u * clen));
     const __amdgpu_buffer_rsrc_t rw = rsrc_of(window, 4u * NFFT);
     const __amdgpu_buffer_rsrc_t rtw = rsrc_of(twp, 8u * 15u * (TPF + TPF / 16 + 1));
-    const __amdgpu_buffer_rsrc_t rrt = rsrc_of(rtp, 8u * (SH::RT_SPECIAL + 4));
+    const __amdgpu_buffer_rsrc_t rrt = rsrc_of(rtp, 8u * (slide_rt_base<M>() + 8 * TPF + 1));
 
     // per-strip constants
-    c2 win[16], tw1[15], tw2[15], wk[SH::NPAIR];
+    c2 win[16], tw1[15], tw2[15], wk[8];
     c2 ring[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) {  // the ring holds x * gain (the normalised samples, src/lib.rs:124)
@@ -488,7 +518,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
     for (int j = 0; j < 15; j++) tw2[j] = ld_c2(rtw, 8 * pp2, 8 * (15 * TPF + j * (TPF / 16)));
 #pragma unroll
-    for (int j = 0; j < SH::NPAIR; j++) wk[j] = ld_c2(rrt, vo, 8 * TPF * (2 * j));
+    for (int j = 0; j < 8; j++) wk[j] = ld_c2(rrt, vo, 8 * (slide_rt_base<M>() + TPF * j));
     c2 tw3[15];  // pass 3 (M = 4096): p' = 0, wave-uniform
     if constexpr (M == 4096) {
 #pragma unroll
@@ -497,8 +527,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             tw3[j] = c2{t.re, t.im};
         }
     }
-    const c2 rt0 = ld_c2(rrt, 0, 8 * SH::RT_SPECIAL), rtM = ld_c2(rrt, 0, 8 * (SH::RT_SPECIAL + 1)),
-             rtH = ld_c2(rrt, 0, 8 * (SH::RT_SPECIAL + 2));
+    const c2 rtH = ld_c2(rrt, 0, 8 * (slide_rt_base<M>() + 8 * TPF));  // bin M/2
+    // last-pass columns and the bins of the post slots
+    int colA, colA2, colB, colB2;
+    if constexpr (M == 4096) {
+        colA = slide_col8(lt);
+        colA2 = colB = colB2 = 0;
+    } else {
+        slide_cols2(lt, &colA, &colA2, &colB, &colB2);
+    }
+    const bool self0 = M == 4096 ? (threadIdx.x == 0) : (lt == 0);  // the column-0 thread
+    const bool self128 = M == 4096 && threadIdx.x == 32;             // the column-128 lane (N = 8192)
+    // N = 8192: the partner lane (l ^ 32), or the lane itself for the self-paired columns
+    const int src_lane = (self0 || self128) ? (threadIdx.x & 63) : ((threadIdx.x & 63) ^ 32);
 
     // every per-strip load has landed before the frame loop: the loop header then carries no
     // pending load, so the compiler does not wait there for the previous frame's stores
@@ -533,28 +574,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             for (int k = 0; k < 16; k++) bufB[wb + P17 * k] = v[k];
         }
         frame_sync<TPF>();
-        if constexpr (M == 4096) {  // pass 3 (n = 16, s = 256, p' = 0), in place in B
-            const int rb = lpad(lt);
-#pragma unroll
-            for (int k = 0; k < 16; k++) v[k] = bufB[rb + P272 * k];
-            radix16<true>(v, tw3);
-#pragma unroll
-            for (int k = 0; k < 16; k++) bufB[rb + P272 * k] = v[k];
-        } else {  // trailing radix-4 (n = 4, s = M/4, p = 0), in place in B
-#pragma unroll
-            for (int r = 0; r < (M / 4) / TPF; r++) {
-                const int b = lpad(lt + TPF * r);
-                c2 y0, y1, y2, y3;
-                bfly4<false>(bufB[b], bufB[b + P272], bufB[b + 2 * P272], bufB[b + 3 * P272], c2{}, c2{}, c2{}, y0, y1,
-                             y2, y3);
-                bufB[b] = y0;
-                bufB[b + P272] = y1;
-                bufB[b + 2 * P272] = y2;
-                bufB[b + 3 * P272] = y3;
-            }
-        }
-        frame_sync<TPF>();
-        // post-processing from B (see k_stft_mag); rt[M-k] = (-rt[k].re, rt[k].im)
+        // last pass, then the post-processing from registers (sdsp_fft_spec.h STFT section):
+        //   S = Z[k] + conj(Z[M-k]),  D' = (Z[k].im + Z[M-k].im, -(Z[k].re - Z[M-k].re)),
+        //   Y = S + rt[k] D' (FMA form),  |X[k]| = 0.5 sqrt(fma(Y.re, Y.re, Y.im Y.im));  bin M-k from the
+        //   same S, D' conjugated with rt[M-k] = (-rt[k].re, rt[k].im).
         float* out = mags + (mag_row0[trk] + f) * (uint64_t)stride;
         float mx = 0.0f;
         uint32_t lo = 0xFFFFFFFFu, hi = 0u;
@@ -571,33 +594,70 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #endif
             if (FRAME_MAX) mx = sd_maxf(mx, mag);
         };
+        // one pair: own bin k from Zk, partner bin M-k from Zr, post twiddle w = rt[k]
+        auto pair = [&](c2 Zk, c2 Zr, c2 w, int k) {
+            const float sx = Zk.x + Zr.x, sy = Zk.y - Zr.y, dx = Zk.y + Zr.y, dy = -(Zk.x - Zr.x);
+            put(k, sq(__builtin_fmaf(w.x, dx, __builtin_fmaf(-w.y, dy, sx)), __builtin_fmaf(w.x, dy, __builtin_fmaf(w.y, dx, sy))));
+            put(M - k, sq(__builtin_fmaf(-w.x, dx, __builtin_fmaf(w.y, dy, sx)), __builtin_fmaf(w.x, dy, __builtin_fmaf(w.y, dx, -sy))));
+        };
+        auto single = [&](c2 Z, c2 w, int k) {  // a self-paired bin (k = M/2)
+            const float sx = Z.x + Z.x, sy = Z.y - Z.y, dx = Z.y + Z.y, dy = -(Z.x - Z.x);
+            put(k, sq(__builtin_fmaf(w.x, dx, __builtin_fmaf(-w.y, dy, sx)), __builtin_fmaf(w.x, dy, __builtin_fmaf(w.y, dx, sy))));
+        };
+        if constexpr (M == 4096) {
+            // pass 3 (n = 16, s = 256, p' = 0) on column colA: v[m] = Z[colA + 256 m]
+            const int rb = lpad(colA);
 #pragma unroll
-        for (int j = 0; j < SH::NPAIR; j++) {
-            const int k = 1 + lt + TPF * j;
-            if (j + 1 < SH::NPAIR || k < M / 2) {
-                const c2 Zk = bufB[lpad(k)], Zr = bufB[lpad(M - k)];
-                const float sx = Zk.x + Zr.x, sy = Zk.y - Zr.y, dx = Zk.y + Zr.y, dy = -(Zk.x - Zr.x);
-                const float a = wk[j].x, b = wk[j].y;
-                put(k, sq(__builtin_fmaf(a, dx, __builtin_fmaf(-b, dy, sx)), __builtin_fmaf(a, dy, __builtin_fmaf(b, dx, sy))));
-                // bin M-k: S' = conj(S), D'' = conj(D'), rt' = (-a, b)
-                put(M - k, sq(__builtin_fmaf(-a, dx, __builtin_fmaf(b, dy, sx)), __builtin_fmaf(a, dy, __builtin_fmaf(b, dx, -sy))));
+            for (int k = 0; k < 16; k++) v[k] = bufB[rb + P272 * k];
+            radix16<true>(v, tw3);
+            // exchange: every lane sends its elements 8..15 to the partner lane (ds_bpermute);
+            // the column-0 lane sends itself elements 9..15, 0 (its pairs are (m, 16 - m))
+            c2 rv[8];
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const c2 snd = self0 ? v[(9 + i) & 15] : v[8 + i];
+                rv[i] = {__shfl(snd.x, src_lane, 64), __shfl(snd.y, src_lane, 64)};
             }
-        }
-        if (lt == 0) {
-            const c2 Z0 = bufB[0];
-            const float sx = Z0.x + Z0.x, sy = Z0.y - Z0.y, dx = Z0.y + Z0.y, dy = -(Z0.x - Z0.x);
-            put(0, sq(__builtin_fmaf(rt0.x, dx, __builtin_fmaf(-rt0.y, dy, sx)), __builtin_fmaf(rt0.x, dy, __builtin_fmaf(rt0.y, dx, sy))));
-            put(M, sq(__builtin_fmaf(rtM.x, dx, __builtin_fmaf(-rtM.y, dy, sx)), __builtin_fmaf(rtM.x, dy, __builtin_fmaf(rtM.y, dx, sy))));
-        } else if (lt == 1) {
-            const c2 Zh = bufB[lpad(M / 2)];
-            const float sx = Zh.x + Zh.x, sy = Zh.y - Zh.y, dx = Zh.y + Zh.y, dy = -(Zh.x - Zh.x);
-            put(M / 2, sq(__builtin_fmaf(rtH.x, dx, __builtin_fmaf(-rtH.y, dy, sx)), __builtin_fmaf(rtH.x, dy, __builtin_fmaf(rtH.y, dx, sy))));
+            // pair j: Z[colA + 256 j] with the partner column's element 15 - j (= rv[7 - j])
+#pragma unroll
+            for (int j = 0; j < 8; j++) pair(v[j], rv[7 - j], wk[j], colA + 256 * j);
+            if (self0) single(v[8], rtH, M / 2);
+        } else {
+            // trailing radix-4 (n = 4, s = M/4, p = 0) on the thread's four columns
+            c2 A[4], A2[4], Bv[4], B2[4];
+            auto col4 = [&](int c, c2 (&z)[4]) {
+                const int b = lpad(c);
+                bfly4<false>(bufB[b], bufB[b + P272], bufB[b + 2 * P272], bufB[b + 3 * P272], c2{}, c2{}, c2{}, z[0],
+                             z[1], z[2], z[3]);
+            };
+            col4(colA, A);
+            col4(colA2, A2);
+            col4(colB, Bv);
+            col4(colB2, B2);
+            // pairs of (colA, colA2): (A[j], A2[3 - j]); thread 0 (columns 0 and 128, each self-paired):
+            // (A0, A0) -> bins 0 / M, (A1, A3) -> 256 / 768, (A2'0, A2'3) -> 128 / 896, (A2'1, A2'2) -> 384 / 640
+            const c2 zk0 = A[0], zr0 = self0 ? A[0] : A2[3];
+            const c2 zk1 = A[1], zr1 = self0 ? A[3] : A2[2];
+            const c2 zk2 = self0 ? A2[0] : A[2], zr2 = self0 ? A2[3] : A2[1];
+            const c2 zk3 = self0 ? A2[1] : A[3], zr3 = self0 ? A2[2] : A2[0];
+            pair(zk0, zr0, wk[0], self0 ? 0 : colA);
+            pair(zk1, zr1, wk[1], self0 ? 256 : colA + 256);
+            pair(zk2, zr2, wk[2], self0 ? 128 : colA + 512);
+            pair(zk3, zr3, wk[3], self0 ? 384 : colA + 768);
+#pragma unroll
+            for (int j = 0; j < 4; j++) pair(Bv[j], B2[3 - j], wk[4 + j], colB + 256 * j);
+            if (self0) single(A[2], rtH, M / 2);
         }
 #ifndef SDSP_EXP_NOSQRT
-        // a magnitude^2 of subnormal scale (or inf / NaN): redo this thread's bins with the general
-        // sqrt and store them again (same thread, same addresses: the later store wins).  B is
-        // intact until this thread reaches the next barrier.
-        if (__builtin_expect(sqrt_fast_missed(lo, hi), 0)) mx = stft_post_exact<M>(bufB, lt, rtp, out);
+        // a magnitude^2 of subnormal scale (or inf / NaN) somewhere in the wave: the frame goes on
+        // the redo list, which k_stft_mag recomputes with the general sqrt right after this kernel
+        // (stream order), overwriting the whole row.  A frame may be listed by several waves.
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(sqrt_fast_missed(lo, hi)) != 0, 0)) {
+            if ((threadIdx.x & 63) == 0) {
+                const uint32_t at = atomicAdd(redo, 1u);
+                redo[1 + at] = (uint32_t)(frame_pfx[trk] + f);
+            }
+        }
 #endif
         if constexpr (FRAME_MAX) {
             static_assert(!FRAME_MAX || TPF == 64, "frame maxima: one wave per frame");
@@ -664,9 +724,22 @@ void stft_tables(int N, const std::vector<float>& tw, const std::vector<float>& 
             put(rtp, (size_t)(2 * j + 1) * TPF + lt, sym);
         }
     put(rtp, (size_t)sp + 0, &rt[0]);
-    put(rtp, (size_t)sp + 1, &rt[2 * (size_t)M]);
+    const float rtm[2] = {-rt[0], rt[1]};  // rt[M] := (-rt[0].re, rt[0].im), the symmetric rule at k = 0
+    put(rtp, (size_t)sp + 1, rtm);
     put(rtp, (size_t)sp + 2, &rt[2 * (size_t)(M / 2)]);
     put(rtp, (size_t)sp + 3, &tw[0]);
+    // k_stft_slide's post table: [slot j < 8][lane] = rt of the slot's own bin (slide_bin), then
+    // rt[M/2]; bins above M/2 take the symmetric value (-rt[M-k].re, rt[M-k].im)
+    const size_t sbase = (size_t)sp + 4;
+    rtp->resize(2 * (sbase + 8 * (size_t)TPF + 1), 0.0f);
+    for (int j = 0; j < 8; j++)
+        for (int lt = 0; lt < TPF; lt++) {
+            const int k = slide_bin(M, lt, j);
+            const float v[2] = {k <= M / 2 ? rt[2 * (size_t)k] : -rt[2 * (size_t)(M - k)],
+                                k <= M / 2 ? rt[2 * (size_t)k + 1] : rt[2 * (size_t)(M - k) + 1]};
+            put(rtp, sbase + (size_t)j * TPF + lt, v);
+        }
+    put(rtp, sbase + 8 * (size_t)TPF, &rt[2 * (size_t)(M / 2)]);
 }
 
 // hop = S * 2 * TPF complex values with a k_stft_slide instance
@@ -682,14 +755,16 @@ bool stft_slide_ok(int nfft, int hop) {
 void launch_stft(int nfft, bool frame_max, const float* samples, const uint64_t* frame_pfx, int n_tracks,
                  uint64_t total_frames, const uint64_t* src_off, const float* gain, int hop, const float* window,
                  const cx* twp, const cx* rtp, float* mags, const uint64_t* mag_row0, int stride, float* fmax,
-                 hipStream_t st, const uint64_t* strip_pfx, uint64_t n_strips) {
+                 hipStream_t st, const uint64_t* strip_pfx, uint64_t n_strips, uint32_t* redo) {
     if (total_frames == 0) return;
     const dim3 block(256);
-    if (strip_pfx && n_strips && stft_slide_ok(nfft, hop)) {
+    if (strip_pfx && n_strips && redo && stft_slide_ok(nfft, hop)) {
+        // redo[0] = 0; redo[1..] receives the frames the sliding kernel could not finish exactly
+        SDSP_HIP_CHECK(hipMemsetAsync(redo, 0, sizeof(uint32_t), st));
 #define SDSP_SLIDE(N, S, FM)                                                                                      \
     hipLaunchKernelGGL((k_stft_slide<N, S, FM>), dim3((unsigned)((n_strips + 256 / (N / 32) - 1) / (256 / (N / 32)))), \
                        block, 0, st, samples, frame_pfx, strip_pfx, n_tracks, n_strips, src_off, gain, hop, window, twp, \
-                       rtp, mags, mag_row0, stride, fmax)
+                       rtp, mags, mag_row0, stride, fmax, redo)
         if (nfft == 8192) {
             if (hop == 512)
                 SDSP_SLIDE(8192, 1, false);
@@ -711,19 +786,31 @@ void launch_stft(int nfft, bool frame_max, const float* samples, const uint64_t*
                 SDSP_SLIDE(2048, 8, false);
         }
 #undef SDSP_SLIDE
+        // the redo pass: a few workgroups that read the count and exit when it is 0
+        const dim3 rgrid(nfft == 2048 ? 64 : 256);
+        if (nfft == 8192)
+            hipLaunchKernelGGL((k_stft_mag<8192, false>), rgrid, block, 0, st, samples, frame_pfx, n_tracks, total_frames,
+                               src_off, gain, hop, window, twp, rtp, mags, mag_row0, stride, fmax, redo);
+        else if (frame_max)
+            hipLaunchKernelGGL((k_stft_mag<2048, true>), rgrid, block, 0, st, samples, frame_pfx, n_tracks, total_frames,
+                               src_off, gain, hop, window, twp, rtp, mags, mag_row0, stride, fmax, redo);
+        else
+            hipLaunchKernelGGL((k_stft_mag<2048, false>), rgrid, block, 0, st, samples, frame_pfx, n_tracks, total_frames,
+                               src_off, gain, hop, window, twp, rtp, mags, mag_row0, stride, fmax, redo);
         return;
     }
     if (nfft == 2048) {
         const dim3 grid((unsigned)((total_frames + 3) / 4));
         if (frame_max)
             hipLaunchKernelGGL((k_stft_mag<2048, true>), grid, block, 0, st, samples, frame_pfx, n_tracks,
-                               total_frames, src_off, gain, hop, window, twp, rtp, mags, mag_row0, stride, fmax);
+                               total_frames, src_off, gain, hop, window, twp, rtp, mags, mag_row0, stride, fmax, nullptr);
         else
             hipLaunchKernelGGL((k_stft_mag<2048, false>), grid, block, 0, st, samples, frame_pfx, n_tracks,
-                               total_frames, src_off, gain, hop, window, twp, rtp, mags, mag_row0, stride, fmax);
+                               total_frames, src_off, gain, hop, window, twp, rtp, mags, mag_row0, stride, fmax, nullptr);
     } else if (nfft == 8192) {
         hipLaunchKernelGGL((k_stft_mag<8192, false>), dim3((unsigned)total_frames), block, 0, st, samples, frame_pfx,
-                           n_tracks, total_frames, src_off, gain, hop, window, twp, rtp, mags, mag_row0, stride, fmax);
+                           n_tracks, total_frames, src_off, gain, hop, window, twp, rtp, mags, mag_row0, stride, fmax,
+                           nullptr);
     }
 }
 

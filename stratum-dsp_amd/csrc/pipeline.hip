@@ -881,7 +881,7 @@ void Pipeline::tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPa
         const std::vector<uint64_t> ostr = stft_strips(opfx);
         launch_stft(FS, true, in.samples, d_opfx, P_T, stft_frames, c_.up(tag + "osrc", osrc), d_gain, 2 * hop,
                     tb.window.as<float>(), tb.stft_tw.as<cx>(), tb.stft_rt.as<cx>(), o.mags, d_opfx, STRIDE2, o.fmax,
-                    d_.stream, c_.up(tag + "ostrip", ostr), ostr.back());
+                    d_.stream, c_.up(tag + "ostrip", ostr), ostr.back(), c_.dev<uint32_t>(tag + "redo", stft_frames + 1));
         SDSP_HIP_CHECK(hipGetLastError());
         rm = RowMap{in.base_mags, o.mags, in.base_fmax, o.fmax, c_.up(tag + "brow", in.base_row0), d_opfx, 0, 1, 1};
     } else {
@@ -890,7 +890,7 @@ void Pipeline::tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPa
         const std::vector<uint64_t> str = stft_strips(o.fpfx);
         launch_stft(FS, true, in.samples, o.d_fpfx, P_T, total, d_src, d_gain, hop, tb.window.as<float>(),
                     tb.stft_tw.as<cx>(), tb.stft_rt.as<cx>(), o.mags, o.d_fpfx, STRIDE2, o.fmax, d_.stream,
-                    c_.up(tag + "strip", str), str.back());
+                    c_.up(tag + "strip", str), str.back(), c_.dev<uint32_t>(tag + "redo", total + 1));
         SDSP_HIP_CHECK(hipGetLastError());
         stft_frames = total;
     }
@@ -1278,7 +1278,8 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         SDSP_HIP_CHECK(hipStreamWaitEvent(st2, kt.ev[7], 0));
         kt.mark(0, st2);
         launch_stft(KFS, false, d_samples, d_kpfx, NK, total8, d_ksrc, d_kgain, KHOP, t8.window.as<float>(), t8.stft_tw.as<cx>(),
-                    t8.stft_rt.as<cx>(), mags8, d_kpfx, STRIDE8, nullptr, st2, d_kstr, kstr.back());
+                    t8.stft_rt.as<cx>(), mags8, d_kpfx, STRIDE8, nullptr, st2, d_kstr, kstr.back(),
+                    c_.dev<uint32_t>("E.redo", total8 + 1));
         SDSP_HIP_CHECK(hipGetLastError());
         kt.mark(1, st2);
         // key spectrogram conditioning (src/lib.rs:1011-1060)

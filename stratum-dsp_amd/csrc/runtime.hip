@@ -292,8 +292,9 @@ int32_t sdsp_probe_stft(int32_t device, uint64_t nfft, uint64_t hop, uint64_t n_
         }
         const bool frame_parallel = std::getenv("SDSP_STFT_FRAME_PARALLEL") != nullptr;  // A/B switch
         const std::vector<uint64_t> sp = stft_strips(pf);
-        DevBuf strips;
+        DevBuf strips, redo;
         strips.ensure(sp.size() * 8);
+        redo.ensure((total + 1) * 4);
         SDSP_HIP_CHECK(hipMemcpy(strips.p, sp.data(), sp.size() * 8, hipMemcpyHostToDevice));
         pfx.ensure(pf.size() * 8);
         off.ensure(o.size() * 8);
@@ -310,7 +311,7 @@ int32_t sdsp_probe_stft(int32_t device, uint64_t nfft, uint64_t hop, uint64_t n_
             launch_stft((int)nfft, nfft == 2048, x.as<float>(), pfx.as<uint64_t>(), (int)n_tracks, total,
                         off.as<uint64_t>(), g.as<float>(), (int)hop, tb.window.as<float>(), tb.stft_tw.as<cx>(),
                         tb.stft_rt.as<cx>(), mags.as<float>(), row0.as<uint64_t>(), stride, fmax.as<float>(), c.stream,
-                        frame_parallel ? nullptr : strips.as<uint64_t>(), sp.back());
+                        frame_parallel ? nullptr : strips.as<uint64_t>(), sp.back(), redo.as<uint32_t>());
         };
         launch();  // warm: first touch of the output pages
         SDSP_HIP_CHECK(hipEventRecord(e0, c.stream));
@@ -353,8 +354,9 @@ int32_t sdsp_debug_stft(const float* host_x, uint64_t n, uint64_t nfft, uint64_t
         row0.ensure(8);
         const uint64_t pf[2] = {0, frames}, o0 = 0, r0 = 0;
         const std::vector<uint64_t> sp = stft_strips(std::vector<uint64_t>{0, frames});
-        DevBuf strips;
+        DevBuf strips, redo;
         strips.ensure(16);
+        redo.ensure((frames + 1) * 4);
         SDSP_HIP_CHECK(hipMemcpy(strips.p, sp.data(), 16, hipMemcpyHostToDevice));
         // SDSP_STFT_FRAME_PARALLEL=1: the frame-parallel kernel (k_stft_mag) for every hop
         const bool frame_parallel = std::getenv("SDSP_STFT_FRAME_PARALLEL") != nullptr;
@@ -366,7 +368,7 @@ int32_t sdsp_debug_stft(const float* host_x, uint64_t n, uint64_t nfft, uint64_t
         launch_stft((int)nfft, nfft == 2048, x.as<float>(), pfx.as<uint64_t>(), 1, frames, off.as<uint64_t>(),
                     g.as<float>(), (int)hop, tb.window.as<float>(), tb.stft_tw.as<cx>(), tb.stft_rt.as<cx>(), mags.as<float>(),
                     row0.as<uint64_t>(), stride, fmax.as<float>(), c.stream, frame_parallel ? nullptr : strips.as<uint64_t>(),
-                    sp.back());
+                    sp.back(), redo.as<uint32_t>());
         SDSP_HIP_CHECK(hipGetLastError());
         SDSP_HIP_CHECK(hipStreamSynchronize(c.stream));
         SDSP_HIP_CHECK(hipMemcpy2D(host_out, (size_t)bins * 4, mags.p, (size_t)stride * 4, (size_t)bins * 4,

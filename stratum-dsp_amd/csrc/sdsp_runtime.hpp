@@ -86,7 +86,7 @@ void stft_tables(int N, const std::vector<float>& tw, const std::vector<float>& 
 void launch_stft(int nfft, bool frame_max, const float* samples, const uint64_t* frame_pfx, int n_tracks,
                  uint64_t total_frames, const uint64_t* src_off, const float* gain, int hop, const float* window,
                  const cx* tw, const cx* rt, float* mags, const uint64_t* mag_row0, int stride, float* fmax,
-                 hipStream_t st, const uint64_t* strip_pfx = nullptr, uint64_t n_strips = 0);
+                 hipStream_t st, const uint64_t* strip_pfx = nullptr, uint64_t n_strips = 0, uint32_t* redo = nullptr);
 // the sliding-strip STFT (k_stft.hip): strip prefix over tracks from the frame prefix, and the
 // (nfft, hop) pairs it serves
 std::vector<uint64_t> stft_strips(const std::vector<uint64_t>& frame_pfx);
