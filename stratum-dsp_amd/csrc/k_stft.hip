@@ -586,13 +586,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #else
         auto sq = [&](float yx, float yy) { return 0.5f * sqrt_fast(__builtin_fmaf(yx, yx, yy * yy), lo, hi); };
 #endif
+        // frame maximum: magnitudes are +0 or positive, so v_max_f32 (IEEE maxNum: a NaN operand
+        // yields the other) is sd_maxf here except for the payload of an all-NaN row
         auto put = [&](int k, float mag) {
 #ifdef SDSP_EXP_NOSTORE
             if (mag == 1234.5f) out[k] = mag;
 #else
             out[k] = mag;
 #endif
-            if (FRAME_MAX) mx = sd_maxf(mx, mag);
+            if (FRAME_MAX) mx = __builtin_fmaxf(mx, mag);
         };
         // one pair: own bin k from Zk, partner bin M-k from Zr, post twiddle w = rt[k]
         auto pair = [&](c2 Zk, c2 Zr, c2 w, int k) {
