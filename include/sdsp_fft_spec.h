@@ -43,7 +43,11 @@
  *        D' = (Zk.im + Zr.im, -(Zk.re - Zr.re))          (-i (Zk - conj(Zr)))
  *        Y.re = fma(rt.re, D'.re, fma(-rt.im, D'.im, S.re))
  *        Y.im = fma(rt.re, D'.im, fma(rt.im, D'.re, S.im))
- *        |X[k]| = 0.5 * sqrt(fma(Y.re, Y.re, Y.im * Y.im))    (X = Y / 2; sqrt correctly rounded)
+ *        |X[k]| = 2^-33 * sqrt(fma(Y.re, Y.re, Y.im * Y.im))    (sqrt correctly rounded)
+ *     where the frame is windowed with w[i] * 2^32 (an exact scaling of the Hann table), so
+ *     Y = 2^33 X: |X|^2 * 2^66 stays above the subnormal range for any audible input, the range in
+ *     which the kernels' fast correctly rounded sqrt is exact, and the scaling itself changes no
+ *     rounding (powers of two commute with round-to-nearest away from subnormals);
  * FMA is a single rounding on both sides (gfx950 v_fma_f32 / x86 vfmadd), so the STFT stays
  * bit-identical between the CPU restatement and the kernels, at about two thirds of the
  * general section's arithmetic.  tests/test_spec.py checks it against numpy float64 too.

@@ -166,7 +166,8 @@ static void stft_fft_complex(std::vector<Cx>& x, std::vector<Cx>& y) {
 
 // |X[k]|, k = 0..n/2, of a real frame of n samples: z[j] = (x[2j], x[2j+1]), Z = FFT_M(z),
 // S = Z[k] + conj(Z[M-k]), D' = -i (Z[k] - conj(Z[M-k])), Y = S + rt[k] D' (two FMAs per
-// component), |X[k]| = 0.5 * sqrt(fma(Y.re, Y.re, Y.im * Y.im)); the post twiddles are symmetric,
+// component), |X[k]| = 2^-33 * sqrt(fma(Y.re, Y.re, Y.im * Y.im)) (the frame carries the window's
+// 2^32, so Y = 2^33 X); the post twiddles are symmetric,
 // rt[M-k] = (-rt[k].re, rt[k].im) for 0 <= k < M/2.
 static void stft_mag(const float* x, size_t n, float* mag, std::vector<Cx>& z, std::vector<Cx>& tmp) {
     const size_t M = n / 2;
@@ -183,7 +184,7 @@ static void stft_mag(const float* x, size_t n, float* mag, std::vector<Cx>& z, s
         const float dre = Zk.im + Zr.im, dim = -(Zk.re - Zr.re);
         const float yre = std::fma(w.re, dre, std::fma(-w.im, dim, sre));
         const float yim = std::fma(w.re, dim, std::fma(w.im, dre, sim));
-        mag[k] = 0.5f * std::sqrt(std::fma(yre, yre, yim * yim));
+        mag[k] = 0x1p-33f * std::sqrt(std::fma(yre, yre, yim * yim));
     }
 }
 
@@ -194,7 +195,8 @@ Spec compute_stft(const float* s, size_t n_samples, size_t frame_size, size_t ho
     const size_t n_frames = (n_samples - frame_size) / hop + 1;
     const size_t n_bins = frame_size / 2 + 1;
     std::vector<float> window(frame_size);
-    for (size_t i = 0; i < frame_size; i++) window[i] = sdsp_hann_f32((int)i, (int)frame_size);
+    // the STFT section's window carries 2^32 (exact; |X| carries 2^-33, see stft_mag)
+    for (size_t i = 0; i < frame_size; i++) window[i] = sdsp_hann_f32((int)i, (int)frame_size) * 0x1p32f;
     out.frames = n_frames;
     out.bins = n_bins;
     out.d.resize(n_frames * n_bins);

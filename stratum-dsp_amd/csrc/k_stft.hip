@@ -309,9 +309,9 @@ __device__ __forceinline__ void stft_mag_frame(const float* __restrict__ samples
         const float yx = __builtin_fmaf(wt.x, dx, __builtin_fmaf(-wt.y, dy, sx));
         const float yy = __builtin_fmaf(wt.x, dy, __builtin_fmaf(wt.y, dx, sy));
 #ifdef SDSP_EXP_NOSQRT  // ablation: hardware sqrt, not correctly rounded
-        return 0.5f * __builtin_amdgcn_sqrtf(__builtin_fmaf(yx, yx, yy * yy));
+        return 0x1p-33f * __builtin_amdgcn_sqrtf(__builtin_fmaf(yx, yx, yy * yy));
 #else
-        return 0.5f * sqrt_cr(__builtin_fmaf(yx, yx, yy * yy));
+        return 0x1p-33f * sqrt_cr(__builtin_fmaf(yx, yx, yy * yy));
 #endif
     };
     auto put = [&](int k, float mag) {
@@ -576,15 +576,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         frame_sync<TPF>();
         // last pass, then the post-processing from registers (sdsp_fft_spec.h STFT section):
         //   S = Z[k] + conj(Z[M-k]),  D' = (Z[k].im + Z[M-k].im, -(Z[k].re - Z[M-k].re)),
-        //   Y = S + rt[k] D' (FMA form),  |X[k]| = 0.5 sqrt(fma(Y.re, Y.re, Y.im Y.im));  bin M-k from the
+        //   Y = S + rt[k] D' (FMA form),  |X[k]| = 2^-33 sqrt(fma(Y.re, Y.re, Y.im Y.im)) (the window carries
+        //   2^32, so Y = 2^33 X);  bin M-k from the
         //   same S, D' conjugated with rt[M-k] = (-rt[k].re, rt[k].im).
         float* out = mags + (mag_row0[trk] + f) * (uint64_t)stride;
         float mx = 0.0f;
         uint32_t lo = 0xFFFFFFFFu, hi = 0u;
 #ifdef SDSP_EXP_NOSQRT
-        auto sq = [&](float yx, float yy) { return 0.5f * __builtin_amdgcn_sqrtf(__builtin_fmaf(yx, yx, yy * yy)); };
+        auto sq = [&](float yx, float yy) { return 0x1p-33f * __builtin_amdgcn_sqrtf(__builtin_fmaf(yx, yx, yy * yy)); };
 #else
-        auto sq = [&](float yx, float yy) { return 0.5f * sqrt_fast(__builtin_fmaf(yx, yx, yy * yy), lo, hi); };
+        auto sq = [&](float yx, float yy) { return 0x1p-33f * sqrt_fast(__builtin_fmaf(yx, yx, yy * yy), lo, hi); };
 #endif
         // frame maximum: magnitudes are +0 or positive, so v_max_f32 (IEEE maxNum: a NaN operand
         // yields the other) is sd_maxf here except for the payload of an all-NaN row
@@ -789,7 +790,7 @@ void launch_stft(int nfft, bool frame_max, const float* samples, const uint64_t*
         }
 #undef SDSP_SLIDE
         // the redo pass: a few workgroups that read the count and exit when it is 0
-        const dim3 rgrid(nfft == 2048 ? 64 : 256);
+        const dim3 rgrid(256);
         if (nfft == 8192)
             hipLaunchKernelGGL((k_stft_mag<8192, false>), rgrid, block, 0, st, samples, frame_pfx, n_tracks, total_frames,
                                src_off, gain, hop, window, twp, rtp, mags, mag_row0, stride, fmax, redo);

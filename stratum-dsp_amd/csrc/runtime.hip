@@ -70,7 +70,9 @@ FftTables& DeviceCtx::tables(int N, bool with_window) {
     }
     if (with_window && !t->window.p) {
         std::vector<float> w((size_t)N);
-        for (int i = 0; i < N; i++) w[(size_t)i] = sdsp_hann_f32(i, N);  // extractor.rs:318-323
+        // extractor.rs:318-323, times 2^32 (exact): the STFT section of sdsp_fft_spec.h scales the
+        // windowed frame so |X|^2 stays clear of the subnormal range, and |X| carries 2^-33
+        for (int i = 0; i < N; i++) w[(size_t)i] = sdsp_hann_f32(i, N) * 0x1p32f;
         t->window.ensure(w.size() * 4);
         SDSP_HIP_CHECK(hipMemcpy(t->window.p, w.data(), w.size() * 4, hipMemcpyHostToDevice));
         std::vector<float> tw(2 * (size_t)(N / 2)), rt((size_t)N + 2), a, b;
