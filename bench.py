@@ -259,6 +259,12 @@ def main():
         if (stft["ms2"] + stft["ms8"]) > 0 else None,
     }
 
+    if not args.dry_run and rank == 0:
+        # the same kernel launched alone (nothing else on the chip): the kernel's own bandwidth, as
+        # opposed to `achieved` above, which is measured inside the two-stream pipeline where the
+        # tempo path shares the CUs (tools/stft_probe.py)
+        roofline["isolated"] = isolated_stft(8192 if key_k else 2048, 512, int(lens.max()) if len(lens) else 0)
+
     cpu = None
     parity = None
     extras = {}
@@ -321,6 +327,29 @@ def main():
         print(json.dumps(out), flush=True)
     if tdist is not None:
         tdist.destroy_process_group()
+
+
+def isolated_stft(nfft, hop, length, tracks=32, reps=3):
+    """sdsp_probe_stft: `reps` launches of the STFT kernel alone over `tracks` device-resident
+    noise tracks of `length` samples, HIP events on its stream."""
+    import ctypes as C
+
+    if length < nfft:
+        return None
+    L = sdsp.lib()
+    f = L.sdsp_probe_stft
+    f.argtypes = [C.c_int32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int32, C.c_int32,
+                  C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    f.restype = C.c_int32
+    ms, by = C.c_double(), C.c_double()
+    stride = 4160 if nfft == 8192 else 1028  # the pipeline's row strides (pipeline.hip STRIDE8 / STRIDE2)
+    if f(0, nfft, hop, tracks, length, reps, stride, C.byref(ms), C.byref(by)) != 0:
+        return None
+    gbs = by.value / (ms.value * 1e-3) / 1e9
+    return {"kernel": f"k_stft_slide<{nfft}>", "tracks": tracks, "ms_per_launch": round(ms.value, 3),
+            "ms_per_track": round(ms.value / tracks, 5), "achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+            "method": "sdsp_probe_stft: the kernel launched alone on device-resident noise tracks of the workload's "
+                      "length, HIP events, mean of 3 launches"}
 
 
 def bpm_only_check(eng, buf, offs, lens, sr, res, k):

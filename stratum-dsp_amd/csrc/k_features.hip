@@ -111,7 +111,11 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
             const int r = sub + u * RSTEP;
             if (r < ROWS) {
                 Mt[r][slot] = nx[u];
+#ifdef SDSP_EXP_FT_NOLOG
+                Lt[r][slot] = nx[u] * 0.5f;
+#else
                 Lt[r][slot] = sd_logf_ge1(1.0f + sd_maxf(nx[u], 0.0f), ltab);
+#endif
             }
         }
     };
@@ -154,7 +158,11 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
                     h[v] += hh;
                 }
             const float lc = Lt[i + 1][s];
+#ifndef SDSP_EXP_FT_NOMEL
             if (P.n_mels > 0) {
+#else
+            if (false) {
+#endif
                 const MelPlan mp = mel[b];
                 for (int q = 0; q < mp.nflush; q++) {
                     MEL[(uint64_t)mA * total + g] = accA;
@@ -176,8 +184,13 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
             }
             if (has_prev) {
                 const float mp = Mt[i][s];
+#ifdef SDSP_EXP_FT_NODIV
+                const float pv = pn ? mp * mx_p : 0.0f;
+                const float cv = cn ? m * mx_c : 0.0f;
+#else
                 const float pv = pn ? mp / mx_p : 0.0f;
                 const float cv = cn ? m / mx_c : 0.0f;
+#endif
                 const float d = max_bnn(cv - pv, 0.0f);
                 so += d * d;
                 // SuperFlux, full band window [b-K, b+K] clipped to [0, B).  Every L >= +0 and
@@ -186,7 +199,11 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
                 const int lo = b - K < 0 ? 0 : b - K;
                 const int hi = b + K + 1 < B ? b + K + 1 : B;
                 float pm = 0.0f;
+#ifdef SDSP_EXP_FT_NOSF
+                if (false) {
+#else
                 if constexpr (KK > 0) {
+#endif
                     pm = Rw[j];
 #pragma unroll
                     for (int q = 1; q <= 2 * KK; q++) pm = max_bnn(pm, Rw[j + q]);
