@@ -27,13 +27,7 @@
 
 namespace sdsp {
 
-// LDS visibility within one wave: its LDS operations complete in order, so a wave-scope fence +
-// wave barrier suffices (no workgroup barrier)
-__device__ __forceinline__ void ft_wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
+
 
 // KK > 0: compile-time SuperFlux half width (the default 4) -- the previous frame's logs for
 // the chunk's windows are read once into registers and every bin's window max is taken from
@@ -262,253 +256,11 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
     }
 }
 
-// -----------------------------------------------------------------------------------------------
-// k_features_w: the same per-frame folds, one WAVE per 64 consecutive frames (lane = frame), so
-// the bin walk needs only wave-level synchronisation (the workgroup version above pays two
-// workgroup barriers per 8 bins).  Per wave, three LDS rings of W = CW + 2K = 24 bin columns x 65
-// rows (frames f0-1 .. f0+63): magnitudes M, normalised magnitudes N = M / max_t (spectral_flux.rs
-// :120-128, computed once per element instead of twice) and L = ln(1 + max(M, 0)).  Bins are
-// staged K ahead of the walk (the SuperFlux window's right halo) with float4 loads that are issued
-// one chunk ahead of their commit.  The ring slot of bin b is (b + 24) % 24: b is wave-uniform,
-// so the modulo is scalar.
-//
-// N uses the reciprocal-correction quotient y = RN(1/max), q = RN(M y), r = fma(-q, max, M),
-// N = fma(r, y, q), which equals the IEEE quotient M / max whenever neither M nor the result is
-// below 2^-100 (Markstein; tools/micro/check_div_rcp.c finds no mismatch in 3.4e9 quotients);
-// below that the kernel divides.
-constexpr int FW_FRAMES = 64;
-constexpr int FW_CW = 16;
-
-template <int KK>
-__global__ __launch_bounds__(128) void k_features_w(const RowMap rm, const uint64_t* __restrict__ frame_pfx,
-                                                    const uint64_t* __restrict__ wtile_pfx, int T, uint64_t n_wtiles,
-                                                    FeatParams P, const MelPlan* __restrict__ mel,
-                                                    float* __restrict__ E, float* __restrict__ H,
-                                                    float* __restrict__ SFX, float* __restrict__ SFO,
-                                                    float* __restrict__ MEL, uint64_t total) {
-    constexpr int CW = FW_CW, W = CW + 2 * KK, R = FW_FRAMES + 1, LS = W + 1;
-    constexpr int NW = 2;  // waves per workgroup
-    static_assert(KK > 0 && KK <= CW, "staging runs KK bins ahead by less than one chunk");
-    __shared__ float Ms[NW][R][LS], Ns[NW][R][LS], Ls[NW][R][LS];
-    __shared__ sd_logtab_t ltab[128];
-    for (int q = threadIdx.x; q < 128; q += 64 * NW) ltab[q] = SD_LOGTAB_D[q];
-    __syncthreads();
-
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint64_t wt =
-        (uint64_t)__builtin_amdgcn_readfirstlane((int)((uint64_t)xcd_block(blockIdx.x, gridDim.x) * NW + wv));
-    if (wt >= n_wtiles) return;  // whole waves only; no workgroup barrier below
-    float(*Mw)[LS] = Ms[wv];
-    float(*Nw)[LS] = Ns[wv];
-    float(*Lw)[LS] = Ls[wv];
-    const int trk = find_track(wtile_pfx, T, wt);
-    const int64_t F = (int64_t)(frame_pfx[trk + 1] - frame_pfx[trk]);
-    const int64_t f0 = (int64_t)(wt - wtile_pfx[trk]) * FW_FRAMES;
-    const uint64_t g0 = frame_pfx[trk];
-    const int64_t f = f0 + lane;
-    const bool valid = f < F;
-    const bool has_prev = valid && f >= 1;
-    const int B = P.B;
-    const uint64_t g = g0 + (uint64_t)f;
-    const uint64_t ra0 = rm.rowA0[trk], rb0 = rm.rowB0 ? rm.rowB0[trk] : ra0 + (uint64_t)rm.offB;
-    auto row_of = [&](int64_t fr, bool* odd) {
-        *odd = fr & 1;
-        return (*odd ? rb0 + (uint64_t)(fr >> 1) * (uint64_t)rm.stepB : ra0 + (uint64_t)(fr >> 1) * (uint64_t)rm.stepA);
-    };
-    auto fmax_of = [&](int64_t fr) {
-        bool odd;
-        const uint64_t r = row_of(fr, &odd);
-        return odd ? rm.fmaxB[r] : rm.fmaxA[r];
-    };
-    const float mx_c = valid ? fmax_of(f) : 0.0f;
-    const float mx_p = has_prev ? fmax_of(f - 1) : 0.0f;
-    const bool pn = mx_p > EPS;
-    (void)pn;
-
-    // staging rows of this lane: r = (lane >> 2) + 16 u, bins 4 (lane & 3) .. +3 of the unit
-    constexpr int NU = (R + 15) / 16;  // 5
-    const int q4 = lane & 3;
-    const float* rowp[NU];
-    float rmx[NU], ry[NU];
-#pragma unroll
-    for (int u = 0; u < NU; u++) {
-        const int r = (lane >> 2) + 16 * u;
-        const int64_t fr = f0 - 1 + r;
-        rowp[u] = nullptr;
-        rmx[u] = 0.0f;
-        ry[u] = 0.0f;
-        if (r < R && fr >= 0 && fr < F) {
-            bool odd;
-            const uint64_t row = row_of(fr, &odd);
-            rowp[u] = (odd ? rm.magsB : rm.magsA) + row * (uint64_t)P.stride;
-            rmx[u] = odd ? rm.fmaxB[row] : rm.fmaxA[row];
-            ry[u] = 1.0f / rmx[u];  // IEEE reciprocal (only used when rmx > EPS)
-        }
-    }
-    // a staging unit covers bins [b0, b0 + CW); its float4 loads land in nx
-    float4 nx[NU];
-    auto load = [&](int b0) {
-        const int b = b0 + 4 * q4;
-#pragma unroll
-        for (int u = 0; u < NU; u++) {
-            nx[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            if (rowp[u] && b >= 0) {
-                if (b + 3 < B)
-                    nx[u] = *reinterpret_cast<const float4*>(rowp[u] + b);
-                else {  // the last, partial column group
-                    float t[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-                    for (int c = 0; c < 4; c++)
-                        if (b + c < B) t[c] = rowp[u][b + c];
-                    nx[u] = make_float4(t[0], t[1], t[2], t[3]);
-                }
-            }
-        }
-    };
-    auto norm = [](float m, float mx, float y) {  // m / mx, or 0 when mx <= EPS (spectral_flux.rs:123-130)
-        if (!(mx > EPS)) return 0.0f;
-        const float q = m * y;
-        const float r = __builtin_fmaf(-q, mx, m);
-        float n = __builtin_fmaf(r, y, q);
-        if (__builtin_expect(sd_minf(n, m) < 0x1p-100f, 0)) n = m / mx;
-        return n;
-    };
-    auto commit = [&](int b0) {
-        const int slot0 = (b0 + W) % W + 4 * q4;  // b0 is wave-uniform: a scalar modulo
-#pragma unroll
-        for (int u = 0; u < NU; u++) {
-            const int r = (lane >> 2) + 16 * u;
-            if (r >= R) continue;
-            const float v[4] = {nx[u].x, nx[u].y, nx[u].z, nx[u].w};
-#pragma unroll
-            for (int c = 0; c < 4; c++) {
-                const int slot = slot0 + c >= W ? slot0 + c - W : slot0 + c;
-                Mw[r][slot] = v[c];
-                Nw[r][slot] = norm(v[c], rmx[u], ry[u]);
-                Lw[r][slot] = sd_logf_ge1(1.0f + sd_maxf(v[c], 0.0f), ltab);  // bins < 0 and >= B: 0
-            }
-        }
-    };
-    float e[4] = {0, 0, 0, 0}, h[4] = {0, 0, 0, 0}, sx[4] = {0, 0, 0, 0}, so = 0.0f;
-    float accA = 0.0f, accB = 0.0f;
-    int mA = 0;
-    const int i = lane;  // frame f0 + i is row i + 1; its previous frame is row i
-
-    // prologue: units [-CW + KK, KK) and [KK, KK + CW)
-    load(KK - CW);
-    commit(KK - CW);
-    load(KK);
-    for (int c0 = 0; c0 < B; c0 += CW) {
-        ft_wave_sync();  // the previous walk is done with the slots overwritten here
-        commit(c0 + KK);
-        ft_wave_sync();
-        if (c0 + CW < B) load(c0 + CW + KK);  // in flight during the walk
-        const int nb = B - c0 < CW ? B - c0 : CW;
-        if (!valid) continue;
-        // previous frame's L for bins [c0 - KK, c0 + CW + KK) (0 outside [0, B))
-        float Rw[CW + 2 * KK];
-        if (has_prev) {
-#pragma unroll
-            for (int q = 0; q < CW + 2 * KK; q++) Rw[q] = Lw[i][(c0 - KK + q + W) % W];
-        }
-#pragma unroll
-        for (int j = 0; j < CW; j++) {
-            if (j >= nb) break;
-            const int b = c0 + j;
-            const int s = (b + W) % W;
-            const float m = Mw[i + 1][s];
-            const float ee = m * m;
-            const float hh = (float)b * m * m;
-            e[0] += ee;
-            h[0] += hh;
-#pragma unroll
-            for (int v = 1; v < 4; v++)
-                if (P.band_on[v] && b >= P.bs[v] && b < P.be[v]) {
-                    e[v] += ee;
-                    h[v] += hh;
-                }
-            const float lc = Lw[i + 1][s];
-            if (P.n_mels > 0) {
-                const MelPlan mp = mel[b];
-                for (int q = 0; q < mp.nflush; q++) {
-                    MEL[(uint64_t)mA * total + g] = accA;
-                    accA = accB;
-                    accB = 0.0f;
-                    mA++;
-                }
-                // novelty.rs:181-186 skips v <= 0; adding +0 to a non-negative sum is exact
-                if (lc > 0.0f) {
-                    if (mp.w0 != 0.0f) {
-                        if (mp.s0 == 0) accA += lc * mp.w0;
-                        else accB += lc * mp.w0;
-                    }
-                    if (mp.w1 != 0.0f) {
-                        if (mp.s1 == 0) accA += lc * mp.w1;
-                        else accB += lc * mp.w1;
-                    }
-                }
-            }
-            if (has_prev) {
-                const float pv = Nw[i][s];
-                const float cv = Nw[i + 1][s];
-                const float d = max_bnn(cv - pv, 0.0f);
-                so += d * d;
-                // SuperFlux window [b-K, b+K] clipped to [0, B): max over the register window
-                // (entries outside [0, B) are +0, every L >= +0; see k_features)
-                float pm = Rw[j];
-#pragma unroll
-                for (int q = 1; q <= 2 * KK; q++) pm = max_bnn(pm, Rw[j + q]);
-                const float df = max_bnn(lc - pm, 0.0f);
-                sx[0] += df * df;
-                const int lo = b - KK < 0 ? 0 : b - KK;
-                const int hi = b + KK + 1 < B ? b + KK + 1 : B;
-#pragma unroll
-                for (int v = 1; v < 4; v++) {
-                    if (P.band_on[v] && b >= P.bs[v] && b < P.be[v]) {
-                        float pmb = pm;
-                        if (lo < P.bs[v] || hi > P.be[v]) {
-                            const int lb = lo < P.bs[v] ? P.bs[v] : lo;
-                            const int hb = hi > P.be[v] ? P.be[v] : hi;
-                            pmb = 0.0f;
-#pragma unroll
-                            for (int q = 0; q <= 2 * KK; q++)
-                                if (b - KK + q >= lb && b - KK + q < hb) pmb = max_bnn(pmb, Rw[j + q]);
-                        }
-                        const float db = max_bnn(lc - pmb, 0.0f);
-                        sx[v] += db * db;
-                    }
-                }
-            }
-        }
-    }
-    if (!valid) return;
-    for (; mA < P.n_mels; mA++) {
-        MEL[(uint64_t)mA * total + g] = accA;
-        accA = accB;
-        accB = 0.0f;
-    }
-#pragma unroll
-    for (int v = 0; v < 4; v++) {
-        E[(uint64_t)v * total + g] = e[v];
-        H[(uint64_t)v * total + g] = h[v];
-    }
-    if (has_prev) {
-        const uint64_t gp = g - 1;  // pair (t-1, t) stored at t-1
-        SFO[gp] = __builtin_sqrtf(so);
-#pragma unroll
-        for (int v = 0; v < 4; v++) SFX[(uint64_t)v * total + gp] = __builtin_sqrtf(sx[v]);
-    }
-}
-
 void launch_features(const RowMap& mags, const uint64_t* frame_pfx, const uint64_t* tile_pfx,
                      int T, uint64_t n_tiles, const FeatParams& P, const MelPlan* mel, float* E, float* H, float* SFX,
-                     float* SFO, float* MEL, uint64_t total, hipStream_t st, const uint64_t* wtile_pfx,
-                     uint64_t n_wtiles) {
+                     float* SFO, float* MEL, uint64_t total, hipStream_t st) {
     if (n_tiles == 0) return;
-    if (P.K == 4 && wtile_pfx && n_wtiles) {  // the default SuperFlux width: one wave per 64 frames
-        hipLaunchKernelGGL((k_features_w<4>), dim3((unsigned)((n_wtiles + 1) / 2)), dim3(128), 0, st, mags, frame_pfx,
-                           wtile_pfx, T, n_wtiles, P, mel, E, H, SFX, SFO, MEL, total);
-        return;
-    }
+
     // window must hold [c0-K, c0+CW+K): CW + 2K <= W
     if (P.K == 4)
         hipLaunchKernelGGL((k_features<8, 16, 4>), dim3((unsigned)n_tiles), dim3(FT_FRAMES), 0, st, mags,

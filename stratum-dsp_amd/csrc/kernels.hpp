@@ -232,9 +232,7 @@ void launch_consensus(const uint32_t* energy, const uint64_t* e_off, const int* 
                       hipStream_t st, int hpss = 0);
 void launch_features(const RowMap& mags, const uint64_t* frame_pfx, const uint64_t* tile_pfx,
                      int T, uint64_t n_tiles, const FeatParams& P, const MelPlan* mel, float* E, float* H, float* SFX,
-                     float* SFO, float* MEL, uint64_t total, hipStream_t st, const uint64_t* wtile_pfx = nullptr,
-                     uint64_t n_wtiles = 0);
-constexpr int FT_WFRAMES = 64;  // frames per wave tile of k_features_w
+                     float* SFO, float* MEL, uint64_t total, hipStream_t st);
 void launch_novelty(const float* E, const float* H, const float* SFX, const uint64_t* frame_pfx, int T, uint64_t total,
                     const NovParams& P, float* scratch, float* nov, float* nov_sum, const float* MEL, int n_mels,
                     int mel_k, bool mel_on, unsigned int* mel_max, hipStream_t st);

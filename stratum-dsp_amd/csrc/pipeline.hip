@@ -837,14 +837,13 @@ void Pipeline::tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPa
     const int FS = 2048, hop = in.hop;
     // frames per pass-track
     o.fpfx.assign((size_t)P_T + 1, 0);
-    std::vector<uint64_t> tpfx((size_t)P_T + 1, 0), wpfx((size_t)P_T + 1, 0);
+    std::vector<uint64_t> tpfx((size_t)P_T + 1, 0);
     o.active_h.assign((size_t)P_T, 0);
     for (int t = 0; t < P_T; t++) {
         const uint64_t n = in.n_trim[(size_t)t];
         const uint64_t F = n >= (uint64_t)FS ? (n - FS) / (uint64_t)hop + 1 : 0;
         o.fpfx[(size_t)t + 1] = o.fpfx[(size_t)t] + F;
         tpfx[(size_t)t + 1] = tpfx[(size_t)t] + (F + FT_FRAMES - 1) / FT_FRAMES;
-        wpfx[(size_t)t + 1] = wpfx[(size_t)t] + (F + FT_WFRAMES - 1) / FT_WFRAMES;
         o.active_h[(size_t)t] = F >= 2;
     }
     const uint64_t total = o.fpfx[(size_t)P_T];
@@ -943,10 +942,8 @@ void Pipeline::tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPa
     o.SFX = c_.dev<float>(tag + "SFX", 4 * total);
     o.SFO = c_.dev<float>(tag + "SFO", total);
     o.MEL = c_.dev<float>(tag + "MEL", std::max<uint64_t>(total * (uint64_t)std::max(fp.n_mels, 1), 1));
-    // SDSP_FEATURES_WG=1: the workgroup-per-256-frames kernel (A/B switch)
-    const bool ft_wg = std::getenv("SDSP_FEATURES_WG") != nullptr;
     launch_features(rm, o.d_fpfx, d_tpfx, P_T, tpfx[(size_t)P_T], fp, d_mplan, o.E, o.H, o.SFX, o.SFO,
-                    o.MEL, total, d_.stream, ft_wg ? nullptr : c_.up(tag + "wtpfx", wpfx), wpfx[(size_t)P_T]);
+                    o.MEL, total, d_.stream);
     SDSP_HIP_CHECK(hipGetLastError());
     // novelty
     NovParams np{};
