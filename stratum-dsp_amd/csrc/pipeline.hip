@@ -1249,7 +1249,14 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     kt.init(d_);
     // SDSP_SERIAL_STREAMS=1 keeps the key path on the main stream (per-kernel profiling)
     static const bool serial_streams = std::getenv("SDSP_SERIAL_STREAMS") != nullptr;
+    // SDSP_KEY_STFT_FIRST=1 (schedule experiment): the 8192-point STFT on the main stream ahead
+    // of the tempo path, so only the HBM-bound mask / HPCP / vote kernels share the chip with the
+    // tempo kernels.  Measured slower (606 vs 558 ms per 1024-track step, tools/bench_ab.sh): the
+    // tempo path's latency-bound chains overlap the STFT's VALU work better than the mask's
+    // long-lived waves, so by default the STFT runs on the key stream beside the tempo path.
+    static const bool key_stft_first = std::getenv("SDSP_KEY_STFT_FIRST") != nullptr;
     hipStream_t st2 = serial_streams ? st : d_.stream2;
+    hipStream_t sk = key_stft_first ? st : st2;
     float* d_tune = nullptr;  // per key track tuning offset (tuning compensation)
     float* mags8 = nullptr;
     uint64_t* d_kpfx = nullptr;
@@ -1276,12 +1283,13 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         // uploads above were queued on the main stream: order the key stream after them
         kt.mark(7);
         SDSP_HIP_CHECK(hipStreamWaitEvent(st2, kt.ev[7], 0));
-        kt.mark(0, st2);
+        kt.mark(0, sk);
         launch_stft(KFS, false, d_samples, d_kpfx, NK, total8, d_ksrc, d_kgain, KHOP, t8.window.as<float>(), t8.stft_tw.as<cx>(),
-                    t8.stft_rt.as<cx>(), mags8, d_kpfx, STRIDE8, nullptr, st2, d_kstr, kstr.back(),
+                    t8.stft_rt.as<cx>(), mags8, d_kpfx, STRIDE8, nullptr, sk, d_kstr, kstr.back(),
                     c_.dev<uint32_t>("E.redo", total8 + 1));
         SDSP_HIP_CHECK(hipGetLastError());
-        kt.mark(1, st2);
+        kt.mark(1, sk);
+        if (sk != st2) SDSP_HIP_CHECK(hipStreamWaitEvent(st2, kt.ev[1], 0));
         // key spectrogram conditioning (src/lib.rs:1011-1060)
         if (cfg_.enable_key_hpss_harmonic) {
             const KeyHpssParams kh = key_hpss_params(cfg_, sr_, B8, fres8);

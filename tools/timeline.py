@@ -5,7 +5,8 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 iv = sorted((int(r['Start_Timestamp']), int(r['End_Timestamp']), r['Kernel_Name'][:40]) for r in rows)
 t00 = iv[0][0]
 if len(sys.argv) > 2:
-    iv = [x for x in iv if x[0] - t00 >= float(sys.argv[2]) * 1e6]
+    skip = [x for x in iv if x[0] - t00 >= float(sys.argv[2]) * 1e6]
+    iv = skip if skip else iv
 t0 = iv[0][0]; t1 = max(e for _, e, _ in iv)
 busy = 0; cur_s, cur_e = iv[0][0], iv[0][1]; gaps = []
 for s, e, n in iv[1:]:
