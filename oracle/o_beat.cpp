@@ -147,37 +147,57 @@ static std::vector<Seg> tempo_variations(const std::vector<float>& b, float nomi
 // bayesian.rs:104-272 (tracker state carried across segments)
 struct Bayes {
     float bpm, conf;
+    std::vector<float> history;  // BayesianBeatTracker::history (new(): [initial])
 };
+static Bayes bayes_new(float bpm, float conf) { return {bpm, sd_clampf(conf, 0.0f, 1.0f), {bpm}}; }  // :77-83
+// generate_bpm_candidates (:183-199): f32 0.5-BPM steps over [max(bpm-5, 60), min(bpm+5, 180)]
+static std::vector<float> bayes_candidates(const Bayes& st) {
+    std::vector<float> c;
+    const float lo = sd_maxf(st.bpm - 5.0f, 60.0f), hi = sd_minf(st.bpm + 5.0f, 180.0f);
+    for (float b = lo; b <= hi; b += 0.5f) c.push_back(b);
+    return c;
+}
+// compute_likelihood (:201-252): exp of the mean Gaussian log-likelihood (sigma 0.05 s) of the
+// onsets' distances to the nearest grid beat anchored at the first onset
+static float bayes_likelihood(const std::vector<float>& on, float cb) {
+    if (cb <= EPS) fail(SDSP_ERR_INVALID_INPUT, "Invalid BPM for likelihood");
+    if (on.empty()) return 0.0f;
+    const float bi = 60.0f / cb;
+    const float st0 = on[0];
+    float ll = 0.0f;
+    int32_t valid = 0;
+    const float sig_sq = 0.05f * 0.05f;
+    for (float o : on) {
+        const int32_t idx = sd_f2i32(sd_roundf((o - st0) / bi));
+        const float exp_t = st0 + ((float)idx * bi);
+        const float d = sd_absf(o - exp_t);
+        const float dsq = d * d;
+        ll += -dsq / (2.0f * sig_sq);
+        valid++;
+    }
+    return valid == 0 ? 0.0f : sd_expf(ll / (float)valid);
+}
+// compute_prior (:254-265): Gaussian in the BPM change, sigma 2 BPM
+static float bayes_prior(const Bayes& st, float bpm) {
+    const float d = sd_absf(bpm - st.bpm);
+    const float sig_sq = 2.0f * 2.0f;
+    return sd_expf(-(d * d) / (2.0f * sig_sq));
+}
 static void bayes_update(Bayes& st, const std::vector<float>& on, float* out_bpm) {
     if (on.empty()) fail(SDSP_ERR_INVALID_INPUT, "Cannot update: no onsets provided");
     if (st.bpm <= EPS || st.bpm > 300.0f) fail(SDSP_ERR_INVALID_INPUT, "Invalid current BPM");
-    std::vector<float> cands;
-    const float lo = sd_maxf(st.bpm - 5.0f, 60.0f), hi = sd_minf(st.bpm + 5.0f, 180.0f);
-    for (float b = lo; b <= hi; b += 0.5f) cands.push_back(b);
     float best_bpm = st.bpm, best_l = 0.0f;
-    for (float cb : cands) {
-        if (cb <= EPS) fail(SDSP_ERR_INVALID_INPUT, "Invalid BPM for likelihood");
-        const float bi = 60.0f / cb;
-        const float st0 = on[0];
-        float ll = 0.0f;
-        int32_t valid = 0;
-        const float sig_sq = 0.05f * 0.05f;
-        for (float o : on) {
-            const int32_t idx = sd_f2i32(sd_roundf((o - st0) / bi));
-            const float exp_t = st0 + ((float)idx * bi);
-            const float d = sd_absf(o - exp_t);
-            const float dsq = d * d;
-            ll += -dsq / (2.0f * sig_sq);
-            valid++;
-        }
-        const float lik = valid == 0 ? 0.0f : sd_expf(ll / (float)valid);
+    for (float cb : bayes_candidates(st)) {
+        const float lik = bayes_likelihood(on, cb);
         if (lik > best_l) {
             best_l = lik;
             best_bpm = cb;
         }
     }
+    (void)bayes_prior(st, best_bpm);  // the posterior (:140-141) is computed and unused
     const float old = st.bpm;
     st.bpm = best_bpm;
+    st.history.push_back(best_bpm);
     const float ch = sd_absf(best_bpm - old);
     const float pen = ch < 1.0f ? 1.0f : ch < 3.0f ? 0.8f : 0.5f;
     st.conf = sd_minf(best_l * pen, 1.0f);
@@ -208,8 +228,11 @@ static float score_ts(const std::vector<float>& iv, uint32_t bpb, float mean) {
     return sd_minf(ac * 0.7f + cons * 0.3f, 1.0f);
 }
 
-// time_signature.rs:90-149 -> beats per bar
-static uint32_t time_signature(const std::vector<float>& b, float bpm) {
+// time_signature.rs:90-149 -> beats per bar (+ confidence = the best score clamped to [0, 1])
+static uint32_t time_signature(const std::vector<float>& b, float bpm, float* conf = nullptr) {
+    float dummy;
+    if (!conf) conf = &dummy;
+    *conf = 0.5f;
     if (b.size() < 8) return 4;
     if (bpm <= EPS) fail(SDSP_ERR_INVALID_INPUT, "Invalid BPM for time signature detection");
     std::vector<float> iv;
@@ -233,6 +256,7 @@ static uint32_t time_signature(const std::vector<float>& b, float bpm) {
         best = 6;
         bs = s68;
     }
+    *conf = sd_clampf(bs, 0.0f, 1.0f);
     return best;
 }
 
@@ -255,7 +279,7 @@ bool generate_beat_grid(float bpm, float conf, const std::vector<float>& onsets_
         for (auto& s : segs) var |= s.variable;
         if (var) {
             std::vector<BeatPos> refined;
-            Bayes st{bpm, sd_clampf(conf, 0.0f, 1.0f)};
+            Bayes st = bayes_new(bpm, conf);
             for (auto& s : segs) {
                 if (s.variable) {
                     std::vector<float> so;
@@ -347,3 +371,115 @@ extern "C" int32_t sdsp_oracle_hmm_track(float bpm, const float* on, int32_t n, 
     return m;
 }
 
+
+// ---- unit probes (tests only; tests/test_oracle_units_beat.py) ----
+using namespace orc;
+
+extern "C" {
+
+// generate_beat_grid (mod.rs:108-247): the reference returns Err for bpm <= 0 or > 300, empty
+// onsets and a failed HMM; the oracle maps every such case to "no grid" (-1 here).
+// counts = (beats, downbeats); bars == downbeats (mod.rs:316)
+int32_t sdsp_oracle_beat_grid(float bpm, float conf, const float* on, uint64_t n, uint32_t sr, float* beats,
+                              float* downs, uint64_t cap, uint64_t* counts, float* stability) {
+    std::vector<float> o(on, on + n), b, d;
+    float st = 0.0f;
+    if (!generate_beat_grid(bpm, conf, o, sr, &b, &d, &st)) return -1;
+    for (size_t i = 0; i < b.size() && i < cap; i++) beats[i] = b[i];
+    for (size_t i = 0; i < d.size() && i < cap; i++) downs[i] = d[i];
+    counts[0] = b.size();
+    counts[1] = d.size();
+    *stability = st;
+    return 0;
+}
+
+// detect_downbeats_with_time_sig (mod.rs:363-404)
+int64_t sdsp_oracle_downbeats(const float* beats, uint64_t n, float bpm, uint32_t beats_per_bar, float* out) {
+    return probe_call([&]() -> int64_t {
+        if (n == 0) return 0;
+        if (bpm <= 0.0f) fail(SDSP_ERR_INVALID_INPUT, "Invalid BPM for downbeat detection");
+        const float bar = (60.0f / bpm) * (float)beats_per_bar;
+        const float tol = bar * 0.1f;
+        int64_t k = 0;
+        out[k++] = beats[0];
+        for (uint64_t i = 1; i < n; i++)
+            if (sd_absf(beats[i] - (out[k - 1] + bar)) <= tol) out[k++] = beats[i];
+        return k;
+    });
+}
+
+// calculate_grid_stability (mod.rs:425-485) over beat times
+int32_t sdsp_oracle_grid_stability(const float* t, uint64_t n, float bpm, float* out) {
+    return (int32_t)probe_call([&]() -> int64_t {
+        *out = 0.0f;
+        if (n < 2) return 0;
+        if (bpm <= 0.0f) fail(SDSP_ERR_INVALID_INPUT, "Invalid BPM for stability calculation");
+        std::vector<float> iv;
+        for (uint64_t i = 1; i < n; i++)
+            if (t[i] - t[i - 1] > 0.0f) iv.push_back(t[i] - t[i - 1]);
+        if (iv.empty()) return 0;
+        float sum = 0.0f;
+        for (float x : iv) sum += x;
+        const float mean = sum / (float)iv.size();
+        if (mean <= 1e-10f) return 0;
+        float vs = 0.0f;
+        for (float x : iv) vs += (x - mean) * (x - mean);
+        *out = 1.0f / (1.0f + __builtin_sqrtf(vs / (float)iv.size()) / mean);
+        return 0;
+    });
+}
+
+// detect_tempo_variations (tempo_variation.rs:95-227): 5 floats per segment
+// (start, end, bpm, confidence, is_variable); returns the segment count
+int64_t sdsp_oracle_tempo_variations(const float* beats, uint64_t n, float nominal, float* out, uint64_t cap) {
+    return probe_call([&]() -> int64_t {
+        const auto segs = tempo_variations(std::vector<float>(beats, beats + n), nominal);
+        for (size_t i = 0; i < segs.size() && i < cap; i++) {
+            const float v[5] = {segs[i].start, segs[i].end, segs[i].bpm, segs[i].conf, segs[i].variable ? 1.0f : 0.0f};
+            std::memcpy(out + 5 * i, v, sizeof v);
+        }
+        return (int64_t)segs.size();
+    });
+}
+
+// BayesianBeatTracker (bayesian.rs:77-272) created with (bpm, conf):
+//   op 0: generate_bpm_candidates -> out (returns the count)
+//   op 1: compute_likelihood(onsets, x) -> out[0]
+//   op 2: compute_prior(x) -> out[0]
+//   op 3: new() state -> out = (current_bpm, current_confidence, history...)
+//   op 4: update_with_onsets(onsets) -> out = (current_bpm, current_confidence, history...)
+// ops 3-4 return the history length
+int64_t sdsp_oracle_bayes(int32_t op, float bpm, float conf, const float* on, uint64_t n, float x, float* out,
+                          uint64_t cap) {
+    return probe_call([&]() -> int64_t {
+        Bayes st = bayes_new(bpm, conf);
+        const std::vector<float> o(on, on + n);
+        switch (op) {
+            case 0: {
+                const auto c = bayes_candidates(st);
+                for (size_t i = 0; i < c.size() && i < cap; i++) out[i] = c[i];
+                return (int64_t)c.size();
+            }
+            case 1: out[0] = bayes_likelihood(o, x); return 0;
+            case 2: out[0] = bayes_prior(st, x); return 0;
+            default: break;
+        }
+        if (op == 4) {
+            float ub;
+            bayes_update(st, o, &ub);
+        }
+        out[0] = st.bpm;
+        out[1] = st.conf;
+        for (size_t i = 0; i < st.history.size() && i + 2 < cap; i++) out[2 + i] = st.history[i];
+        return (int64_t)st.history.size();
+    });
+}
+
+// detect_time_signature (time_signature.rs:90-149): beats per bar (4 / 3 / 6) and confidence
+int32_t sdsp_oracle_time_signature(const float* beats, uint64_t n, float bpm, uint32_t* bpb, float* conf) {
+    return (int32_t)probe_call([&]() -> int64_t {
+        *bpb = time_signature(std::vector<float>(beats, beats + n), bpm, conf);
+        return 0;
+    });
+}
+}

@@ -487,3 +487,66 @@ float key_clarity(const float* s, int n) {
 }
 
 }  // namespace orc
+
+// ---- unit probes (tests only; tests/test_oracle_units_key.py) ----
+using namespace orc;
+
+extern "C" {
+
+// detect_key_weighted (detector.rs:68-313) with K-K templates (KeyTemplates::new()); weights
+// nullable (detect_key).  dims = the chroma vectors' length (the reference rejects != 12);
+// n_weights = the weight slice length (rejected when != frames).  Outputs: key index
+// (mode * 12 + tonic), confidence, the 24 refined scores in sorted order and their key indices
+// (all_scores; top_keys = the first 3).
+int32_t sdsp_oracle_detect_key(const float* chroma, uint64_t frames, uint64_t dims, const float* weights,
+                               uint64_t n_weights, int32_t* key, float* conf, float* scores24, int32_t* keys24) {
+    return (int32_t)probe_call([&]() -> int64_t {
+        if (frames == 0) fail(SDSP_ERR_INVALID_INPUT, "Empty chroma vectors");
+        if (dims != 12) fail(SDSP_ERR_INVALID_INPUT, "Chroma vectors must have 12 elements");
+        if (weights && n_weights != frames) fail(SDSP_ERR_INVALID_INPUT, "frame_weights length mismatch");
+        float maj[12][12], mnr[12][12];
+        key_templates(maj, mnr, 0);
+        const KeyResult r = detect_key_weighted(chroma, frames, weights, maj, mnr);
+        *key = r.mode * 12 + (int32_t)r.tonic;
+        *conf = r.confidence;
+        for (int i = 0; i < 24; i++) {
+            scores24[i] = r.scores[i];
+            keys24[i] = r.order[i];
+        }
+        return 0;
+    });
+}
+
+// smooth_chroma (smoothing.rs:37-94, median) or smooth_chroma_average (:103-150): frames x 12
+void sdsp_oracle_smooth_chroma(const float* ch, uint64_t frames, uint64_t window, int32_t average, float* out) {
+    std::vector<float> v(ch, ch + frames * 12);
+    if (!average) {
+        smooth_chroma_inplace(v, (size_t)frames, (size_t)window);
+    } else if (frames > 0 && window > 1) {
+        const int64_t half = (int64_t)window / 2;
+        std::vector<float> o(v.size());
+        for (int64_t t = 0; t < (int64_t)frames; t++)
+            for (int s = 0; s < 12; s++) {
+                float sum = 0.0f;
+                int cnt = 0;
+                for (int64_t k = 0; k < (int64_t)window; k++) {
+                    const int64_t fi = t + (k - half);
+                    if (fi >= 0 && fi < (int64_t)frames) {
+                        sum += v[(size_t)fi * 12 + (size_t)s];
+                        cnt++;
+                    }
+                }
+                o[(size_t)t * 12 + (size_t)s] = cnt > 0 ? sum / (float)cnt : v[(size_t)t * 12 + (size_t)s];
+            }
+        v.swap(o);
+    }
+    std::memcpy(out, v.data(), v.size() * sizeof(float));
+}
+
+// dot_product (detector.rs:979-981): sequential f32 sum of products
+float sdsp_oracle_dot(const float* a, const float* b, uint64_t n) {
+    float acc = 0.0f;
+    for (uint64_t i = 0; i < n; i++) acc += a[i] * b[i];
+    return acc;
+}
+}

@@ -93,8 +93,10 @@ void normalize_lufs(std::vector<float>& x, uint32_t sr, float target_lufs, float
 
 // src/preprocessing/silence.rs:102-279
 void detect_and_trim(const std::vector<float>& x, uint32_t sr, float threshold_db, uint32_t min_ms,
-                     size_t frame_size, size_t* trim_start, size_t* trim_end) {
+                     size_t frame_size, size_t* trim_start, size_t* trim_end,
+                     std::vector<std::pair<size_t, size_t>>* silence_map) {
     const size_t n = x.size();
+    if (silence_map) silence_map->clear();
     if (n == 0) {
         *trim_start = *trim_end = 0;
         return;
@@ -139,6 +141,8 @@ void detect_and_trim(const std::vector<float>& x, uint32_t sr, float threshold_d
     if (in_sil) {
         if (num_frames - sil_start >= min_frames || sil_start == 0) regions.push_back({starts[sil_start], n});
     }
+    if (silence_map)
+        for (auto& r : regions) silence_map->push_back({r.s, r.e});
     size_t ts = 0, te = n;
     if (!regions.empty() && regions.front().s == 0) ts = regions.front().e;
     if (!regions.empty() && regions.back().e == n) te = regions.back().s;
@@ -435,4 +439,78 @@ extern "C" int64_t sdsp_oracle_hpss_onsets(const float* p, uint64_t frames, uint
     }
     for (size_t i = 0; i < on.size() && i < cap; i++) out[i] = (uint64_t)on[i];
     return (int64_t)on.size();
+}
+
+// ---- unit probes (tests only; tests/test_oracle_units_onset.py) ----
+namespace orc {
+std::string g_probe_err;
+
+void spec_from_rows(const float* d, size_t frames, size_t bins, const uint64_t* row_lens, Spec* out) {
+    if (row_lens)
+        for (size_t t = 0; t < frames; t++)
+            if (row_lens[t] != row_lens[0])
+                fail(SDSP_ERR_INVALID_INPUT, "Inconsistent frame lengths: frame 0 has " + std::to_string(row_lens[0]) +
+                                                 " bins, frame " + std::to_string(t) + " has " +
+                                                 std::to_string(row_lens[t]) + " bins");
+    out->frames = frames;
+    out->bins = frames ? bins : 0;
+    out->d.assign(d, d + frames * bins);
+}
+}  // namespace orc
+
+using namespace orc;
+
+template <class V>
+static int64_t put_list(const V& v, uint64_t* out, uint64_t cap) {
+    for (size_t i = 0; i < v.size() && i < cap; i++) out[i] = (uint64_t)v[i];
+    return (int64_t)v.size();
+}
+
+extern "C" {
+const char* sdsp_oracle_probe_error(void) { return g_probe_err.c_str(); }
+
+// detect_energy_flux_onsets (energy_flux.rs:67-243) -> onset sample positions
+int64_t sdsp_oracle_energy_flux_onsets(const float* s, uint64_t n, uint64_t frame, uint64_t hop, float thr_db,
+                                       uint64_t* out, uint64_t cap) {
+    return probe_call([&]() -> int64_t { return put_list(energy_flux_onsets(s, n, frame, hop, thr_db), out, cap); });
+}
+
+// detect_spectral_flux_onsets (spectral_flux.rs:69-221) -> onset frame indices
+int64_t sdsp_oracle_spectral_flux_onsets(const float* spec, uint64_t frames, uint64_t bins, const uint64_t* row_lens,
+                                         float pct, uint64_t* out, uint64_t cap) {
+    return probe_call([&]() -> int64_t {
+        Spec m;
+        spec_from_rows(spec, frames, bins, row_lens, &m);
+        return put_list(spectral_flux_onsets(m, pct), out, cap);
+    });
+}
+
+// detect_hfc_onsets (hfc.rs:76-214) -> onset frame indices
+int64_t sdsp_oracle_hfc_onsets(const float* spec, uint64_t frames, uint64_t bins, const uint64_t* row_lens,
+                               uint32_t sr, float pct, uint64_t* out, uint64_t cap) {
+    return probe_call([&]() -> int64_t {
+        Spec m;
+        spec_from_rows(spec, frames, bins, row_lens, &m);
+        return put_list(hfc_onsets(m, sr, pct), out, cap);
+    });
+}
+
+// detect_and_trim (silence.rs:102-279): trim = [start, end) of the kept samples; regions =
+// the silence map as (start, end) sample pairs; returns the region count
+int64_t sdsp_oracle_detect_and_trim(const float* x, uint64_t n, uint32_t sr, float thr_db, uint32_t min_ms,
+                                    uint64_t frame, uint64_t* trim, uint64_t* regions, uint64_t cap) {
+    return probe_call([&]() -> int64_t {
+        std::vector<float> v(x, x + n);
+        std::vector<std::pair<size_t, size_t>> map;
+        size_t ts = 0, te = 0;
+        detect_and_trim(v, sr, thr_db, min_ms, (size_t)frame, &ts, &te, &map);
+        trim[0] = ts;
+        trim[1] = te;
+        for (size_t i = 0; i < map.size() && i < cap; i++) {
+            regions[2 * i] = map[i].first;
+            regions[2 * i + 1] = map[i].second;
+        }
+        return (int64_t)map.size();
+    });
+}
 }

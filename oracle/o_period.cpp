@@ -1097,3 +1097,176 @@ extern "C" int64_t sdsp_oracle_legacy(int32_t which, const uint64_t* on, uint64_
     }
     return (int64_t)est.size();
 }
+
+// =====================================================================================
+// Unit probes (tests only; tests/test_oracle_units_tempo.py): the reference functions at the
+// granularity of its own unit tests, built from the restatement above.
+// =====================================================================================
+namespace orc {
+
+static void check_bins(const Spec& m) {  // validate_spectrogram (novelty.rs:39-60); raggedness: spec_from_rows
+    if (m.frames >= 2 && m.bins == 0) fail(SDSP_ERR_INVALID_INPUT, "Empty magnitude frames");
+}
+
+std::vector<float> superflux_novelty(const Spec& m, size_t k) {
+    if (m.frames < 2) return {};
+    check_bins(m);
+    if (m.bins == 0) return {};
+    NovFrames lf = log_frames(m);
+    return superflux(lf.logf_, m.frames, m.bins, k, 0, m.bins);
+}
+
+std::vector<float> energy_flux_novelty(const Spec& m) {
+    if (m.frames < 2) return {};
+    check_bins(m);
+    return scalar_flux_norm(frame_energy(m, 0, m.bins));
+}
+
+std::vector<float> hfc_novelty(const Spec& m, uint32_t sr) {
+    if (m.frames == 0) return {};
+    if (sr == 0) fail(SDSP_ERR_INVALID_INPUT, "Sample rate must be > 0");
+    if (m.frames < 2) return {};
+    check_bins(m);
+    return scalar_flux_norm(frame_hfc(m, 0, m.bins));
+}
+
+// per-frame max-normalised half-wave L2 flux, normalised by its max (novelty.rs:222-334)
+std::vector<float> spectral_flux_novelty(const Spec& m) {
+    if (m.frames < 2) return {};
+    check_bins(m);
+    const size_t B = m.bins;
+    std::vector<float> norm(m.d.size(), 0.0f);
+    for (size_t t = 0; t < m.frames; t++) {
+        const float* r = m.row(t);
+        float mx = 0.0f;
+        for (size_t b = 0; b < B; b++) mx = sd_maxf(mx, r[b]);
+        if (mx > EPS)
+            for (size_t b = 0; b < B; b++) norm[t * B + b] = r[b] / mx;
+    }
+    std::vector<float> flux;
+    for (size_t t = 1; t < m.frames; t++) {
+        float sum = 0.0f;
+        for (size_t b = 0; b < B; b++) {
+            const float d = sd_maxf(norm[t * B + b] - norm[(t - 1) * B + b], 0.0f);
+            sum += d * d;
+        }
+        flux.push_back(__builtin_sqrtf(sum));
+    }
+    normalize_in_place(flux);
+    return flux;
+}
+
+std::vector<float> combined_novelty_params(const std::vector<float>& s, const std::vector<float>& e,
+                                           const std::vector<float>& h, float ws, float we, float wh, size_t lmw,
+                                           size_t smw) {
+    return combine(s, e, h, ws, we, wh, lmw, smw);
+}
+
+}  // namespace orc
+
+using namespace orc;
+
+extern "C" {
+
+static int64_t put_curve(const std::vector<float>& v, float* out) {
+    if (out) std::memcpy(out, v.data(), v.size() * sizeof(float));
+    return (int64_t)v.size();
+}
+
+// kind 0 spectral_flux_novelty, 1 energy_flux_novelty, 2 hfc_novelty, 3 superflux_novelty(k);
+// out holds frames - 1 values; returns the curve length
+int64_t sdsp_oracle_novelty(int32_t kind, const float* spec, uint64_t frames, uint64_t bins, const uint64_t* row_lens,
+                            uint32_t sr, uint64_t k, float* out) {
+    return probe_call([&]() -> int64_t {
+        Spec m;
+        spec_from_rows(spec, frames, bins, row_lens, &m);
+        switch (kind) {
+            case 0: return put_curve(spectral_flux_novelty(m), out);
+            case 1: return put_curve(energy_flux_novelty(m), out);
+            case 2: return put_curve(hfc_novelty(m, sr), out);
+            default: return put_curve(superflux_novelty(m, (size_t)k), out);
+        }
+    });
+}
+
+// combined_novelty_with_params (novelty.rs:874-932); combined_novelty = (.5, .3, .2, 16, 5)
+int64_t sdsp_oracle_combined_novelty(const float* s, uint64_t ns, const float* e, uint64_t ne, const float* h,
+                                     uint64_t nh, float ws, float we, float wh, uint64_t lmw, uint64_t smw, float* out) {
+    return probe_call([&]() -> int64_t {
+        return put_curve(combined_novelty_params(std::vector<float>(s, s + ns), std::vector<float>(e, e + ne),
+                                                 std::vector<float>(h, h + nh), ws, we, wh, (size_t)lmw, (size_t)smw),
+                         out);
+    });
+}
+
+// kind 0 fft_tempogram (tempogram_fft.rs:78-192), 1 autocorrelation_tempogram
+// (tempogram_autocorr.rs:79-178): (bpm, value) pairs sorted by value, stable; returns the count
+int64_t sdsp_oracle_tempogram(int32_t kind, const float* nov, uint64_t n, uint32_t sr, uint32_t hop, float min_bpm,
+                              float max_bpm, float res, float* bpm, float* val, uint64_t cap) {
+    return probe_call([&]() -> int64_t {
+        const std::vector<float> v(nov, nov + n);
+        const Tg tg = kind == 0 ? fft_tempogram(v, sr, hop, min_bpm, max_bpm) : acf_tempogram(v, sr, hop, min_bpm, max_bpm, res);
+        for (size_t i = 0; i < tg.size() && i < cap; i++) {
+            bpm[i] = tg[i].first;
+            val[i] = tg[i].second;
+        }
+        return (int64_t)tg.size();
+    });
+}
+
+// estimate_bpm_tempogram (tempogram.rs:155-174, no band fusion): out = (bpm, confidence, agreement)
+int32_t sdsp_oracle_tempogram_estimate(const float* spec, uint64_t frames, uint64_t bins, uint32_t sr, uint32_t hop,
+                                       float min_bpm, float max_bpm, float res, float* out3) {
+    return (int32_t)probe_call([&]() -> int64_t {
+        Spec m;
+        spec_from_rows(spec, frames, bins, nullptr, &m);
+        BpmEstimate e{};
+        tempogram_impl(m, sr, hop, min_bpm, max_bpm, res, nullptr, &e, nullptr);
+        out3[0] = e.bpm;
+        out3[1] = e.confidence;
+        out3[2] = (float)e.method_agreement;
+        return 0;
+    });
+}
+
+// multi_resolution_analysis (multi_resolution.rs:76-203): estimate_bpm_tempogram of the same
+// spectrogram at hops 256/512/1024; all within 2 BPM -> mean BPM, mean conf x1.2 (<= 1),
+// agreement = count; else the most confident (max_by: last maximum) with conf x0.9
+int32_t sdsp_oracle_multi_resolution_analysis(const float* spec, uint64_t frames, uint64_t bins, uint32_t sr,
+                                              float min_bpm, float max_bpm, float res, float* out3) {
+    return (int32_t)probe_call([&]() -> int64_t {
+        Spec m;
+        spec_from_rows(spec, frames, bins, nullptr, &m);
+        std::vector<BpmEstimate> rs;
+        for (uint32_t hop : {256u, 512u, 1024u}) {
+            try {
+                BpmEstimate e{};
+                tempogram_impl(m, sr, hop, min_bpm, max_bpm, res, nullptr, &e, nullptr);
+                rs.push_back(e);
+            } catch (const AErr&) {
+            }
+        }
+        if (rs.empty()) fail(SDSP_ERR_PROCESSING, "All multi-resolution tempogram analyses failed");
+        BpmEstimate r = rs[0];
+        if (rs.size() >= 2) {
+            bool agree = true;
+            for (auto& e : rs) agree &= sd_absf(e.bpm - rs[0].bpm) < 2.0f;
+            if (agree) {
+                float sb = 0.0f, sc = 0.0f;
+                for (auto& e : rs) sb += e.bpm;
+                for (auto& e : rs) sc += e.confidence;
+                r = {sb / (float)rs.size(), sd_minf((sc / (float)rs.size()) * 1.2f, 1.0f), (uint32_t)rs.size()};
+            } else {
+                size_t bi = 0;
+                for (size_t i = 1; i < rs.size(); i++)
+                    if (!(rs[i].confidence < rs[bi].confidence)) bi = i;
+                r = {rs[bi].bpm, rs[bi].confidence * 0.9f, 1};
+            }
+        }
+        out3[0] = r.bpm;
+        out3[1] = r.confidence;
+        out3[2] = (float)r.method_agreement;
+        return 0;
+    });
+}
+}

@@ -69,7 +69,8 @@ void normalize_peak(std::vector<float>& x, float headroom_db);
 void normalize_rms(std::vector<float>& x, float target_lufs, float headroom_db);
 void normalize_lufs(std::vector<float>& x, uint32_t sr, float target_lufs, float headroom_db);
 void detect_and_trim(const std::vector<float>& x, uint32_t sr, float threshold_db, uint32_t min_ms,
-                     size_t frame_size, size_t* trim_start, size_t* trim_end);
+                     size_t frame_size, size_t* trim_start, size_t* trim_end,
+                     std::vector<std::pair<size_t, size_t>>* silence_map = nullptr);
 std::vector<size_t> energy_flux_onsets(const float* s, size_t n, size_t frame, size_t hop, float thr_db);
 std::vector<size_t> spectral_flux_onsets(const Spec& m, float pct);
 std::vector<size_t> hfc_onsets(const Spec& m, uint32_t sr, float pct);
@@ -171,6 +172,31 @@ bool detect_key_multi_scale(const float* chroma, size_t frames, const float* wei
                             const float min[12][12], const std::vector<size_t>& lengths, size_t hop, float min_clarity,
                             const std::vector<float>* scale_weights, const ModeHeuristic& mh, KeyResult* out,
                             int* used_segments);
+
+// ---------- unit probes (o_*.cpp "unit probes" sections; tests/test_oracle_units_*.py) ----------
+// Entry points at the granularity of the reference's own unit tests.  A probe returns a count /
+// 0 on success or -(AnalysisError code) on error, with the message kept for
+// sdsp_oracle_probe_error().
+extern std::string g_probe_err;
+template <class F>
+int64_t probe_call(F f) {
+    try {
+        return f();
+    } catch (const AErr& e) {
+        g_probe_err = e.msg;
+        return -(int64_t)e.code;
+    }
+}
+// Vec<Vec<f32>> from a flat row-major buffer; row_lens (nullable) lets a test pass a ragged
+// spectrogram: the reference's validate loops reject frame lengths that differ from frame 0's
+void spec_from_rows(const float* d, size_t frames, size_t bins, const uint64_t* row_lens, Spec* out);
+std::vector<float> superflux_novelty(const Spec& m, size_t k);                    // novelty.rs:336-393
+std::vector<float> energy_flux_novelty(const Spec& m);                            // novelty.rs:477-545
+std::vector<float> hfc_novelty(const Spec& m, uint32_t sr);                       // novelty.rs:687-772
+std::vector<float> spectral_flux_novelty(const Spec& m);                          // novelty.rs:222-334
+std::vector<float> combined_novelty_params(const std::vector<float>& s, const std::vector<float>& e,
+                                           const std::vector<float>& h, float ws, float we, float wh,
+                                           size_t lmw, size_t smw);              // novelty.rs:874-932
 
 // ---------- trace (test probes) ----------
 struct Trace {
