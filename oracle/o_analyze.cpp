@@ -471,7 +471,7 @@ void analyze(const float* samples, size_t n, uint32_t sr, const sdsp_config& c, 
         for (size_t s : on_beat) os.push_back((float)s / (float)sr);
         std::vector<float> beats, down;
         float stab = 0.0f;
-        if (generate_beat_grid(bpm, bconf, os, sr, &beats, &down, &stab)) {
+        if (generate_beat_grid(bpm, bconf, os, sr, &beats, &down, &stab, &tr.beat)) {
             o.beats = beats;
             o.downbeats = down;
             o.stability = stab;
@@ -721,6 +721,16 @@ void set_trace(const Trace& t) {
           << t.base_cands[i].fft_norm << "," << t.base_cands[i].autocorr_norm << "]";
     s << "],";
     s << "\"weights_used\":" << t.weights_used << ",\"used_segments\":" << t.used_segments << ",";
+    s << "\"beat_variable\":" << t.beat.variable << ",\"beat_refined\":" << t.beat.refined
+      << ",\"beats_per_bar\":" << t.beat.beats_per_bar << ",";
+    // key-stage checksums (sums in double over the frame-major arrays)
+    double cs = 0, cq = 0, es = 0, ws = 0;
+    for (float v : t.chroma) cs += v, cq += (double)v * v;
+    for (float v : t.energies) es += v;
+    for (float v : t.weights) ws += v;
+    s.precision(17);
+    s << "\"chroma_sum\":" << cs << ",\"chroma_sq\":" << cq << ",\"energy_sum\":" << es << ",\"weights_sum\":" << ws
+      << ",";
     s << "\"n_key_frames\":" << t.energies.size();
     s << "}";
     g_trace_json = s.str();

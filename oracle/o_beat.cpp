@@ -262,8 +262,10 @@ static uint32_t time_signature(const std::vector<float>& b, float bpm, float* co
 
 // beat_tracking/mod.rs:108-247 (+ downbeats :363-404, stability :425-485)
 bool generate_beat_grid(float bpm, float conf, const std::vector<float>& onsets_s, uint32_t sr,
-                        std::vector<float>* beats_out, std::vector<float>* down_out, float* stab_out) {
+                        std::vector<float>* beats_out, std::vector<float>* down_out, float* stab_out,
+                        BeatDiag* diag) {
     (void)sr;
+    BeatDiag dg;
     try {
         if (bpm <= 0.0f || bpm > 300.0f) return false;
         if (onsets_s.empty()) return false;
@@ -277,6 +279,7 @@ bool generate_beat_grid(float bpm, float conf, const std::vector<float>& onsets_
         auto segs = tempo_variations(bt, bpm);
         bool var = false;
         for (auto& s : segs) var |= s.variable;
+        dg.variable = var;
         if (var) {
             std::vector<BeatPos> refined;
             Bayes st = bayes_new(bpm, conf);
@@ -299,11 +302,13 @@ bool generate_beat_grid(float bpm, float conf, const std::vector<float>& onsets_
             if (!refined.empty()) {
                 std::stable_sort(refined.begin(), refined.end(), [](auto& a, auto& b) { return a.t < b.t; });
                 pos.swap(refined);
+                dg.refined = true;
             }
         }
         bt.clear();
         for (auto& p : pos) bt.push_back(p.t);
         const uint32_t bpb = time_signature(bt, bpm);
+        dg.beats_per_bar = bpb;
         // generate_beat_grid_from_positions_with_time_sig (:290-320)
         std::vector<float> beats(bt);
         std::stable_sort(beats.begin(), beats.end(), [](float a, float b) { return a < b; });
@@ -345,6 +350,7 @@ bool generate_beat_grid(float bpm, float conf, const std::vector<float>& onsets_
         *beats_out = beats;
         *down_out = down;
         *stab_out = stab;
+        if (diag) *diag = dg;
         return true;
     } catch (const AErr&) {
         return false;  // src/lib.rs:932-943: any error -> empty grid, stability 0

@@ -113,8 +113,14 @@ void multi_resolution(const std::vector<float>& samples, uint32_t sr, size_t fra
                       const BandCfg* band, BpmEstimate* est, std::vector<TempoCand>* c512);
 
 // ---------- beat grid (beat_tracking/) ----------
+struct BeatDiag {            // which branches generate_beat_grid took (test probes)
+    bool variable = false;   // detect_tempo_variations flagged a variable segment (mod.rs:152-154)
+    bool refined = false;    // the Bayesian / per-segment HMM beats replaced the HMM beats (:205-219)
+    uint32_t beats_per_bar = 4;
+};
 bool generate_beat_grid(float bpm, float conf, const std::vector<float>& onsets_s, uint32_t sr,
-                        std::vector<float>* beats, std::vector<float>* downbeats, float* stability);
+                        std::vector<float>* beats, std::vector<float>* downbeats, float* stability,
+                        BeatDiag* diag = nullptr);
 
 // ---------- key (chroma/, key/) ----------
 void harmonic_mask_inplace(Spec& s, size_t margin, float power);
@@ -215,6 +221,7 @@ struct Trace {
     bool weights_used = false;
     float tuning = 0.0f;
     int used_segments = 0;
+    BeatDiag beat;
 };
 
 }  // namespace orc

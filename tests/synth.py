@@ -74,3 +74,31 @@ def make_track(seed, seconds=30.0, sr=44100, bpm=None, mode=None, tonic=None, si
         z = np.zeros(int(silence_pad * sr), np.float32)
         x = np.concatenate([z, x, z])
     return x, bpm, mode, tonic
+
+
+def chord_stab_track(bpm=72.0, seconds=20.0, hat_amp=0.04, stab_s=0.4, sr=44100, seed=0):
+    """Harmonic C-major stabs (e^-4t, stab_s long) on every beat and quiet 20-ms noise hats
+    (e^-150t) on every half beat.  The full mix's tempogram locks onto the stabs, so the base
+    estimate lands in the low trap zone [55, 80]; the percussive component carries the hats at
+    twice the rate.  At the defaults the percussive tempogram fallback (src/lib.rs:587-683) is
+    *accepted* (tempogram_percussive_used = true, BPM ~143.8): the input that exercises that
+    branch's "taken" outcome."""
+    rng = np.random.default_rng(seed)
+    n = int(sr * seconds)
+    t = np.arange(n) / sr
+    beat = 60.0 / bpm
+    env = np.zeros(n)
+    b = 0.0
+    while b < seconds:
+        i = int(b * sr)
+        e = min(n, i + int(stab_s * sr))
+        env[i:e] = np.maximum(env[i:e], np.exp(-np.arange(e - i) / sr * 4.0))
+        b += beat
+    x = env * sum(np.sin(2 * np.pi * f * t) for f in (261.63, 329.63, 392.0)) / 3
+    b, hl = 0.0, int(0.02 * sr)
+    while b < seconds:
+        i = int(b * sr)
+        e = min(n, i + hl)
+        x[i:e] += hat_amp * rng.standard_normal(e - i) * np.exp(-np.arange(e - i) / sr * 150)
+        b += beat / 2
+    return (x * 0.9 / np.abs(x).max()).astype(np.float32)

@@ -8,9 +8,9 @@
 
 Each case runs a ragged batch through the C ABI (GPU: k_hpss.hip) and compares every result field
 and the escalation flags with the oracle (oracle/o_onset.cpp, o_analyze.cpp) on the same inputs:
-bit-exact. The oracle's HPSS is pinned by tests/test_oracle_hpss.py.  None of these inputs makes
-the acceptance rule take the percussive estimate (tempogram_percussive_used stays false), so that
-rule is compared through its "not taken" outcome only.
+bit-exact. The oracle's HPSS is pinned by tests/test_oracle_hpss.py.  Both outcomes of the
+acceptance rule are exercised: the crafted chord-stab track (synth.chord_stab_track) makes it take
+the percussive estimate (tempogram_percussive_used = true), the other trap-zone tracks do not.
 """
 import os
 
@@ -59,6 +59,7 @@ def tracks():
         xs.append(_kick_track(58.0, 12.0, 0.3))
         xs.append(_kick_track(70.0, 10.0, 0.1))
         xs.append(synth.make_track(9, seconds=8.0, bpm=78.0)[0])
+        xs.append(synth.chord_stab_track())  # the percussive estimate is accepted (see synth.py)
         xs.append(parity.load_wav(os.path.join(GOLDEN, "120bpm_4bar.wav"))[0])
         rng = np.random.default_rng(3)
         xs.append((rng.standard_normal(2048) * 0.3).astype(np.float32))
@@ -111,6 +112,9 @@ def test_hpss_branches_live():
     got = sdsp.analyze_batch(xs, 44100, _apply(sdsp.default_config(), CASES["perc_fallback"]))
     trig = sum(1 for g in got if isinstance(g, dict) and g["metadata"]["tempogram_percussive_triggered"] is True)
     assert trig >= 2, trig
+    # the acceptance rule's "taken" outcome (src/lib.rs:640-668) on the crafted chord-stab track
+    used = [g for g in got if isinstance(g, dict) and g["metadata"]["tempogram_percussive_used"] is True]
+    assert len(used) >= 1 and 140.0 < used[0]["bpm"] < 148.0, [g["bpm"] for g in used]
     base = sdsp.analyze_batch(xs, 44100, sdsp.default_config())
     on = sdsp.analyze_batch(xs, 44100, _apply(sdsp.default_config(), CASES["hpss_onsets"]))
     diff = 0

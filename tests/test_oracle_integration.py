@@ -8,6 +8,7 @@
   is held to.
 """
 import json
+import sys
 import os
 
 import numpy as np
@@ -93,10 +94,29 @@ def test_golden_fixture_results(name):
     _same(r, _golden()["fixtures"][name])
 
 
-@pytest.mark.parametrize("key", ["0:30", "1:30", "2:45", "3:20"])
+SYNTH_KEYS = [f"{s}:{(30, 30, 45, 20)[s] if s < 4 else (20, 30, 45)[s % 3]}" for s in range(16)]
+
+
+@pytest.mark.parametrize("key", SYNTH_KEYS)
 def test_golden_synthetic_results(key):
     seed, sec = key.split(":")
     x, *_ = synth.make_track(int(seed), seconds=float(sec))
     st, r = oracle.analyze(x, 44100)
     assert st == 0
     _same(r, _golden()["synthetic"][key])
+
+
+@pytest.mark.parametrize("key", FIX + SYNTH_KEYS)
+def test_golden_stage_checksums(key):
+    """Per-stage checksums (trim, onset lists, novelty, base tempogram and candidates, escalation,
+    beat-grid branches, key arrays) stay identical: the oracle cannot drift stage by stage."""
+    sys.path.insert(0, GOLDEN)
+    import make_golden
+
+    if key in FIX:
+        x, sr = parity.load_wav(os.path.join(GOLDEN, key))
+    else:
+        seed, sec = key.split(":")
+        x, sr = synth.make_track(int(seed), seconds=float(sec))[0], 44100
+    got = json.loads(json.dumps(make_golden.stages(x, sr)))
+    assert got == _golden()["stages"][key]
