@@ -226,7 +226,7 @@ def main():
     total_tracks = n * world * args.steps
     value = total_tracks / dt
     stages = eng.stage_times()
-    # roofline of the dominant STFT kernel: k_stft_mag<8192> (the key STFT), or k_stft_mag<2048>
+    # roofline of the dominant STFT kernel: k_stft_slide<8192> (the key STFT), or k_stft_slide<2048>
     # when the key path does not run (bpm-only).  Algorithmic bytes per launch (4*N_in +
     # 4*F*(nfft/2+1)) / average launch time (HIP events on the kernel's stream).
     key_k = stft["l8"] > 0
@@ -246,7 +246,7 @@ def main():
             traffic = round(ratio * bytes_per_launch)
     roofline = {
         "bound": "hbm",
-        "kernel": "k_stft_mag<8192> (key STFT, 8192/512)" if key_k else "k_stft_mag<2048> (tempo STFT, 2048/512)",
+        "kernel": "k_stft_slide<8192> (key STFT, 8192/512)" if key_k else "k_stft_slide<2048> (tempo STFT, 2048/512)",
         "achieved": round(achieved, 2),
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
@@ -254,6 +254,7 @@ def main():
         "traffic": traffic,
         "bytes_per_launch": bytes_per_launch,
         "ms_per_launch": ms_per_launch,
+        "launches": stft["l" + tag],
         "stft2048_GBps": round(stft["b2"] / (stft["ms2"] * 1e-3) / 1e9, 2) if stft["ms2"] > 0 else None,
         "stft_stage_GBps": round((stft["b2"] + stft["b8"]) / ((stft["ms2"] + stft["ms8"]) * 1e-3) / 1e9, 2)
         if (stft["ms2"] + stft["ms8"]) > 0 else None,
