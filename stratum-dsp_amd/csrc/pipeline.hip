@@ -675,10 +675,11 @@ void Pipeline::run(const float* d_samples, const std::vector<uint64_t>& in_off, 
     // short last sub-batch runs at a fraction of the chip)
     std::vector<double> need(T, 0.0);
     double total_need = 0;
+    const double ckpt_f = std::getenv("SDSP_KEY_FUSE") ? 1.0 + 1.0 / KEY_CKPT_SEG : 1.0;  // + prefix checkpoints
     for (size_t i = 0; i < T; i++) {
         if (res[i].status != SDSP_OK) continue;
         const double n = (double)n_raw[i];
-        need[i] = n / hop * (STRIDE2 * 4.0 * 1.3 + 4 * 70.0) + (bpm_only_ ? 0.0 : n / khop * STRIDE8 * 4.0) +
+        need[i] = n / hop * (STRIDE2 * 4.0 * 1.3 + 4 * 70.0) + (bpm_only_ ? 0.0 : n / khop * STRIDE8 * 4.0 * ckpt_f) +
                   (n / 256 + n / 1024) * STRIDE2 * 4.0 + 1e6;
         if (cfg_.enable_hpss_onsets || cfg_.enable_tempogram_percussive_fallback)  // H, P ping-pong + a copy
             need[i] += n / hop * STRIDE2 * 4.0 * 5.0;
@@ -1290,8 +1291,25 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         SDSP_HIP_CHECK(hipGetLastError());
         kt.mark(1, sk);
         if (sk != st2) SDSP_HIP_CHECK(hipStreamWaitEvent(st2, kt.ev[1], 0));
-        // key spectrogram conditioning (src/lib.rs:1011-1060)
-        if (cfg_.enable_key_hpss_harmonic) {
+        // key spectrogram conditioning (src/lib.rs:1011-1060).  SDSP_KEY_FUSE=1 (experiment): on
+        // the default path (harmonic time mask, margin 12, power 2, then plain HPCP, whose masked
+        // spectrogram nothing else reads) the mask runs inside the HPCP pass (launch_hpcp_masked)
+        // instead of in place over HBM.  It moves a third less HBM data but measured slower
+        // (0.192 vs 0.175 ms per 3-min track, 1757 vs 1796 tracks/s): the mask's
+        // two divisions per element, hidden under k_mask_r's memory time, land on the VALU-bound
+        // HPCP walk.  The default stays k_mask_r in place, then k_hpcp.
+        const bool use_log = cfg_.enable_key_log_frequency;  // :1062-1095
+        const bool tuned = cfg_.enable_key_tuning_compensation && !use_log;
+        const bool whiten = cfg_.enable_key_hpcp_whitening && cfg_.key_hpcp_whitening_smooth_bins >= 3;
+        const bool plain_hpcp = !use_log && cfg_.enable_key_hpcp && !tuned && !whiten && !cfg_.enable_key_hpcp_bass_blend;
+        const bool fuse_mask = std::getenv("SDSP_KEY_FUSE") != nullptr && !cfg_.enable_key_hpss_harmonic &&
+                               cfg_.enable_key_harmonic_mask && plain_hpcp && !cfg_.enable_key_beat_synchronous &&
+                               mask_fused_ok(B8, STRIDE8, (int)std::min<uint64_t>(cfg_.key_spectrogram_smooth_margin, 1 << 20),
+                                             cfg_.key_harmonic_mask_power,
+                                             (int)std::max<uint64_t>(std::min<uint64_t>(cfg_.key_hpcp_peaks_per_frame, 1 << 20), 1));
+        if (fuse_mask) {
+            // the mask runs in launch_hpcp_masked below
+        } else if (cfg_.enable_key_hpss_harmonic) {
             const KeyHpssParams kh = key_hpss_params(cfg_, sr_, B8, fres8);
             if (kh.nb > 0) {  // an empty band returns the spectrogram unchanged (extractor.rs:1408-1410)
                 std::vector<uint64_t> moff(1, 0), mt(1, 0), at(1, 0);
@@ -1318,9 +1336,8 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         else if (cfg_.enable_key_spectrogram_time_smoothing)
             launch_mask(mags8, STRIDE8, B8, d_kpfx, d_kid, NK, (int)cfg_.key_spectrogram_smooth_margin,
                         cfg_.key_harmonic_mask_power, st2, true);
-        const bool use_log = cfg_.enable_key_log_frequency;  // :1062-1095
         // tuning offset per track (:1097-1119)
-        if (cfg_.enable_key_tuning_compensation && !use_log) {
+        if (tuned) {
             TuningParams tp = tuning_params(cfg_, sr_, B8, fres8);
             d_tune = c_.dev<float>("E.tune", (size_t)NK);
             launch_tuning(mags8, d_kpfx, d_kid, NK, tp, d_tune, st2);
@@ -1328,7 +1345,6 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         }
         float* d_chroma = c_.dev<float>("E.chroma", total8 * 12);
         float* d_energy = c_.dev<float>("E.energy", total8);
-        const bool whiten = cfg_.enable_key_hpcp_whitening && cfg_.key_hpcp_whitening_smooth_bins >= 3;
         if (use_log) {  // :1120-1131
             const ChromaParams cp = chroma_params(cfg_, sr_, 1, B8, fres8);
             launch_chroma(1, mags8, d_kpfx, d_ktile, d_kid, NK, ktile.back(), cp, nullptr, d_chroma, d_energy, st2);
@@ -1351,7 +1367,19 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
             // the table upload is queued on the main stream: order the key stream after it
             kt.mark(10);
             SDSP_HIP_CHECK(hipStreamWaitEvent(st2, kt.ev[10], 0));
-            launch_hpcp(mags8, d_kpfx, d_ktile, d_kid, NK, ktile.back(), hp, d_ht, d_chroma, d_energy, st2);
+            if (fuse_mask) {
+                std::vector<uint64_t> kspfx(1, 0);  // mask segments (prefix checkpoints) per key track
+                for (int k = 0; k < NK; k++)
+                    kspfx.push_back(kspfx.back() + (kpfx[(size_t)k + 1] - kpfx[(size_t)k] + KEY_CKPT_SEG - 1) / KEY_CKPT_SEG);
+                uint64_t* d_kspfx = c_.up("E.kseg_pfx", kspfx);
+                float* d_ckpt = c_.dev<float>("E.kckpt", kspfx.back() * KEY_CKPT_STRIDE);
+                kt.mark(11);  // the segment prefix upload is on the main stream
+                SDSP_HIP_CHECK(hipStreamWaitEvent(st2, kt.ev[11], 0));
+                launch_hpcp_masked(mags8, STRIDE8, d_kpfx, d_ktile, d_kspfx, d_ckpt, d_kid, NK, ktile.back(), hp, d_ht,
+                                   d_chroma, d_energy, st2);
+            } else {
+                launch_hpcp(mags8, d_kpfx, d_ktile, d_kid, NK, ktile.back(), hp, d_ht, d_chroma, d_energy, st2);
+            }
         } else {  // :1169-1197 (the tuned variant only when |offset| > 1e-6)
             const ChromaParams cp = chroma_params(cfg_, sr_, 0, B8, fres8);
             launch_chroma(0, mags8, d_kpfx, d_ktile, d_kid, NK, ktile.back(), cp, d_tune, d_chroma, d_energy, st2);
