@@ -16,29 +16,43 @@
 namespace sdsp {
 
 // ---- peak |x| per track (order-free max via atomicMax on the IEEE bits of |x| >= 0) ----
-// PK_CH samples per workgroup, PK_U independent loads in flight per thread.
-constexpr int PK_U = 8;
+// PK_CH samples per workgroup: the 16-B aligned body as float4 loads, all PK_U of a thread in
+// flight at once (a 4-B stream kept too few bytes in flight to reach HBM bandwidth); the < 4
+// unaligned samples at either end as scalars.
+constexpr int PK_U = PK_CH / (4 * 256);  // float4 loads per thread
+static_assert(PK_U * 4 * 256 == PK_CH, "PK_CH = 1024 * PK_U");
 __global__ __launch_bounds__(256) void k_peak_abs(const float* __restrict__ x, const uint64_t* __restrict__ in_off,
                                                   const uint64_t* __restrict__ n_raw,
                                                   const uint64_t* __restrict__ chunk_pfx, int T,
                                                   unsigned int* __restrict__ peak_bits) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
     const uint64_t g = blockIdx.x;
     const int trk = find_track(chunk_pfx, T, g);
     const uint64_t c = g - chunk_pfx[trk];
     const uint64_t s0 = c * PK_CH, n = n_raw[trk];
-    const uint64_t lim = s0 + PK_CH < n ? s0 + PK_CH : n;
-    const float* p = x + in_off[trk];
+    const int64_t len = (int64_t)((s0 + PK_CH < n ? s0 + PK_CH : n) - s0);
+    const float* p = x + in_off[trk] + s0;
+    const int lead = (int)(((16u - ((uintptr_t)p & 15u)) & 15u) / 4u);  // samples before 16-B alignment
+    const int64_t h = lead < len ? lead : len;
+    const int64_t nb = (len - h) / 4;  // aligned float4s
+    // with no aligned float4 the clamped loads below read the 16-B block holding p[0], which lies
+    // inside the allocation like p[0] itself
+    const f4* q = reinterpret_cast<const f4*>(nb > 0 ? p + h : (const float*)((uintptr_t)p & ~(uintptr_t)15));
+    const int tid = threadIdx.x;
     float m = 0.0f;
-    for (uint64_t i0 = s0 + threadIdx.x; i0 < lim; i0 += 256 * PK_U) {
-        float v[PK_U];
+    f4 v[PK_U];
 #pragma unroll
-        for (int u = 0; u < PK_U; u++) {
-            const uint64_t i = i0 + (uint64_t)u * 256;
-            v[u] = i < lim ? sd_absf(p[i]) : 0.0f;
-        }
-#pragma unroll
-        for (int u = 0; u < PK_U; u++) m = sd_maxf(m, v[u]);
+    for (int u = 0; u < PK_U; u++) {
+        const int64_t k = tid + 256 * u;  // clamped unconditional load, then a select (no per-load wait)
+        const f4 qv = q[k < nb ? k : (nb > 0 ? nb - 1 : 0)];  // nb == 0: q[0], see above
+        v[u] = k < nb ? qv : f4{0.0f, 0.0f, 0.0f, 0.0f};
     }
+    if (tid < h) m = sd_absf(p[tid]);
+    const int64_t tl = h + 4 * nb;
+    if (tid < len - tl) m = sd_maxf(m, sd_absf(p[tl + tid]));
+#pragma unroll
+    for (int u = 0; u < PK_U; u++)
+        m = sd_maxf(m, sd_maxf(sd_maxf(sd_absf(v[u].x), sd_absf(v[u].y)), sd_maxf(sd_absf(v[u].z), sd_absf(v[u].w))));
     m = wave_max(m);
     if ((threadIdx.x & 63) == 0 && m > 0.0f) atomicMax(&peak_bits[trk], sd_bits_f(m));
 }
