@@ -54,7 +54,7 @@
  *
  * Twiddles are cos/sin evaluated in double by sdsp_libm and rounded once to f32.  Both the
  * CPU restatement (oracle/) and the HIP kernels implement exactly this operation order, so
- * their spectra agree bit for bit; tests/test_oracle_fft.py checks the specification
+ * their spectra agree bit for bit; tests/test_spec.py checks the specification
  * against numpy's float64 FFT (relative error <= 2e-6 of the frame's peak).
  */
 #ifndef SDSP_FFT_SPEC_H
