@@ -8,8 +8,9 @@
 //   folds from -0.0) and divided by `channels as f32`.
 // This front-end reads RIFF/WAVE (PCM, IEEE float, A-law, mu-law, and WAVE_FORMAT_EXTENSIBLE
 // with those sub-formats), which symphonia decodes into exactly those buffer types (A-law /
-// mu-law expand to S16, ITU-T G.711).  A frame's mono value depends only on that frame, so
-// packet boundaries do not matter.  Everything else is a decoding error.
+// mu-law expand to S16, ITU-T G.711), and FLAC (host_flac.hip; symphonia's S32 buffers).  A
+// frame's mono value depends only on that frame, so packet boundaries do not matter.  Other
+// containers and codecs (MP3, AAC, Ogg Vorbis, ALAC, ...) are a decoding error.
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -18,6 +19,8 @@
 #include <vector>
 
 #include "../../include/stratum_hip.h"
+
+bool sdsp_decode_flac(const std::vector<uint8_t>& f, std::vector<float>* out, uint32_t* sr, std::string* err);
 
 namespace {
 
@@ -183,7 +186,17 @@ extern "C" int32_t sdsp_decode_audio_file(const char* path, float** samples, uin
     std::fclose(fp);
     std::vector<float> mono;
     uint32_t sr = 0;
-    if (!decode_wav(buf, &mono, &sr, err, errlen)) return SDSP_ERR_DECODING;
+    const bool flac = (buf.size() >= 4 && std::memcmp(buf.data(), "fLaC", 4) == 0) ||
+                      (buf.size() >= 3 && std::memcmp(buf.data(), "ID3", 3) == 0);
+    if (flac) {
+        std::string why;
+        if (!sdsp_decode_flac(buf, &mono, &sr, &why)) {
+            fail(err, errlen, why);
+            return SDSP_ERR_DECODING;
+        }
+    } else if (!decode_wav(buf, &mono, &sr, err, errlen)) {
+        return SDSP_ERR_DECODING;
+    }
     float* p = (float*)std::malloc(std::max<size_t>(mono.size(), 1) * sizeof(float));
     if (!p) return SDSP_ERR_PROCESSING;
     if (!mono.empty()) std::memcpy(p, mono.data(), mono.size() * sizeof(float));

@@ -170,7 +170,7 @@ def compute_confidence(result):
 
 
 def decode_audio_file(path):
-    """The decode front-end (sdsp_decode_audio_file): RIFF/WAVE -> (mono float32 array, sample_rate),
+    """The decode front-end (sdsp_decode_audio_file): RIFF/WAVE or FLAC -> (mono float32 array, sample_rate),
     converted as examples/analyze_file.rs:25-180 does.  Raises AnalysisError(DecodingError)."""
     p = C.POINTER(C.c_float)()
     n = C.c_uint64()
