@@ -304,18 +304,20 @@ __device__ inline void hpcp_accumulate(float (*pc)[HP_FRAMES], int i, int bin, f
 template <int KCAP, int KB>
 __device__ __forceinline__ void topk_insert(float (&pm)[KCAP], int (&pb)[KCAP], float& thr, float v, int vb) {
     if (!(v > thr)) return;
-    bool ins = false;
+    // the descending list's insertion as in HpcpFrame::walk (k_key.hip): gt[q] = v > pm[q] turns
+    // true once; slots are updated from the tail in place
+    bool gt[KCAP];
 #pragma unroll
-    for (int q = 0; q < KCAP; q++) {
-        const bool sw = ins || v > pm[q];
-        const float tv = pm[q];
-        const int tb = pb[q];
-        pm[q] = sw ? v : tv;
-        pb[q] = sw ? vb : tb;
-        v = sw ? tv : v;
-        vb = sw ? tb : vb;
-        ins = sw;
+    for (int q = 0; q < KCAP; q++) gt[q] = v > pm[q];
+#pragma unroll
+    for (int q = KCAP - 1; q >= 1; q--) {
+        const float nv = gt[q - 1] ? pm[q - 1] : v;
+        const int nbv = gt[q - 1] ? pb[q - 1] : vb;
+        pm[q] = gt[q] ? nv : pm[q];
+        pb[q] = gt[q] ? nbv : pb[q];
     }
+    pm[0] = gt[0] ? v : pm[0];
+    pb[0] = gt[0] ? vb : pb[0];
     thr = pm[KCAP - 1];
 }
 

@@ -214,22 +214,22 @@ struct HpcpFrame {
             e += m * m;
             const int c = b - 1;  // candidate peak bin, needs m[c-1] = m2, m[c] = m1, m[c+1] = m
             if (c >= P.pk_lo && c <= P.pk_hi && !(m1 <= m2 || m1 < m) && m1 > thr) {
-                // insertion into the descending list; once inserted, every later slot shifts
-                // (an equal magnitude already listed has the lower bin and stays ahead)
-                float v = m1;
-                int vb = c;
-                bool ins = false;
+                // insertion into the descending list: gt[q] = m1 > pm[q] is false then true along
+                // the list (an equal magnitude already listed has the lower bin and stays
+                // ahead), so slot q takes m1 where gt turns true and its predecessor after that.
+                // Updated from the tail in place: one compare and four selects per slot.
+                bool gt[KCAP];
 #pragma unroll
-                for (int q = 0; q < KCAP; q++) {
-                    const bool sw = ins || v > pm[q];
-                    const float tv = pm[q];
-                    const int tb = pb[q];
-                    pm[q] = sw ? v : tv;
-                    pb[q] = sw ? vb : tb;
-                    v = sw ? tv : v;
-                    vb = sw ? tb : vb;
-                    ins = sw;
+                for (int q = 0; q < KCAP; q++) gt[q] = m1 > pm[q];
+#pragma unroll
+                for (int q = KCAP - 1; q >= 1; q--) {
+                    const float nv = gt[q - 1] ? pm[q - 1] : m1;
+                    const int nbv = gt[q - 1] ? pb[q - 1] : c;
+                    pm[q] = gt[q] ? nv : pm[q];
+                    pb[q] = gt[q] ? nbv : pb[q];
                 }
+                pm[0] = gt[0] ? m1 : pm[0];
+                pb[0] = gt[0] ? c : pb[0];
                 thr = pm[KCAP - 1];
             }
             m2 = m1;
@@ -271,11 +271,16 @@ struct HpcpFrame {
     }
 };
 
+// 4 waves per SIMD (128 VGPRs for KCAP = 24, a 16-byte spill outside the bin walk): 8 % faster
+// than the 129-VGPR / 3-wave build in the serial profile (14.6 vs 15.9 ms per 256-track launch)
+#ifndef SDSP_HPCP_ATTR
+#define SDSP_HPCP_ATTR __attribute__((amdgpu_waves_per_eu(4)))
+#endif
 // One thread per frame, HP_FRAMES frames per workgroup.  Bins are staged through LDS in
 // HP_CW-column chunks (coalesced row segments) and each thread walks its frame's bins in
 // order (HpcpFrame).
 template <int KCAP>
-__global__ __launch_bounds__(HP_FRAMES) void k_hpcp(const float* __restrict__ mags,
+__global__ __launch_bounds__(HP_FRAMES) SDSP_HPCP_ATTR void k_hpcp(const float* __restrict__ mags,
                                                     const uint64_t* __restrict__ frame_pfx,
                                                     const uint64_t* __restrict__ tile_pfx,
                                                     const int* __restrict__ tracks, int n_items, HpcpParams P,
