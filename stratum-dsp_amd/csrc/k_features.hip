@@ -62,6 +62,27 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
     const uint64_t g = g0 + (uint64_t)f;
 
     float e[4] = {0, 0, 0, 0}, h[4] = {0, 0, 0, 0}, sx[4] = {0, 0, 0, 0}, so = 0.0f;
+    // The sub-bands are disjoint and ascend in bin order (pipeline: low [b0, bl), mid [bl, bm),
+    // high [bm, bh)), so each band's folds are one contiguous run of the walk: they go to the
+    // accumulators eb/hb/sb of the band the walk is in (cur, wave-uniform), which are stored
+    // into e/h/sx[cur] when the run ends.  Per bin that is one add each instead of a select per
+    // band, and the band's SuperFlux term is the full band's (same product) except within K
+    // bins of a band edge.
+    float eb = 0.0f, hb = 0.0f, sb = 0.0f;
+    int cur = 0;
+    auto band_of = [&](int b) {
+        int v = 0;
+#pragma unroll
+        for (int q = 3; q >= 1; q--)
+            if (P.band_on[q] && b >= P.bs[q] && b < P.be[q]) v = q;
+        return v;
+    };
+    auto flush = [&]() {
+        if (cur == 1) e[1] = eb, h[1] = hb, sx[1] = sb;
+        else if (cur == 2) e[2] = eb, h[2] = hb, sx[2] = sb;
+        else if (cur == 3) e[3] = eb, h[3] = hb, sx[3] = sb;
+        eb = hb = sb = 0.0f;
+    };
     float accA = 0.0f, accB = 0.0f;
     int mA = 0;
     // frame f of this track lives in row (f even ? A : B) r0 + (f >> 1) * step (RowMap)
@@ -136,7 +157,10 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
         __syncthreads();
         if (c0 + CW < B) load(c0 + CW + K);
         const int nb = B - c0 < CW ? B - c0 : CW;
-        if (!valid) continue;
+        // a wave with no valid frame skips the walk; lanes of invalid frames in a partly valid
+        // wave walk zero rows (their results are not stored), which keeps the band bookkeeping
+        // (cur) wave-uniform
+        if (__builtin_amdgcn_ballot_w64(valid) == 0) continue;
         // KK > 0: previous frame's L for bins [c0 - KK, c0 + CW + KK) (0 outside [0, B))
         float Rw[KK > 0 ? CW + 2 * KK : 1];
         if (KK > 0 && has_prev) {
@@ -153,12 +177,15 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
             const float hh = (float)b * m * m;
             e[0] += ee;
             h[0] += hh;
-#pragma unroll
-            for (int v = 1; v < 4; v++)
-                if (P.band_on[v] && b >= P.bs[v] && b < P.be[v]) {
-                    e[v] += ee;
-                    h[v] += hh;
-                }
+            const int vb = band_of(b);
+            if (vb != cur) {
+                flush();
+                cur = vb;
+            }
+            if (vb) {
+                eb += ee;
+                hb += hh;
+            }
             const float lc = Lt[i + 1][s];
 #ifndef SDSP_EXP_FT_NOMEL
             if (P.n_mels > 0) {
@@ -167,7 +194,7 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
 #endif
                 const MelPlan mp = mel[b];
                 for (int q = 0; q < mp.nflush; q++) {
-                    MEL[(uint64_t)mA * total + g] = accA;
+                    if (valid) MEL[(uint64_t)mA * total + g] = accA;
                     accA = accB;
                     accB = 0.0f;
                     mA++;
@@ -213,30 +240,31 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
                     for (int q = lo; q < hi; q++) pm = max_bnn(pm, Lt[i][q & (W - 1)]);  // L is never NaN
                 }
                 const float df = max_bnn(lc - pm, 0.0f);
-                sx[0] += df * df;
+                const float df2 = df * df;
+                sx[0] += df2;
+                if (vb) {
+                    const int bsv = P.bs[vb], bev = P.be[vb];
+                    if (lo < bsv || hi > bev) {  // window clipped at the band edge
+                        const int lb = lo < bsv ? bsv : lo;
+                        const int hbd = hi > bev ? bev : hi;
+                        float pmb = 0.0f;
+                        if constexpr (KK > 0) {
 #pragma unroll
-                for (int v = 1; v < 4; v++) {
-                    if (P.band_on[v] && b >= P.bs[v] && b < P.be[v]) {
-                        float pmb = pm;
-                        if (lo < P.bs[v] || hi > P.be[v]) {
-                            const int lb = lo < P.bs[v] ? P.bs[v] : lo;
-                            const int hb = hi > P.be[v] ? P.be[v] : hi;
-                            pmb = 0.0f;
-                            if constexpr (KK > 0) {
-#pragma unroll
-                                for (int q = 0; q <= 2 * KK; q++)
-                                    if (b - KK + q >= lb && b - KK + q < hb) pmb = max_bnn(pmb, Rw[j + q]);
-                            } else {
-                                for (int q = lb; q < hb; q++) pmb = max_bnn(pmb, Lt[i][q & (W - 1)]);
-                            }
+                            for (int q = 0; q <= 2 * KK; q++)
+                                if (b - KK + q >= lb && b - KK + q < hbd) pmb = max_bnn(pmb, Rw[j + q]);
+                        } else {
+                            for (int q = lb; q < hbd; q++) pmb = max_bnn(pmb, Lt[i][q & (W - 1)]);
                         }
                         const float db = max_bnn(lc - pmb, 0.0f);
-                        sx[v] += db * db;
+                        sb += db * db;
+                    } else {
+                        sb += df2;
                     }
                 }
             }
         }
     }
+    flush();
     if (!valid) return;
     for (; mA < P.n_mels; mA++) {
         MEL[(uint64_t)mA * total + g] = accA;
