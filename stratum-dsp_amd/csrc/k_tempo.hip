@@ -533,7 +533,8 @@ __global__ __launch_bounds__(64) void k_multires(const int* __restrict__ tracks,
     __shared__ int ok_s;
     const int i = blockIdx.x;
     const int trk = tracks[i];
-    if (n256[i] < 0 || n1024[i] < 0) {  // a hop's tempogram failed: multi_resolution returns Err
+    const int j512 = P.own512 ? i : trk;  // index of this item's hop-512 data
+    if (n256[i] < 0 || n1024[i] < 0 || n512[j512] < 0) {  // a hop's tempogram failed: multi_resolution returns Err
         if (threadIdx.x == 0) {
             mr_est[i].ok = 0;
             used[trk] = 0;
@@ -543,7 +544,7 @@ __global__ __launch_bounds__(64) void k_multires(const int* __restrict__ tracks,
     // candidate lists staged in LDS when they fit (lane 0's lookups are latency-bound)
     __shared__ float s_c[3][4 * MR_CAP_LDS];
     CandList L256{c256 + (uint64_t)i * cap256 * 4, n256[i]};
-    CandList L512{c512 + (uint64_t)trk * cap512 * 4, n512[trk]};
+    CandList L512{c512 + (uint64_t)j512 * cap512 * 4, n512[j512]};
     CandList L1024{c1024 + (uint64_t)i * cap1024 * 4, n1024[i]};
     CandList* Ls[3] = {&L256, &L512, &L1024};
     for (int l = 0; l < 3; l++) {
@@ -698,8 +699,8 @@ __global__ __launch_bounds__(64) void k_multires(const int* __restrict__ tracks,
         return;
     }
     const int nf = n_fam_s;
-    const uint64_t g0 = fpfx512[trk];
-    const int nn = (int)(fpfx512[trk + 1] - g0) - 1;
+    const uint64_t g0 = fpfx512[j512];
+    const int nn = (int)(fpfx512[j512 + 1] - g0) - 1;
     const float* nov = nov512 + g0;
     __shared__ float sbuf[SEQ_CH];
     const float nov_total = (nf >= 2 && nn > 0) ? block_seq_sum(nov, nn, sbuf) : 0.0f;

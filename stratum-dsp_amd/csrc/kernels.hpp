@@ -80,6 +80,7 @@ struct MrParams {
     float min_bpm, max_bpm, tol, w512, w256, w1024, dt, margin_thr;
     int human_prior, top_k, band;
     int sr, hop512;
+    int own512;  // 1: the hop-512 lists / novelty are the escalation's own pass (item order), else the base pass's (track order)
 };
 
 // ---- k_beat ----

@@ -549,10 +549,6 @@ std::string unsupported(const sdsp_config& c, uint32_t sr) {
     if (c.key_hpcp_num_harmonics > (uint64_t)SUPPORT_HMAX) return "key_hpcp_num_harmonics > 8";
     if (c.enable_key_multi_scale && c.key_multi_scale_lengths_len > 8) return "more than 8 multi-scale key lengths";
     if (c.enable_ml_refinement) return "ML refinement";
-    const bool use_aux = c.enable_tempogram_band_fusion || c.enable_tempogram_mel_novelty ||
-                         c.tempogram_band_consensus_bonus > 0.0f;
-    if (c.enable_tempogram_multi_resolution && (c.hop_size != 512 || !use_aux))
-        return "multi-resolution escalation with hop_size != 512 or without band/mel variants";
     return "";
 }
 
@@ -576,13 +572,16 @@ struct TempoPassIn {
     const float* base_mags = nullptr;
     const float* base_fmax = nullptr;
     std::vector<uint64_t> base_row0;
+    // also the hop-512 novelty multi_resolution.rs:680-694 gates its folds with (the combined
+    // novelty with the configured weights, whatever the band-fusion setting; out.nov_mr)
+    bool mr_nov = false;
 };
 struct TempoPassOut {
     std::vector<uint64_t> fpfx;  // frame prefix over the pass's tracks
     uint64_t total = 0;
     // device pointers (valid until the next pass with the same tag)
     float *mags = nullptr, *fmax = nullptr, *E = nullptr, *H = nullptr, *SFX = nullptr, *SFO = nullptr, *MEL = nullptr,
-          *nov = nullptr, *nov_sum = nullptr, *cand = nullptr;
+          *nov = nullptr, *nov_sum = nullptr, *cand = nullptr, *nov_mr = nullptr;
     uint64_t* d_fpfx = nullptr;
     TempoEst* est = nullptr;
     int* active = nullptr;
@@ -684,6 +683,7 @@ void Pipeline::run(const float* d_samples, const std::vector<uint64_t>& in_off, 
         if (cfg_.enable_hpss_onsets || cfg_.enable_tempogram_percussive_fallback)  // H, P ping-pong + a copy
             need[i] += n / hop * STRIDE2 * 4.0 * 5.0;
         if (cfg_.enable_key_hpss_harmonic && !bpm_only_) need[i] += n / khop * 1024.0 * 4.0;
+        if (cfg_.enable_tempogram_multi_resolution && hop != 512) need[i] += n / 512 * STRIDE2 * 4.0 * 1.3;
         total_need += need[i];
     }
     const double parts = std::max(1.0, std::ceil(total_need / budget));
@@ -970,6 +970,25 @@ void Pipeline::tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPa
                    (int)std::max<uint64_t>(cfg_.tempogram_mel_max_filter_bins, 1), mel_on,
                    c_.dev<unsigned int>(tag + "melmax", (size_t)std::max(P_T, 1)), d_.stream);
     SDSP_HIP_CHECK(hipGetLastError());
+    o.nov_mr = o.nov;
+    if (in.mr_nov && !band_cfg) {
+        // without the auxiliary variants the tempogram's novelty uses combined_novelty's defaults,
+        // but multi-resolution's hop-512 novelty still takes the configured weights
+        // (multi_resolution.rs:680-694): the full-band variant again, with those
+        NovParams nm = np;
+        nm.ws = sd_maxf(cfg_.tempogram_novelty_w_spectral, 0.0f);
+        nm.we = sd_maxf(cfg_.tempogram_novelty_w_energy, 0.0f);
+        nm.wh = sd_maxf(cfg_.tempogram_novelty_w_hfc, 0.0f);
+        nm.lmw = (int)cfg_.tempogram_novelty_local_mean_window;
+        nm.smw = (int)cfg_.tempogram_novelty_smooth_window;
+        nm.wsum = sd_maxf(nm.ws + nm.we + nm.wh, EPS);
+        for (int v = 1; v < 4; v++) nm.band_on[v] = 0;
+        o.nov_mr = c_.dev<float>(tag + "novmr", NVAR * std::max<uint64_t>(total, 1));
+        launch_novelty(o.E, o.H, o.SFX, o.d_fpfx, P_T, total, nm, scratch, o.nov_mr,
+                       c_.dev<float>(tag + "novmrsum", NVAR * (size_t)std::max(P_T, 1)), o.MEL, 0, 1, false,
+                       c_.dev<unsigned int>(tag + "melmax", (size_t)std::max(P_T, 1)), d_.stream);
+        SDSP_HIP_CHECK(hipGetLastError());
+    }
     tm.mark(2);
     // tempograms: items (track, variant) for active tracks
     int present[NVAR];
@@ -1201,6 +1220,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     bin.top_n = mr_on ? base_top_n : (cfg_.emit_tempogram_candidates ? (int)cfg_.tempogram_candidates_top_n : 1);
     bin.cand_cap = std::max(bin.top_n, 1);
     bin.gate = mr_on;
+    bin.mr_nov = mr_on && HOP == 512;  // at another hop the escalation runs its own hop-512 pass
     // ---------------- E: key (second stream; overlaps B-D) ----------------
     // The key path depends only on the trimmed signal, so it is forked onto the context's key
     // stream right after trimming and joined before the results are read back: its
@@ -1561,6 +1581,11 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     int* d_used = c_.up("B.used", used);
     // ---------------- C: escalation (multi_resolution.rs:205-901) ----------------
     TempoEst* d_mr_all = nullptr;  // multi-res estimates of the escalated tracks (E order)
+    // hop_size != 512: the escalation's own hop-512 candidate lists (E order; emitted for the
+    // tracks that take the multi-res estimate, src/lib.rs:546,686) and the E position of each track
+    std::vector<float> c512_h;
+    std::vector<int> n512_own, epos((size_t)NR, -1);
+    int c512_cap = 0;
     if (mr_on && !E.empty()) {
         const int NE = (int)E.size();
         const int top_k = (int)std::max<uint64_t>(cfg_.tempogram_multi_res_top_k, 1);
@@ -1573,22 +1598,37 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
             ein.n_trim.push_back(bin.n_trim[(size_t)i]);
         }
         ein.want_onsets = false;
-        ein.base_mags = bo.mags;
-        ein.base_fmax = bo.fmax;
-        for (int i : E) ein.base_row0.push_back(bo.fpfx[(size_t)i]);
+        ein.gate = 0;
+        // multi_resolution.rs:237-239 recomputes the STFT at hops 256, 512 and 1024 of the trimmed
+        // samples.  At hop_size 512 the base pass is the hop-512 one; otherwise the escalated
+        // tracks get their own hop-512 pass (top_k candidates, :273) first.  The hop-256 and
+        // hop-1024 passes read the hop-512 rows they share with it (SDSP_NO_ROW_REUSE: control).
+        const bool own512 = HOP != 512;
+        TempoPassOut o256, o512, o1024;
+        if (own512) {
+            ein.hop = 512;
+            ein.top_n = top_k;
+            ein.cand_cap = top_k;
+            ein.mr_nov = true;
+            tempo_pass("C512.", ein, o512);
+            ein.mr_nov = false;
+        }
+        const TempoPassOut& b512 = own512 ? o512 : bo;
+        ein.base_mags = b512.mags;
+        ein.base_fmax = b512.fmax;
+        for (int k = 0; k < NE; k++) ein.base_row0.push_back(b512.fpfx[own512 ? (size_t)k : (size_t)E[(size_t)k]]);
         ein.top_n = aux_k;
         ein.cand_cap = aux_k;
-        ein.gate = 0;
-        TempoPassOut o256, o1024;
-        // multi-resolution runs only at hop 512 (unsupported()); SDSP_NO_ROW_REUSE: A/B switch
         const bool reuse_on = std::getenv("SDSP_NO_ROW_REUSE") == nullptr;  // read per call (tests flip it)
         ein.hop = 256;
-        ein.reuse = (HOP == 512 && reuse_on) ? 2 : 0;
+        ein.reuse = reuse_on ? 2 : 0;
         tempo_pass("C256.", ein, o256);
         ein.hop = 1024;
-        ein.reuse = (HOP == 512 && reuse_on) ? 1 : 0;
+        ein.reuse = reuse_on ? 1 : 0;
         tempo_pass("C1024.", ein, o1024);
-        for (TempoPassOut* o : {&o256, &o1024}) {
+        std::vector<TempoPassOut*> mr_passes = {&o256, &o1024};
+        if (own512) mr_passes.push_back(&o512);
+        for (TempoPassOut* o : mr_passes) {
             times_.stft2048_ms += o->stft_ms;
             times_.stft2048_launches += o->stft_launch;
             times_.stft2048_bytes += o->stft_bytes;
@@ -1601,7 +1641,20 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
             n256[(size_t)k] = e256[(size_t)k].ok ? e256[(size_t)k].n_cands : -1;
             n1024[(size_t)k] = e1024[(size_t)k].ok ? e1024[(size_t)k].n_cands : -1;
         }
-        for (int i = 0; i < NR; i++) n512[(size_t)i] = std::min(best[(size_t)i].n_cands, top_k);
+        if (own512) {  // E order; -1: the hop-512 tempogram failed (multi_resolution returns Err)
+            const std::vector<TempoEst> e512 = c_.down(o512.est, (size_t)NE);
+            n512.assign((size_t)NE, 0);
+            for (int k = 0; k < NE; k++)
+                n512[(size_t)k] = e512[(size_t)k].ok ? std::min(e512[(size_t)k].n_cands, top_k) : -1;
+            if (cfg_.emit_tempogram_candidates) {
+                c512_h = c_.down(o512.cand, (size_t)NE * (size_t)top_k * 4);
+                n512_own = n512;
+                c512_cap = top_k;
+                for (int k = 0; k < NE; k++) epos[(size_t)E[(size_t)k]] = k;
+            }
+        } else {
+            for (int i = 0; i < NR; i++) n512[(size_t)i] = std::min(best[(size_t)i].n_cands, top_k);
+        }
         int* d_n256 = c_.up("C.n256", n256);
         int* d_n1024 = c_.up("C.n1024", n1024);
         int* d_n512 = c_.up("C.n512", n512);
@@ -1620,10 +1673,12 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         mp.band = 1;  // src/lib.rs:509 always passes Some(band_cfg)
         mp.sr = (int)sr_;
         mp.hop512 = 512;
+        mp.own512 = own512 ? 1 : 0;
         TempoEst* d_mr = c_.dev<TempoEst>("C.mr", (size_t)NE);
         d_mr_all = d_mr;
-        launch_multires(d_E, NE, o256.cand, d_n256, bo.cand, d_n512, o1024.cand, d_n1024, ein.cand_cap, bin.cand_cap,
-                        ein.cand_cap, bo.est, bo.nov, bo.d_fpfx, mp, d_mr, d_used, d_fbpm, d_fconf, st);
+        launch_multires(d_E, NE, o256.cand, d_n256, b512.cand, d_n512, o1024.cand, d_n1024, ein.cand_cap,
+                        own512 ? top_k : bin.cand_cap, ein.cand_cap, bo.est, b512.nov_mr, b512.d_fpfx, mp, d_mr, d_used,
+                        d_fbpm, d_fconf, st);
         SDSP_HIP_CHECK(hipGetLastError());
         used = c_.down(d_used, (size_t)NR);
         for (int i : E) {
@@ -1859,6 +1914,14 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
             const std::vector<float>& pc = perc_cands[(size_t)i];
             for (size_t k = 0; k + 4 <= pc.size(); k += 4) {
                 sdsp_tempo_candidate tc{pc[k], pc[k + 1], pc[k + 2], pc[k + 3], (uint8_t)(sd_absf(pc[k] - r.bpm) < 0.75f)};
+                r.cands.push_back(tc);
+            }
+        } else if (cfg_.emit_tempogram_candidates && r.mr_used == 1 && epos[(size_t)i] >= 0) {
+            r.has_cands = true;  // the escalation's own hop-512 list (hop_size != 512)
+            const int k = epos[(size_t)i];
+            for (int c = 0; c < n512_own[(size_t)k]; c++) {
+                const float* cc = c512_h.data() + ((size_t)k * (size_t)c512_cap + (size_t)c) * 4;
+                sdsp_tempo_candidate tc{cc[0], cc[1], cc[2], cc[3], (uint8_t)(sd_absf(cc[0] - r.bpm) < 0.75f)};
                 r.cands.push_back(tc);
             }
         } else if (cfg_.emit_tempogram_candidates && best[(size_t)i].ok && tg_on) {
