@@ -15,6 +15,7 @@
 namespace sdsp {
 
 constexpr int NACF_MAX = 512;
+constexpr int ACF_U = 16;  // k_acf_tempogram: fold steps loaded per block
 
 // ----------------------------------------------------------------------------------------
 // Block-cooperative complex FFT, Stockham radix-4 (+radix-2) exactly as sdsp_fft_spec.h.
@@ -198,7 +199,11 @@ __global__ __launch_bounds__(256) void k_fft_tempogram(const int* __restrict__ i
 }
 
 // ----------------------------------------------------------------------------------------
-// Autocorrelation tempogram: one thread per BPM of the min..=max grid (lag per BPM given).
+// Autocorrelation tempogram: one thread per BPM of the min..=max grid (lag per BPM given).  The
+// lag sum is a sequential fold; its operands are loaded ACF_U steps at a time, the next block in
+// flight while the current one is folded, so the fold waits on one L2 round trip per ACF_U steps
+// instead of one per step.  (Staging the curve in LDS measured 2x slower: 62 KB per workgroup
+// cut the waves per CU.)
 __global__ __launch_bounds__(256) void k_acf_tempogram(const int* __restrict__ items, const float* __restrict__ nov,
                                                        const uint64_t* __restrict__ frame_pfx, uint64_t total,
                                                        const float* __restrict__ bpm_grid,
@@ -217,12 +222,38 @@ __global__ __launch_bounds__(256) void k_acf_tempogram(const int* __restrict__ i
         uint64_t key = ~0ull;
         if (j < NB) {
             const int64_t lag = lag_grid[j];
+            const int64_t n = L - lag;  // terms i = 0 .. n-1 (autocorrelation over i + lag < L)
             float acc = 0.0f;
-            int32_t cnt = 0;
-            for (int64_t i = 0; i + lag < L; i++) {
-                acc += x[i] * x[i + lag];
-                cnt++;
+            int64_t i = 0;
+            if (n >= ACF_U) {
+                float a[ACF_U], b[ACF_U], na[ACF_U], nb[ACF_U];
+#pragma unroll
+                for (int u = 0; u < ACF_U; u++) {
+                    a[u] = x[u];
+                    b[u] = x[u + lag];
+                }
+                for (;;) {
+                    const bool more = i + 2 * ACF_U <= n;
+                    if (more) {
+#pragma unroll
+                        for (int u = 0; u < ACF_U; u++) {
+                            na[u] = x[i + ACF_U + u];
+                            nb[u] = x[i + ACF_U + u + lag];
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < ACF_U; u++) acc += a[u] * b[u];
+                    i += ACF_U;
+                    if (!more) break;
+#pragma unroll
+                    for (int u = 0; u < ACF_U; u++) {
+                        a[u] = na[u];
+                        b[u] = nb[u];
+                    }
+                }
             }
+            for (; i < n; i++) acc += x[i] * x[i + lag];
+            const int32_t cnt = n > 0 ? (int32_t)n : 0;
             const float sv = cnt > 0 ? acc / (float)cnt : 0.0f;
             vals[j] = sv;
             key = key_desc(sv, (uint32_t)j);
@@ -450,6 +481,7 @@ __global__ __launch_bounds__(256) void k_tempo_select(const int* __restrict__ ac
 // loop is spread over the lanes (each phase's sums stay sequential; the max over phases is
 // order-free).
 constexpr int MR_CAP_LDS = 256;
+constexpr int MR_WM_CAP = 28672;  // novelty frames whose window maxima k_multires keeps in LDS (112 KB: 4.6 min at hop 512)
 struct CandList {
     const float* c;  // 4 floats per candidate: bpm, score, fft_norm, ac_norm
     int n;
@@ -468,7 +500,9 @@ __device__ float lookup_c(CandList L, float bpm, float tol) {
 }
 
 // nov_total: novelty.iter().sum() (sequential), computed once per track by the caller
-__device__ float beat_contrast_wave(const float* nov, int n, int sr, int hop, float bpm, float nov_total) {
+// wm (optional): the window maxima max(nov[i-2 .. i+2]) precomputed in LDS, else read per lookup
+__device__ float beat_contrast_wave(const float* nov, int n, int sr, int hop, float bpm, float nov_total,
+                                    const float* wm = nullptr) {
     if (n < 16 || !(sd_isfinite_f(bpm) && bpm > 0.0f) || sr == 0 || hop == 0) return 0.0f;
     const float fpb = (60.0f * (float)sr) / (bpm * (float)hop);
     if (!sd_isfinite_f(fpb) || fpb < 3.0f) return 0.0f;
@@ -477,6 +511,7 @@ __device__ float beat_contrast_wave(const float* nov, int n, int sr, int hop, fl
     const int period = (int)pi, w = 2;
     const float total = sd_maxf(nov_total, 1e-6f);
     auto wmax = [&](int i) {
+        if (wm) return wm[i];
         const int s = i >= w ? i - w : 0, e = i + w + 1 < n ? i + w + 1 : n;
         float mx = 0.0f;
         for (int j = s; j < e; j++) mx = sd_maxf(mx, nov[j]);
@@ -704,9 +739,23 @@ __global__ __launch_bounds__(64) void k_multires(const int* __restrict__ tracks,
     const float* nov = nov512 + g0;
     __shared__ float sbuf[SEQ_CH];
     const float nov_total = (nf >= 2 && nn > 0) ? block_seq_sum(nov, nn, sbuf) : 0.0f;
+    // the family / fold gates read every novelty frame's +-2 window maximum several times per
+    // candidate tempo: computed once into LDS when the track fits (an exact, order-free max)
+    extern __shared__ float mr_wm[];
+    const float* wm = nullptr;
+    if (nf >= 2 && nn > 0 && nn <= P.wm_cap) {
+        for (int q = threadIdx.x; q < nn; q += blockDim.x) {
+            const int s0 = q >= 2 ? q - 2 : 0, e0 = q + 3 < nn ? q + 3 : nn;
+            float mx = 0.0f;
+            for (int j = s0; j < e0; j++) mx = sd_maxf(mx, nov[j]);
+            mr_wm[q] = mx;
+        }
+        __syncthreads();
+        wm = mr_wm;
+    }
     if (nf >= 2 && nn > 0) {
         for (int k = 0; k < nf; k++) {
-            const float a = beat_contrast_wave(nov, nn, P.sr, P.hop512, fam_bpm[k], nov_total);
+            const float a = beat_contrast_wave(nov, nn, P.sr, P.hop512, fam_bpm[k], nov_total, wm);
             if (threadIdx.x == 0) fam_align[k] = a;
             __syncthreads();
         }
@@ -740,7 +789,7 @@ __global__ __launch_bounds__(64) void k_multires(const int* __restrict__ tracks,
     }
     __syncthreads();
     if (do_fam_s) {
-        cur_align = beat_contrast_wave(nov, nn, P.sr, P.hop512, best_bpm_s, nov_total);
+        cur_align = beat_contrast_wave(nov, nn, P.sr, P.hop512, best_bpm_s, nov_total, wm);
         if (threadIdx.x == 0) {
             if (sd_absf(fam_bpm[4] - best_bpm_s) > 0.75f && fam_align[4] >= cur_align + 0.40f) {
                 best_bpm_s = fam_bpm[4];
@@ -806,8 +855,12 @@ void launch_multires(const int* tracks, int n_items, const float* c256, const in
                      const TempoEst* base_est, const float* nov512, const uint64_t* fpfx512, const MrParams& P,
                      TempoEst* mr_est, int* used, float* final_bpm, float* final_conf, hipStream_t st) {
     if (n_items == 0) return;
-    hipLaunchKernelGGL(k_multires, dim3(n_items), dim3(64), 0, st, tracks, n_items, c256, n256, c512, n512, c1024,
-                       n1024, cap256, cap512, cap1024, base_est, nov512, fpfx512, P, mr_est, used, final_bpm,
+    MrParams Q = P;
+    Q.wm_cap = MR_WM_CAP;
+    const size_t lds = (size_t)MR_WM_CAP * sizeof(float);
+    (void)hipFuncSetAttribute((const void*)k_multires, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k_multires, dim3(n_items), dim3(64), lds, st, tracks, n_items, c256, n256, c512, n512, c1024,
+                       n1024, cap256, cap512, cap1024, base_est, nov512, fpfx512, Q, mr_est, used, final_bpm,
                        final_conf);
 }
 

@@ -81,6 +81,7 @@ struct MrParams {
     int human_prior, top_k, band;
     int sr, hop512;
     int own512;  // 1: the hop-512 lists / novelty are the escalation's own pass (item order), else the base pass's (track order)
+    int wm_cap;  // set by launch_multires: novelty window maxima kept in LDS up to this many frames
 };
 
 // ---- k_beat ----
