@@ -621,6 +621,17 @@ class Pipeline {
 
     void sub_batch(const float* d_samples, const std::vector<uint64_t>& in_off, const std::vector<uint64_t>& n_raw,
                    const std::vector<int>& idx, std::vector<TrackRes>& res);
+    // The key results of a sub-batch are joined late: its key-stream tail (mask, HPCP, vote) runs
+    // under the next sub-batch's tempo path instead of holding it back.  Uploads read by the key
+    // stream and the key output live in per-parity buffers (E0.*, E1.*) for that.
+    struct KeyPending {
+        std::unique_ptr<Timers> kt;
+        KeyOut* d_kout = nullptr;
+        std::vector<size_t> at;  // result slot of each key track
+    };
+    std::unique_ptr<KeyPending> key_pending_;
+    int sb_parity_ = 0;
+    void finish_key(std::vector<TrackRes>& res);
     void tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPassOut& out);
     void legacy_select(const TempoPassIn& bin, const uint32_t* d_onsets, const uint64_t* d_on_off, const int* d_on_n,
                        const std::vector<int>& R, const std::vector<int>& idx, std::vector<TrackRes>& res,
@@ -701,6 +712,7 @@ void Pipeline::run(const float* d_samples, const std::vector<uint64_t>& in_off, 
         cum += need[i];
     }
     flush();
+    finish_key(res);
     times_.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     d_.last = times_;
 }
@@ -1129,6 +1141,25 @@ struct HostTrace {
     }
 };
 
+void Pipeline::finish_key(std::vector<TrackRes>& res) {
+    if (!key_pending_) return;
+    KeyPending& kp = *key_pending_;
+    SDSP_HIP_CHECK(hipStreamWaitEvent(d_.stream, kp.kt->ev[2], 0));
+    const std::vector<KeyOut> kout = c_.down(kp.d_kout, kp.at.size());
+    for (size_t k = 0; k < kp.at.size(); k++) {
+        TrackRes& r = res[kp.at[k]];
+        const KeyOut& ko = kout[k];
+        if (!ko.ok) continue;
+        r.key_mode = ko.mode;
+        r.key_tonic = ko.tonic;
+        r.key_conf = ko.conf;
+        r.key_clarity = ko.clarity;
+    }
+    times_.stft8192_ms += kp.kt->ms(0, 1);
+    times_.key_ms += kp.kt->ms(1, 2);
+    key_pending_.reset();
+}
+
 void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in_off, const std::vector<uint64_t>& n_raw,
                          const std::vector<int>& idx, std::vector<TrackRes>& res) {
     const int T = (int)idx.size();
@@ -1266,8 +1297,12 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     const int NK = (int)K.size();
     std::vector<KeyOut> kout;
     KeyOut* d_kout = nullptr;
-    Timers kt;
+    std::unique_ptr<Timers> ktp(new Timers());
+    Timers& kt = *ktp;
     kt.init(d_);
+    // per-parity names of what the main stream uploads for the key stream (see KeyPending)
+    sb_parity_ ^= 1;
+    const std::string EP = sb_parity_ ? "E1." : "E0.";
     // SDSP_SERIAL_STREAMS=1 keeps the key path on the main stream (per-kernel profiling)
     static const bool serial_streams = std::getenv("SDSP_SERIAL_STREAMS") != nullptr;
     // SDSP_KEY_STFT_FIRST=1 (schedule experiment): the 8192-point STFT on the main stream ahead
@@ -1289,16 +1324,16 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     const float fres8 = (float)sr_ / (float)KFS;
     if (NK > 0) {
         const uint64_t total8 = kpfx.back();
-        d_kpfx = c_.up("E.kpfx", kpfx);
-        d_ktile = c_.up("E.ktile", ktile);
-        uint64_t* d_kseg = c_.up("E.kseg", kseg);
+        d_kpfx = c_.up(EP + "kpfx", kpfx);
+        d_ktile = c_.up(EP + "ktile", ktile);
+        uint64_t* d_kseg = c_.up(EP + "kseg", kseg);
         const std::vector<uint64_t> kstr = stft_strips(kpfx);
-        uint64_t* d_kstr = c_.up("E.kstrip", kstr);
-        uint64_t* d_ksrc = c_.up("E.ksrc", ksrc);
-        float* d_kgain = c_.up("E.kgain", kgain);
+        uint64_t* d_kstr = c_.up(EP + "kstrip", kstr);
+        uint64_t* d_ksrc = c_.up(EP + "ksrc", ksrc);
+        float* d_kgain = c_.up(EP + "kgain", kgain);
         std::vector<int> kid((size_t)NK);
         for (int k = 0; k < NK; k++) kid[(size_t)k] = k;
-        d_kid = c_.up("E.kid", kid);
+        d_kid = c_.up(EP + "kid", kid);
         FftTables& t8 = d_.tables(KFS, true);
         mags8 = c_.dev<float>("E.mags8", total8 * STRIDE8);
         // uploads above were queued on the main stream: order the key stream after them
@@ -1341,9 +1376,9 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
                                                  (((uint64_t)kh.nb + KH_TILE_BINS - 1) / KH_TILE_BINS));
                     at.push_back(at.back() + (F8 + KH_APPLY_FRAMES - 1) / KH_APPLY_FRAMES);
                 }
-                uint64_t* d_moff = c_.up("E.kh_off", moff);
-                uint64_t* d_mt = c_.up("E.kh_mt", mt);
-                uint64_t* d_at = c_.up("E.kh_at", at);
+                uint64_t* d_moff = c_.up(EP + "kh_off", moff);
+                uint64_t* d_mt = c_.up(EP + "kh_mt", mt);
+                uint64_t* d_at = c_.up(EP + "kh_at", at);
                 float* d_kmask = c_.dev<float>("E.kh_mask", std::max<uint64_t>(moff.back(), 1));
                 // the uploads are on the main stream
                 kt.mark(9);
@@ -1383,7 +1418,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
             hp.p = sd_clampf(cfg_.key_hpcp_mag_power, 0.05f, 1.0f);
             std::vector<HarmEntry> ht =
                 harm_table(B8, sr_, KFS, cfg_.soft_mapping_sigma, hp.hmax, cfg_.key_hpcp_harmonic_decay);
-            HarmEntry* d_ht = c_.up("E.harm", ht);
+            HarmEntry* d_ht = c_.up(EP + "harm", ht);
             // the table upload is queued on the main stream: order the key stream after it
             kt.mark(10);
             SDSP_HIP_CHECK(hipStreamWaitEvent(st2, kt.ev[10], 0));
@@ -1391,7 +1426,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
                 std::vector<uint64_t> kspfx(1, 0);  // mask segments (prefix checkpoints) per key track
                 for (int k = 0; k < NK; k++)
                     kspfx.push_back(kspfx.back() + (kpfx[(size_t)k + 1] - kpfx[(size_t)k] + KEY_CKPT_SEG - 1) / KEY_CKPT_SEG);
-                uint64_t* d_kspfx = c_.up("E.kseg_pfx", kspfx);
+                uint64_t* d_kspfx = c_.up(EP + "kseg_pfx", kspfx);
                 float* d_ckpt = c_.dev<float>("E.kckpt", kspfx.back() * KEY_CKPT_STRIDE);
                 kt.mark(11);  // the segment prefix upload is on the main stream
                 SDSP_HIP_CHECK(hipStreamWaitEvent(st2, kt.ev[11], 0));
@@ -1407,7 +1442,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         SDSP_HIP_CHECK(hipGetLastError());
         std::vector<float> tpl(576);
         key_templates(tpl.data());
-        d_tpl = c_.up("E.tpl", tpl);
+        d_tpl = c_.up(EP + "tpl", tpl);
         kp.weighting = cfg_.enable_key_frame_weighting;
         kp.min_tonal = cfg_.key_min_tonalness;
         kp.tonal_pow = cfg_.key_tonalness_power;
@@ -1439,7 +1474,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         float* d_cs = c_.dev<float>("E.chroma_s", total8 * 12);
         float* d_w = c_.dev<float>("E.weights", total8);
         float* d_sscr = c_.dev<float>("E.segscr", std::max<uint64_t>(kseg.back(), 1));
-        d_kout = c_.dev<KeyOut>("E.kout", (size_t)NK);
+        d_kout = c_.dev<KeyOut>(EP + "kout", (size_t)NK);
         // the template upload above is on the main stream too
         kt.mark(8);
         SDSP_HIP_CHECK(hipStreamWaitEvent(st2, kt.ev[8], 0));
@@ -1826,7 +1861,16 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     SDSP_HIP_CHECK(hipGetLastError());
     tm.mark(5);
     tm.mark(6);
-    if (NK > 0) {  // join the key stream
+    // the previous sub-batch's key results (its key work ran ahead of this one's on the key stream)
+    finish_key(res);
+    const bool beat_sync = cfg_.enable_key_beat_synchronous && !cfg_.enable_key_log_frequency;
+    const bool defer_key = NK > 0 && !beat_sync && !serial_streams && std::getenv("SDSP_NO_KEY_DEFER") == nullptr;
+    if (defer_key) {
+        key_pending_.reset(new KeyPending());
+        key_pending_->kt = std::move(ktp);
+        key_pending_->d_kout = d_kout;
+        for (int k = 0; k < NK; k++) key_pending_->at.push_back((size_t)idx[(size_t)R[(size_t)K[(size_t)k]]]);
+    } else if (NK > 0) {  // join the key stream
         SDSP_HIP_CHECK(hipStreamWaitEvent(st, kt.ev[2], 0));
         kout = c_.down(d_kout, (size_t)NK);
         htr("E join");
@@ -1848,7 +1892,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     htr("D down");
     // beat-synchronous chroma (src/lib.rs:1121-1133): for key tracks with a non-empty beat grid the
     // chroma rows are the beat intervals' mean frame chroma; the key vote is re-run on them
-    if (cfg_.enable_key_beat_synchronous && !cfg_.enable_key_log_frequency && NK > 0) {
+    if (beat_sync && NK > 0) {
         std::vector<int> sel, sel_id;
         std::vector<uint64_t> sb_off, rpfx(1, 0), sseg(1, 0);
         for (int k = 0; k < NK; k++) {
@@ -1935,7 +1979,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
             }
         }
     }
-    for (int k = 0; k < NK; k++) {
+    for (int k = 0; k < NK && !defer_key; k++) {
         TrackRes& r = res[(size_t)idx[(size_t)R[(size_t)K[(size_t)k]]]];
         const KeyOut& ko = kout[(size_t)k];
         if (!ko.ok) continue;

@@ -32,7 +32,12 @@ struct DevBuf {
     size_t bytes = 0;
     void ensure(size_t n) {
         if (n <= bytes) return;
-        if (p) SDSP_HIP_CHECK(hipFree(p));
+        // the old buffer may still be read by work queued on another stream (the key stream's
+        // tail runs under the next sub-batch): drain the device before it is released
+        if (p) {
+            SDSP_HIP_CHECK(hipDeviceSynchronize());
+            SDSP_HIP_CHECK(hipFree(p));
+        }
         p = nullptr;
         bytes = 0;
         const size_t want = n + n / 8 + 4096;
