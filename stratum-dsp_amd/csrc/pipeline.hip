@@ -621,8 +621,8 @@ class Pipeline {
 
     void sub_batch(const float* d_samples, const std::vector<uint64_t>& in_off, const std::vector<uint64_t>& n_raw,
                    const std::vector<int>& idx, std::vector<TrackRes>& res);
-    // The key results of a sub-batch are joined late: its key-stream tail (mask, HPCP, vote) runs
-    // under the next sub-batch's tempo path instead of holding it back.  Uploads read by the key
+    // SDSP_KEY_DEFER=1: the key results of a sub-batch are joined late, so its key-stream tail
+    // (mask, HPCP, vote) runs under the next sub-batch's tempo path.  Uploads read by the key
     // stream and the key output live in per-parity buffers (E0.*, E1.*) for that.
     struct KeyPending {
         std::unique_ptr<Timers> kt;
@@ -1864,7 +1864,11 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     // the previous sub-batch's key results (its key work ran ahead of this one's on the key stream)
     finish_key(res);
     const bool beat_sync = cfg_.enable_key_beat_synchronous && !cfg_.enable_key_log_frequency;
-    const bool defer_key = NK > 0 && !beat_sync && !serial_streams && std::getenv("SDSP_NO_KEY_DEFER") == nullptr;
+    // SDSP_KEY_DEFER=1 (experiment): join this sub-batch's key stream one sub-batch late.  Both
+    // streams then stay busy 95 % of the span instead of 85 %, but the step does not get shorter
+    // (1,918-1,953 vs 1,927-1,933 tracks/s, alternating runs on one box): the chip is saturated,
+    // and the extra overlap only slows each kernel down.
+    const bool defer_key = NK > 0 && !beat_sync && !serial_streams && std::getenv("SDSP_KEY_DEFER") != nullptr;
     if (defer_key) {
         key_pending_.reset(new KeyPending());
         key_pending_->kt = std::move(ktp);

@@ -10,8 +10,8 @@
   SDSP_KEY_FUSE=1) against the default key path (k_mask_r in place, then k_hpcp): identical
   results, on key spectrograms of 1 .. 300 frames around the 16-frame checkpoint segments and the
   256-frame tiles, and on 3-min tracks; with peaks_per_frame 8 / 16 / 32 list capacities.
-* The key stream's late join (a sub-batch's key results are read after the next sub-batch's tempo
-  path is queued) against its control SDSP_NO_KEY_DEFER=1, on a batch split into several
+* The key stream's late join (SDSP_KEY_DEFER=1: a sub-batch's key results are read after the next
+  sub-batch's tempo path is queued) against the default join, on a batch split into several
   sub-batches by a small HBM budget, with a sample checked against the oracle.
 * Config-2/-5 shapes at a larger batch than the parity tests: 3-min tracks checked against the
   oracle on a sample.
@@ -156,9 +156,9 @@ def test_key_defer_across_sub_batches(monkeypatch):
     lens = [44100 * 30 + 37 * k for k in range(36)] + [5000, 44100 * 61]
     buf, offs, lens = _device_tracks(lens, 1700)
     monkeypatch.setenv("SDSP_HBM_BUDGET_GB", "1")  # several sub-batches
-    monkeypatch.setenv("SDSP_NO_KEY_DEFER", "1")
+    monkeypatch.delenv("SDSP_KEY_DEFER", raising=False)
     ctrl = sdsp.analyze_batch_device(buf.ptr, offs, lens)
-    monkeypatch.delenv("SDSP_NO_KEY_DEFER", raising=False)
+    monkeypatch.setenv("SDSP_KEY_DEFER", "1")
     got = sdsp.analyze_batch_device(buf.ptr, offs, lens)
     for i, (a, b) in enumerate(zip(got, ctrl)):
         assert _strip(a) == _strip(b), (i, int(lens[i]))
