@@ -661,7 +661,7 @@ __global__ __launch_bounds__(256) void k_key_vote(const int* __restrict__ tracks
                                                   const float* __restrict__ energy, float* __restrict__ chroma_s,
                                                   float* __restrict__ weights, float* __restrict__ seg_scratch,
                                                   const uint64_t* __restrict__ seg_off, const float* __restrict__ tmpl,
-                                                  KeyParams P, KeyOut* __restrict__ out) {
+                                                  KeyParams P, KeyOut* __restrict__ out, KeyDbg* __restrict__ dbg) {
     __shared__ int hist[256];
     __shared__ int misc[4];
     __shared__ int redi[8];
@@ -778,6 +778,39 @@ __global__ __launch_bounds__(256) void k_key_vote(const int* __restrict__ tracks
     __syncthreads();
     const bool use_w = use_w_s;
     const int toff = P.tset == 1 ? 24 : 0;  // template rows of the selected set
+    if (dbg) {  // debug_track_id: weighted pitch-class sums over the slice, in frame order (src/lib.rs:1473-1491)
+        if (threadIdx.x < 12) {
+            float a = 0.0f;
+            for (int64_t f = 0; f < F; f++) {
+                const float wt = use_w ? w[f] : 1.0f;
+                if (wt <= 0.0f) continue;
+                a += wt * cs[f * 12 + threadIdx.x];
+            }
+            acc[threadIdx.x] = a;
+        }
+        if (threadIdx.x == 32) {
+            int u = 0;
+            for (int64_t f = 0; f < F; f++) u += (use_w ? w[f] : 1.0f) > 0.0f;
+            dbg[it].frames = (int)F;
+            dbg[it].used = u;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            float sa = 0.0f;
+            for (int k = 0; k < 12; k++) sa += acc[k];
+            for (int k = 0; k < 12; k++) dbg[it].agg[k] = sa > 1e-12f ? acc[k] / sa : acc[k];
+        }
+        __syncthreads();
+    }
+    // the final score table for the debug dump (KeyDetectionResult::top_keys)
+    auto put_dbg = [&](const float* sorted, const int* order, int key) {
+        if (!dbg) return;
+        for (int k = 0; k < 24; k++) {
+            dbg[it].tab[k] = sorted[k];
+            dbg[it].order[k] = order[k];
+        }
+        dbg[it].key = key;
+    };
     auto wsd = [&](int64_t f0, int64_t n, int row) {  // weighted_sum_dot, detector.rs:984-1001
         float a = 0.0f;
         const float* t = tpl[row];
@@ -838,6 +871,7 @@ __global__ __launch_bounds__(256) void k_key_vote(const int* __restrict__ tracks
             float conf = sorted[0] > 0.0f ? sd_clampf((sorted[0] - sorted[1]) / sorted[0], 0.0f, 1.0f) : 0.0f;
             if (P.mh_on) mode_heuristic(sorted, order, acc + 24, acc[36], P, &key, &conf);
             write_out(key, conf, clarity_of(sorted), used_segments);
+            put_dbg(sorted, order, key);
         }
     };
     if (P.ensemble) {  // detect_key_ensemble (detector.rs:881-978), src/lib.rs:1289-1299
@@ -859,6 +893,7 @@ __global__ __launch_bounds__(256) void k_key_vote(const int* __restrict__ tracks
             float conf;
             from_table(comb, sorted, order, &conf);
             write_out(order[0], conf, clarity_of(sorted), 0);
+            put_dbg(sorted, order, order[0]);
         }
         return;
     }
@@ -980,6 +1015,7 @@ __global__ __launch_bounds__(256) void k_key_vote(const int* __restrict__ tracks
         float conf;
         from_table(tab, sorted, order, &conf);
         write_out(order[0], conf, clarity_of(sorted), used);
+        put_dbg(sorted, order, order[0]);
     }
 }
 
@@ -1058,10 +1094,10 @@ void launch_hpcp_masked(const float* mags, int stride, const uint64_t* frame_pfx
 }
 void launch_key_vote(const int* tracks, int n_items, const uint64_t* frame_pfx, float* chroma_raw,
                      const float* energy, float* chroma_s, float* weights, float* seg_scratch, const uint64_t* seg_off,
-                     const float* tmpl, const KeyParams& P, KeyOut* out, hipStream_t st) {
+                     const float* tmpl, const KeyParams& P, KeyOut* out, hipStream_t st, KeyDbg* dbg) {
     if (n_items == 0) return;
     hipLaunchKernelGGL(k_key_vote, dim3(n_items), dim3(256), 0, st, tracks, n_items, frame_pfx, chroma_raw, energy,
-                       chroma_s, weights, seg_scratch, seg_off, tmpl, P, out);
+                       chroma_s, weights, seg_scratch, seg_off, tmpl, P, out, dbg);
 }
 
 }  // namespace sdsp

@@ -560,10 +560,13 @@ __global__ __launch_bounds__(64) void k_multires(const int* __restrict__ tracks,
                                                  const TempoEst* __restrict__ base_est,
                                                  const float* __restrict__ nov512, const uint64_t* __restrict__ fpfx512,
                                                  MrParams P, TempoEst* __restrict__ mr_est, int* __restrict__ used,
-                                                 float* __restrict__ final_bpm, float* __restrict__ final_conf) {
+                                                 float* __restrict__ final_bpm, float* __restrict__ final_conf,
+                                                 MrDbg* __restrict__ dbg) {
     SDSP_LATENCY_CRITICAL();
     __shared__ float fam_bpm[5], fam_sup[5], fam_align[5];
     __shared__ int n_fam_s, do_fam_s;
+    __shared__ int fam_lab[5];
+    MrDbg dr{};  // thread 0's debug record (dbg only)
     __shared__ float best_bpm_s, best_score_s, second_s;
     __shared__ int ok_s;
     const int i = blockIdx.x;
@@ -687,7 +690,10 @@ __global__ __launch_bounds__(64) void k_multires(const int* __restrict__ tracks,
                     total_support(best.bpm, &sb, &ab);
                     total_support(half, &sh, &ah);
                     const float ratio = sb > 0.0f ? sh / sb : 0.0f;
-                    if (ah >= 3 && sh > 0.0f && sb > 0.0f && ratio >= 0.45f) best = {half, sh};
+                    if (ah >= 3 && sh > 0.0f && sb > 0.0f && ratio >= 0.45f) {
+                        dr.fd = 1, dr.fd_from = best.bpm, dr.fd_to = half, dr.fd_ratio = ratio, dr.fd_a0 = ab, dr.fd_a1 = ah;
+                        best = {half, sh};
+                    }
                 }
             }
             if (best.bpm <= 80.0f) {
@@ -698,7 +704,10 @@ __global__ __launch_bounds__(64) void k_multires(const int* __restrict__ tracks,
                     total_support(best.bpm, &sb, &ab);
                     total_support(dbl, &sd, &ad);
                     const float ratio = sb > 0.0f ? sd / sb : 0.0f;
-                    if (ad >= 2 && sd > 0.0f && sb > 0.0f && ratio >= 0.55f) best = {dbl, sd};
+                    if (ad >= 2 && sd > 0.0f && sb > 0.0f && ratio >= 0.55f) {
+                        dr.fu = 1, dr.fu_from = best.bpm, dr.fu_to = dbl, dr.fu_ratio = ratio, dr.fu_a0 = ab, dr.fu_a1 = ad;
+                        best = {dbl, sd};
+                    }
                 }
             }
             // triplet-family candidates (alignment computed by the whole wave below)
@@ -715,6 +724,7 @@ __global__ __launch_bounds__(64) void k_multires(const int* __restrict__ tracks,
                     if (ag < 2 || sup <= 0.0f) continue;
                     fam_bpm[nf] = bpm;
                     fam_sup[nf] = sup;
+                    fam_lab[nf] = k;
                     nf++;
                 }
             }
@@ -783,6 +793,13 @@ __global__ __launch_bounds__(64) void k_multires(const int* __restrict__ tracks,
             fam_bpm[0 + 4] = fam_bpm[ch];  // stash chosen
             fam_sup[0 + 4] = fam_sup[ch];
             fam_align[4] = fam_align[ch];
+            if (dbg) {  // current.support (total_support of the best) and the chosen's, over the best family support
+                const float sc = lookup_c(L256, best_bpm_s, tol) + lookup_c(L512, best_bpm_s, tol) +
+                                 lookup_c(L1024, best_bpm_s, tol);
+                dr.tf_sup0 = sc / bs;
+                dr.tf_sup1 = fam_sup[ch] / bs;
+                dr.tf_label = fam_lab[ch];
+            }
         }
     } else if (threadIdx.x == 0) {
         do_fam_s = 0;
@@ -792,6 +809,7 @@ __global__ __launch_bounds__(64) void k_multires(const int* __restrict__ tracks,
         cur_align = beat_contrast_wave(nov, nn, P.sr, P.hop512, best_bpm_s, nov_total, wm);
         if (threadIdx.x == 0) {
             if (sd_absf(fam_bpm[4] - best_bpm_s) > 0.75f && fam_align[4] >= cur_align + 0.40f) {
+                dr.tf = 1, dr.tf_from = best_bpm_s, dr.tf_to = fam_bpm[4], dr.tf_al0 = cur_align, dr.tf_al1 = fam_align[4];
                 best_bpm_s = fam_bpm[4];
                 best_score_s = fam_sup[4];
             }
@@ -821,6 +839,10 @@ __global__ __launch_bounds__(64) void k_multires(const int* __restrict__ tracks,
         if (better) {
             final_bpm[trk] = bb;
             final_conf[trk] = conf;
+        }
+        if (dbg) {
+            dr.rel = rel, dr.fam = fam, dr.forbid = forbid, dr.better = better;
+            dbg[i] = dr;
         }
     }
 }
@@ -853,7 +875,7 @@ void launch_tempo_select(int n_items, const int* active, const float* fft_bpm, c
 void launch_multires(const int* tracks, int n_items, const float* c256, const int* n256, const float* c512,
                      const int* n512, const float* c1024, const int* n1024, int cap256, int cap512, int cap1024,
                      const TempoEst* base_est, const float* nov512, const uint64_t* fpfx512, const MrParams& P,
-                     TempoEst* mr_est, int* used, float* final_bpm, float* final_conf, hipStream_t st) {
+                     TempoEst* mr_est, int* used, float* final_bpm, float* final_conf, hipStream_t st, MrDbg* dbg) {
     if (n_items == 0) return;
     MrParams Q = P;
     Q.wm_cap = MR_WM_CAP;
@@ -861,7 +883,7 @@ void launch_multires(const int* tracks, int n_items, const float* c256, const in
     (void)hipFuncSetAttribute((const void*)k_multires, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(k_multires, dim3(n_items), dim3(64), lds, st, tracks, n_items, c256, n256, c512, n512, c1024,
                        n1024, cap256, cap512, cap1024, base_est, nov512, fpfx512, Q, mr_est, used, final_bpm,
-                       final_conf);
+                       final_conf, dbg);
 }
 
 }  // namespace sdsp

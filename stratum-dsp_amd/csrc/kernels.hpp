@@ -84,6 +84,30 @@ struct MrParams {
     int wm_cap;  // set by launch_multires: novelty window maxima kept in LDS up to this many frames
 };
 
+// debug_track_id diagnostics (src/lib.rs:461-487, 547-573, multi_resolution.rs:707-860): what
+// k_multires decided, written only when a record buffer is passed
+struct MrDbg {
+    int fd, fu, tf;                   // fold-down / fold-up / triplet-family switch taken
+    float fd_from, fd_to, fd_ratio;   // fold-down: best -> half, support ratio
+    int fd_a0, fd_a1;                 //   hop agreement before / after
+    float fu_from, fu_to, fu_ratio;   // fold-up: best -> double
+    int fu_a0, fu_a1;
+    float tf_from, tf_to;             // triplet family: current -> chosen
+    float tf_sup0, tf_sup1;           //   support / best family support, current and chosen
+    float tf_al0, tf_al1;             //   beat-contrast alignment, current and chosen
+    int tf_label;                     //   family factor index: T, 3/2, 2/3, 4/3, 3/4
+    float rel;                        // acceptance (src/lib.rs:515-545)
+    int fam, forbid, better;
+};
+// k_key_vote's final score table and the weighted pitch-class summary (src/lib.rs:1471-1538)
+struct KeyDbg {
+    float tab[24];  // scores, descending
+    int order[24];  // key index (0-11 major, 12-23 minor) of each
+    int key;        // chosen key
+    float agg[12];  // weighted pitch-class sums over the slice, normalised by their sum
+    int frames, used;
+};
+
 // ---- k_beat ----
 struct BeatOut {
     int n_beats, n_down;
@@ -250,7 +274,7 @@ void launch_tempo_select(int n_items, const int* active, const float* fft_bpm, c
 void launch_multires(const int* tracks, int n_items, const float* c256, const int* n256, const float* c512,
                      const int* n512, const float* c1024, const int* n1024, int cap256, int cap512, int cap1024,
                      const TempoEst* base_est, const float* nov512, const uint64_t* fpfx512, const MrParams& P,
-                     TempoEst* mr_est, int* used, float* final_bpm, float* final_conf, hipStream_t st);
+                     TempoEst* mr_est, int* used, float* final_bpm, float* final_conf, hipStream_t st, MrDbg* dbg = nullptr);
 void launch_beat(const int* tracks, int n_items, const uint32_t* onsets, const uint64_t* on_off, const int* on_n,
                  uint32_t sr, const float* bpm, const float* conf, float* scratch, const uint64_t* beat_off,
                  const int* beat_cap, float* beats, float* downs, BeatOut* out, hipStream_t st);
@@ -291,7 +315,7 @@ void launch_hpcp_masked(const float* mags, int stride, const uint64_t* frame_pfx
                         const HpcpParams& P, const HarmEntry* harm, float* chroma, float* energy, hipStream_t st);
 void launch_key_vote(const int* tracks, int n_items, const uint64_t* frame_pfx, float* chroma_raw,
                      const float* energy, float* chroma_s, float* weights, float* seg_scratch, const uint64_t* seg_off,
-                     const float* tmpl, const KeyParams& P, KeyOut* out, hipStream_t st);
+                     const float* tmpl, const KeyParams& P, KeyOut* out, hipStream_t st, KeyDbg* dbg = nullptr);
 void launch_synth(float* out, uint64_t n_tracks, uint64_t len, uint32_t sr, const float* bpm, const int* key,
                   uint64_t seed0, hipStream_t st);
 void launch_synth_normalize(float* out, uint64_t n_tracks, uint64_t len, unsigned int* peak_bits, hipStream_t st);

@@ -594,6 +594,194 @@ struct TempoPassOut {
 }  // namespace
 
 // ---------------------------------------------------------------------------------------
+// debug_track_id dumps (src/lib.rs:461-487, 547-573, 1471-1538; multi_resolution.rs:304-403,
+// 707-745, 845-857): the reference's eprintln! diagnostics, printed per analysed track in batch
+// order from what the kernels computed (candidate lists, estimates, MrDbg / KeyDbg records).
+struct Cand4 {
+    float bpm, score, fft, acf;
+};
+struct TrackDbg {
+    bool base = false;  // base tempogram estimate available (multi-resolution path)
+    TempoEst est{};
+    std::vector<Cand4> base_c;
+    bool mr = false;  // escalated and every hop's tempogram succeeded
+    std::vector<Cand4> c256, c512, c1024;
+    TempoEst mr_est{};
+    MrDbg md{};
+    bool key = false;
+    KeyOut ko{};
+    KeyDbg kd{};
+    float tuning = 0.0f;
+};
+const char* tf_str(bool b) { return b ? "true" : "false"; }
+// cand_support (src/lib.rs:420-431) and lookup_nearest (multi_resolution.rs:281-292)
+float cand_support(const std::vector<Cand4>& c, float bpm, float tol) {
+    float b = 0.0f;
+    for (const Cand4& x : c)
+        if (sd_absf(x.bpm - bpm) <= tol) b = sd_maxf(b, x.score);
+    return b;
+}
+float lookup_nearest_h(const std::vector<Cand4>& c, float bpm, float tol) {
+    float bd = SD_INF_F, bs = 0.0f;
+    for (const Cand4& x : c) {
+        const float d = sd_absf(x.bpm - bpm);
+        if (d <= tol && d < bd) {
+            bd = d;
+            bs = x.score;
+        }
+    }
+    return bs;
+}
+std::string key_str(int key) {  // Key::name
+    char b[8];
+    sdsp_key_name(key < 12 ? 0 : 1, (uint32_t)(key % 12), b, sizeof b);
+    return b;
+}
+void print_debug(const sdsp_config& c, const TrackDbg& d) {
+    const unsigned id = c.debug_track_id;
+    auto gt = [&]() {
+        if (c.has_debug_gt_bpm) std::fprintf(stderr, "GT bpm: %.3f\n", (double)c.debug_gt_bpm);
+    };
+    const float tol = sd_maxf(2.0f, c.bpm_resolution);
+    if (d.base) {
+        const TempoEst& b = d.est;
+        const float s_base = cand_support(d.base_c, b.bpm, tol), s_2x = cand_support(d.base_c, b.bpm * 2.0f, tol),
+                    s_half = cand_support(d.base_c, b.bpm * 0.5f, tol);
+        const bool fam = (s_2x > 0.0f && s_2x >= s_base * 0.90f) || (s_half > 0.0f && s_half >= s_base * 0.90f);
+        const bool fold = b.bpm * 2.0f >= 170.0f && b.bpm * 2.0f <= 200.0f;
+        const bool weak = b.agree == 0 || b.conf < 0.06f;
+        std::fprintf(stderr, "\n=== DEBUG base tempogram (track_id=%u) ===\n", id);
+        gt();
+        std::fprintf(stderr, "base_est: bpm=%.2f conf=%.4f agree=%d (trap_low=%s trap_high=%s ambiguous=%s)\n",
+                     (double)b.bpm, (double)b.conf, b.agree, tf_str(b.trap_low), tf_str(b.trap_high), tf_str(b.ambiguous));
+        std::fprintf(stderr,
+                     "ambiguity signals: family_competes=%s (s_base=%.4f s_2x=%.4f s_half=%.4f) weak_base=%s "
+                     "fold_into_trap=%s\n",
+                     tf_str(fam), (double)s_base, (double)s_2x, (double)s_half, tf_str(weak), tf_str(fold));
+        if (!b.ambiguous) std::fprintf(stderr, "NOTE: multi-res not run (outside trap zones).\n");
+    }
+    if (d.mr) {
+        const size_t top_n = std::max<uint64_t>(c.debug_top_n, 1);
+        std::fprintf(stderr, "\n=== DEBUG multi-res (track_id=%u) ===\n", id);
+        gt();
+        auto top = [&](const char* label, const std::vector<Cand4>& v) {
+            std::fprintf(stderr, "%s top-%zu:\n", label, top_n);
+            for (size_t k = 0; k < v.size() && k < top_n; k++)
+                std::fprintf(stderr, "  bpm=%7.2f score=%.4f\n", (double)v[k].bpm, (double)v[k].score);
+        };
+        top("hop=256", d.c256);
+        top("hop=512", d.c512);
+        top("hop=1024", d.c1024);
+        if (c.has_debug_gt_bpm) {
+            const float g = c.debug_gt_bpm;
+            const float t512 = lookup_nearest_h(d.c512, g, tol), t256 = lookup_nearest_h(d.c256, g, tol),
+                        t1024 = lookup_nearest_h(d.c1024, g, tol);
+            const float d512 = lookup_nearest_h(d.c512, g * 2.0f, tol), d256 = lookup_nearest_h(d.c256, g * 2.0f, tol),
+                        d1024 = lookup_nearest_h(d.c1024, g * 2.0f, tol);
+            const float h512 = lookup_nearest_h(d.c512, g * 0.5f, tol), h256 = lookup_nearest_h(d.c256, g * 0.5f, tol),
+                        h1024 = lookup_nearest_h(d.c1024, g * 0.5f, tol);
+            std::fprintf(stderr, "Support near GT / family (lookup tol=%.2f):\n", (double)tol);
+            std::fprintf(stderr, "  T     @512=%.4f @256=%.4f @1024=%.4f\n", (double)t512, (double)t256, (double)t1024);
+            std::fprintf(stderr, "  2T    @512=%.4f @256=%.4f @1024=%.4f\n", (double)d512, (double)d256, (double)d1024);
+            std::fprintf(stderr, "  T/2   @512=%.4f @256=%.4f @1024=%.4f\n", (double)h512, (double)h256, (double)h1024);
+            const float w512 = c.tempogram_multi_res_w512, w256 = c.tempogram_multi_res_w256,
+                        w1024 = c.tempogram_multi_res_w1024, dt = c.tempogram_multi_res_double_time_512_factor;
+            const float h_t = w512 * t512 + w256 * t256 + w1024 * (t1024 + c.tempogram_multi_res_structural_discount * d1024);
+            float h_2t = w512 * (dt * t512 + (1.0f - dt) * d512) + w256 * d256 + w1024 * d1024;
+            float h_h = w512 * (dt * t512 + (1.0f - dt) * h512) + w256 * h256 + w1024 * h1024;
+            const float eps = 1e-6f;
+            const float r2 = (d256 + eps) / (t256 + eps), rh = (h1024 + eps) / (t1024 + eps);
+            if (r2 < 1.10f) h_2t *= 0.75f;
+            if (r2 < 1.00f) h_2t *= 0.75f;
+            if (rh < 1.10f) h_h *= 0.75f;
+            if (rh < 1.00f) h_h *= 0.75f;
+            struct L {
+                float bpm, s;
+                const char* tag;
+            };
+            std::vector<L> loc = {{g, h_t, "T"}, {g * 2.0f, h_2t, "2T"}, {g * 0.5f, h_h, "T/2"}};
+            std::vector<L> keep;
+            for (const L& l : loc)
+                if (l.bpm >= c.min_bpm && l.bpm <= c.max_bpm) keep.push_back(l);
+            for (L& l : keep) {
+                if (l.bpm > 210.0f) l.s *= 0.80f;
+                else if (l.bpm > 180.0f) l.s *= 0.90f;
+                else if (l.bpm < 60.0f) l.s *= 0.92f;
+            }
+            std::stable_sort(keep.begin(), keep.end(), [](const L& a, const L& b) { return a.s > b.s; });
+            std::fprintf(stderr, "Fusion scores (T anchored at GT, after guardrails+prior):\n");
+            for (const L& l : keep) std::fprintf(stderr, "  %3s bpm=%7.2f score=%.4f\n", l.tag, (double)l.bpm, (double)l.s);
+            if (keep.size() >= 2)
+                std::fprintf(stderr, "  margin(best-second)=%.4f (threshold=%.4f)\n", (double)(keep[0].s - keep[1].s),
+                             (double)c.tempogram_multi_res_margin_threshold);
+            std::fprintf(stderr, "  ratio_2T_256=%.3f ratio_half_1024=%.3f (guardrails)\n", (double)r2, (double)rh);
+        }
+        const MrDbg& m = d.md;
+        if (m.fd)
+            std::fprintf(stderr, "DEBUG fold-down (track_id=%u): %.2f -> %.2f (support ratio %.3f, agree %d->%d).\n", id,
+                         (double)m.fd_from, (double)m.fd_to, (double)m.fd_ratio, m.fd_a0, m.fd_a1);
+        if (m.fu)
+            std::fprintf(stderr, "DEBUG fold-up (track_id=%u): %.2f -> %.2f (support ratio %.3f, agree %d->%d).\n", id,
+                         (double)m.fu_from, (double)m.fu_to, (double)m.fu_ratio, m.fu_a0, m.fu_a1);
+        if (m.tf) {
+            static const char* lab[5] = {"T", "3/2", "2/3", "4/3", "3/4"};
+            std::fprintf(stderr,
+                         "DEBUG triplet-family (track_id=%u): %.2f -> %.2f (%s, support %.3f->%.3f, align %.3f->%.3f)\n",
+                         id, (double)m.tf_from, (double)m.tf_to, lab[m.tf_label < 0 || m.tf_label > 4 ? 0 : m.tf_label],
+                         (double)m.tf_sup0, (double)m.tf_sup1, (double)m.tf_al0, (double)m.tf_al1);
+        }
+        std::fprintf(stderr, "\n=== DEBUG multi-res decision (track_id=%u) ===\n", id);
+        gt();
+        std::fprintf(stderr, "base_est: bpm=%.2f conf=%.4f agree=%d\n", (double)d.est.bpm, (double)d.est.conf, d.est.agree);
+        std::fprintf(stderr, "mr_est:   bpm=%.2f conf=%.4f agree=%d\n", (double)d.mr_est.bpm, (double)d.mr_est.conf,
+                     d.mr_est.agree);
+        std::fprintf(stderr, "ambiguous(trap_low||trap_high)=%s\n", tf_str(d.est.ambiguous));
+        std::fprintf(stderr, "rel=%.3f family_related=%s forbid_promote_high=%s\n", (double)m.rel, tf_str(m.fam),
+                     tf_str(m.forbid));
+        std::fprintf(stderr, "mr_better=%s used_mr=%s\n", tf_str(m.better), tf_str(m.better));
+    }
+    if (d.key) {
+        const KeyDbg& k = d.kd;
+        std::fprintf(stderr, "\n=== DEBUG key (track_id=%u) ===\n", id);
+        std::fprintf(stderr,
+                     "key=%s conf=%.4f clarity=%.4f frames=%d used_frames=%d soft_mapping=%s sigma=%.3f harmonic_mask=%s "
+                     "mask_p=%.2f tuning=%.4f time_smooth=%s margin=%llu edge_trim=%s trim_frac=%.2f\n",
+                     key_str(d.ko.mode * 12 + d.ko.tonic).c_str(), (double)d.ko.conf, (double)d.ko.clarity, k.frames, k.used,
+                     tf_str(c.soft_chroma_mapping), (double)c.soft_mapping_sigma, tf_str(c.enable_key_harmonic_mask),
+                     (double)c.key_harmonic_mask_power, (double)d.tuning, tf_str(c.enable_key_spectrogram_time_smoothing),
+                     (unsigned long long)c.key_spectrogram_smooth_margin, tf_str(c.enable_key_edge_trim),
+                     (double)c.key_edge_trim_fraction);
+        // top_keys: the first three of the final table; the chosen key replaces the third when it is
+        // not among them (detector.rs:506-510)
+        std::vector<std::pair<int, float>> tk;
+        for (int q = 0; q < 3; q++) tk.push_back({k.order[q], k.tab[q]});
+        bool in = false;
+        for (const auto& e : tk) in |= e.first == k.key;
+        if (!in)
+            for (int q = 3; q < 24; q++)
+                if (k.order[q] == k.key) tk.back() = {k.key, k.tab[q]};
+        std::string line;
+        for (size_t q = 0; q < tk.size(); q++) {
+            char b[64];
+            std::snprintf(b, sizeof b, "%s%s:%.4f", q ? ", " : "", key_str(tk[q].first).c_str(), (double)tk[q].second);
+            line += b;
+        }
+        std::fprintf(stderr, "top_keys: %s\n", line.c_str());
+        static const char* notes[12] = {"C", "C#", "D", "D#", "E", "F", "F#", "G", "G#", "A", "A#", "B"};
+        std::vector<int> pcs(12);
+        for (int q = 0; q < 12; q++) pcs[q] = q;
+        std::stable_sort(pcs.begin(), pcs.end(), [&](int a, int b) { return k.agg[a] > k.agg[b]; });
+        line.clear();
+        for (int q = 0; q < 6; q++) {
+            char b[64];
+            std::snprintf(b, sizeof b, "%s%s:%.3f", q ? ", " : "", notes[pcs[q]], (double)k.agg[pcs[q]]);
+            line += b;
+        }
+        std::fprintf(stderr, "top_pitch_classes(weighted): %s\n", line.c_str());
+    }
+}
+
+// ---------------------------------------------------------------------------------------
 class Pipeline {
    public:
     Pipeline(DeviceCtx& d, const sdsp_config& cfg, uint32_t sr, int stages = SDSP_STAGES_FULL)
@@ -627,6 +815,7 @@ class Pipeline {
     struct KeyPending {
         std::unique_ptr<Timers> kt;
         KeyOut* d_kout = nullptr;
+    KeyDbg* d_kdbg = nullptr;
         std::vector<size_t> at;  // result slot of each key track
     };
     std::unique_ptr<KeyPending> key_pending_;
@@ -1232,6 +1421,8 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     }
     const int NR = (int)R.size();
     if (NR == 0) return;
+    const bool dbg_on = cfg_.has_debug_track_id != 0;  // debug_track_id dumps (print_debug)
+    std::vector<TrackDbg> tdbg(dbg_on ? (size_t)NR : 0);
     // ---------------- B: base tempo pass (hop = config hop) + onsets ----------------
     // force_legacy_bpm skips the tempogram estimate (src/lib.rs:337): no escalation, no
     // candidates, the flags stay None; the hop-512 pass still feeds the onset detectors
@@ -1297,6 +1488,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     const int NK = (int)K.size();
     std::vector<KeyOut> kout;
     KeyOut* d_kout = nullptr;
+    KeyDbg* d_kdbg = nullptr;
     std::unique_ptr<Timers> ktp(new Timers());
     Timers& kt = *ktp;
     kt.init(d_);
@@ -1478,7 +1670,8 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         // the template upload above is on the main stream too
         kt.mark(8);
         SDSP_HIP_CHECK(hipStreamWaitEvent(st2, kt.ev[8], 0));
-        launch_key_vote(d_kid, NK, d_kpfx, d_chroma, d_energy, d_cs, d_w, d_sscr, d_kseg, d_tpl, kp, d_kout, st2);
+        d_kdbg = dbg_on ? c_.dev<KeyDbg>(EP + "kdbg", (size_t)NK) : nullptr;
+        launch_key_vote(d_kid, NK, d_kpfx, d_chroma, d_energy, d_cs, d_w, d_sscr, d_kseg, d_tpl, kp, d_kout, st2, d_kdbg);
         SDSP_HIP_CHECK(hipGetLastError());
         kt.mark(2, st2);
         times_.stft8192_launches += 1;
@@ -1611,6 +1804,20 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
             if (e.ambiguous) E.push_back(i);
         }
     }
+    if (dbg_on && mr_on) {  // src/lib.rs:461-487: the base estimate and its candidate list
+        const std::vector<TempoEst> be = best.empty() ? c_.down(bo.est, (size_t)NR) : best;
+        const std::vector<float> bc = c_.down(bo.cand, (size_t)NR * (size_t)bin.cand_cap * 4);
+        for (int i = 0; i < NR; i++) {
+            if (!be[(size_t)i].ok) continue;
+            TrackDbg& t = tdbg[(size_t)i];
+            t.base = true;
+            t.est = be[(size_t)i];
+            for (int c = 0; c < std::min(be[(size_t)i].n_cands, bin.cand_cap); c++) {
+                const float* q = bc.data() + ((size_t)i * (size_t)bin.cand_cap + (size_t)c) * 4;
+                t.base_c.push_back({q[0], q[1], q[2], q[3]});
+            }
+        }
+    }
     float* d_fbpm = c_.up("B.fbpm", fbpm);
     float* d_fconf = c_.up("B.fconf", fconf);
     int* d_used = c_.up("B.used", used);
@@ -1711,10 +1918,40 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         mp.own512 = own512 ? 1 : 0;
         TempoEst* d_mr = c_.dev<TempoEst>("C.mr", (size_t)NE);
         d_mr_all = d_mr;
+        MrDbg* d_mdbg = dbg_on ? c_.dev<MrDbg>("C.mrdbg", (size_t)NE) : nullptr;
         launch_multires(d_E, NE, o256.cand, d_n256, b512.cand, d_n512, o1024.cand, d_n1024, ein.cand_cap,
                         own512 ? top_k : bin.cand_cap, ein.cand_cap, bo.est, b512.nov_mr, b512.d_fpfx, mp, d_mr, d_used,
-                        d_fbpm, d_fconf, st);
+                        d_fbpm, d_fconf, st, d_mdbg);
         SDSP_HIP_CHECK(hipGetLastError());
+        if (dbg_on) {  // multi_resolution.rs:304-403, 707-860 and src/lib.rs:547-573
+            const int cap512 = own512 ? top_k : bin.cand_cap;
+            const std::vector<float> h256 = c_.down(o256.cand, (size_t)NE * (size_t)ein.cand_cap * 4);
+            const std::vector<float> h1024 = c_.down(o1024.cand, (size_t)NE * (size_t)ein.cand_cap * 4);
+            const std::vector<float> h512 =
+                c_.down(b512.cand, (size_t)(own512 ? NE : NR) * (size_t)cap512 * 4);
+            const std::vector<TempoEst> hmr = c_.down(d_mr, (size_t)NE);
+            const std::vector<MrDbg> hmd = c_.down(d_mdbg, (size_t)NE);
+            auto list = [](const std::vector<float>& h, size_t row, int cap, int n) {
+                std::vector<Cand4> v;
+                for (int c = 0; c < n; c++) {
+                    const float* q = h.data() + (row * (size_t)cap + (size_t)c) * 4;
+                    v.push_back({q[0], q[1], q[2], q[3]});
+                }
+                return v;
+            };
+            for (int k = 0; k < NE; k++) {
+                const int i = E[(size_t)k];
+                TrackDbg& t = tdbg[(size_t)i];
+                const int j512 = own512 ? k : i;
+                if (!hmr[(size_t)k].ok || n256[(size_t)k] < 0 || n1024[(size_t)k] < 0 || n512[(size_t)j512] < 0) continue;
+                t.mr = true;
+                t.c256 = list(h256, (size_t)k, ein.cand_cap, n256[(size_t)k]);
+                t.c512 = list(h512, (size_t)j512, cap512, n512[(size_t)j512]);
+                t.c1024 = list(h1024, (size_t)k, ein.cand_cap, n1024[(size_t)k]);
+                t.mr_est = hmr[(size_t)k];
+                t.md = hmd[(size_t)k];
+            }
+        }
         used = c_.down(d_used, (size_t)NR);
         for (int i : E) {
             if (used[(size_t)i]) res[(size_t)idx[(size_t)R[(size_t)i]]].mr_used = 1;
@@ -1868,7 +2105,8 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     // streams then stay busy 95 % of the span instead of 85 %, but the step does not get shorter
     // (1,918-1,953 vs 1,927-1,933 tracks/s, alternating runs on one box): the chip is saturated,
     // and the extra overlap only slows each kernel down.
-    const bool defer_key = NK > 0 && !beat_sync && !serial_streams && std::getenv("SDSP_KEY_DEFER") != nullptr;
+    const bool defer_key =
+        NK > 0 && !beat_sync && !serial_streams && !dbg_on && std::getenv("SDSP_KEY_DEFER") != nullptr;
     if (defer_key) {
         key_pending_.reset(new KeyPending());
         key_pending_->kt = std::move(ktp);
@@ -1991,6 +2229,22 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         r.key_tonic = ko.tonic;
         r.key_conf = ko.conf;
         r.key_clarity = ko.clarity;
+    }
+    if (dbg_on) {
+        if (NK > 0) {  // src/lib.rs:1471-1538 (the beat-synchronous re-vote keeps the frame-level record)
+            const std::vector<KeyDbg> kd = c_.down(d_kdbg, (size_t)NK);
+            const std::vector<float> tu = d_tune ? c_.down(d_tune, (size_t)NK) : std::vector<float>((size_t)NK, 0.0f);
+            for (int k = 0; k < NK; k++) {
+                const KeyOut& ko = kout[(size_t)k];
+                if (!ko.ok) continue;
+                TrackDbg& t = tdbg[(size_t)K[(size_t)k]];
+                t.key = true;
+                t.ko = ko;
+                t.kd = kd[(size_t)k];
+                t.tuning = tu[(size_t)k];
+            }
+        }
+        for (int i = 0; i < NR; i++) print_debug(cfg_, tdbg[(size_t)i]);
     }
     htr("results");
 }
