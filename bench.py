@@ -165,6 +165,7 @@ def main():
     ap.add_argument("--seconds", type=float, default=180.0, help="track length (config2 / bpm-only)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, usable host cores)")
     ap.add_argument("--cpu-tracks", type=int, default=0, help="0 = 2 per thread")
+    ap.add_argument("--cpu-1thread-tracks", type=int, default=2, help="tracks timed alone on one thread")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--bpm-mode", type=int, default=-1, help="synthetic BPM mix (-1 = the workload's; 1 = config 5)")
     ap.add_argument("--dry-run", action="store_true", help="host-logic rehearsal without a GPU (tests)")
@@ -429,8 +430,11 @@ def cpu_baseline(buf, offs, lens, res, n, sr, args):
         # other threads ran): k / the summed per-track seconds
         "value_1thread_loaded": round(k / sum(per_track), 4),
     }
-    # one thread alone, the first tracks again
-    k1 = min(k, 2)
+    # one thread alone, the first tracks again (more than the parallel sample: its own tracks)
+    k1 = max(1, args.cpu_1thread_tracks)
+    if k1 > k:
+        xs = xs + [buf.to_host(int(offs[i]), int(lens[i])) for i in range(k, min(n, k1))]
+    k1 = min(k1, len(xs))
     t0 = time.perf_counter()
     for x in xs[:k1]:
         one(x)

@@ -17,4 +17,7 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_stft --ker
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --kernel-include-regex k_stft --kernel-trace --output-format csv -d $O/sq -o $tag -- python3 $R/bench.py --tracks 64 --steps 1 --warmup 0 --no-cpu-baseline > $O/sq.log 2>&1 &&
 python3 $R/tools/kstats.py $O/serial/${tag}_kernel_stats.csv 30 > $O/serial_top.txt &&
 python3 $R/tools/timeline.py $O/conc/${tag}_kernel_trace.csv 3000 > $O/conc_timeline.txt &&
+python3 $R/tools/streams.py $O/conc/${tag}_kernel_trace.csv 3000 >> $O/conc_timeline.txt &&
+python3 $R/tools/pmc_stft.py 8192 $O/fetch/${tag}_counter_collection.csv $O/write/${tag}_counter_collection.csv $O/fetch.log > $O/pmc_stft8192.json &&
+timeout -k 10 300 python3 $R/bench.py --tracks 64 --steps 1 --warmup 0 --cpu-tracks 32 --cpu-1thread-tracks 32 > $O/cpu1.json 2> $O/cpu1.err &&
 echo "profiles done"
