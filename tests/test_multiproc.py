@@ -109,3 +109,13 @@ def test_gpus_world_mismatch_is_an_error():
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run", "--tracks", "2",
                           "--seconds", "1"], capture_output=True, text=True, timeout=120, cwd=ROOT, env=env)
     assert out.returncode != 0 and "WORLD_SIZE" in out.stderr
+
+
+def test_bench_spawns_eight_ranks_without_torchrun():
+    """The driver's 8-GPU invocation, rehearsed on the CPU: 8 rank processes, one JSON line, the
+    whole job's tracks over the slowest rank's time."""
+    d = _bench_json([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--steps", "1", "--warmup", "0",
+                     "--tracks", "2", "--seconds", "1", "--dry-run"])
+    assert d["n_gpus"] == 8 and d["config"]["parallelism"].startswith("track-sharded x8")
+    assert d["config"]["baseline_config"] == 3
+    assert abs(d["value"] - 2 * 8 / (d["ms_per_step"] / 1000.0)) / d["value"] < 1e-2
