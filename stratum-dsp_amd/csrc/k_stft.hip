@@ -404,6 +404,101 @@ __global__ __launch_bounds__(256) STFT_ATTR void k_stft_mag(const float* __restr
 }
 
 // ---------------------------------------------------------------------------------------------
+// k_stft_gen: the STFT of any power-of-two frame size N in [STFT_GEN_MIN, STFT_GEN_MAX] other
+// than the tuned 2048 / 8192 (AnalysisConfig::frame_size is a free knob, src/config.rs).  The
+// spec's algorithm stage by stage: one 256-thread workgroup per frame, z = M = N/2 complex values
+// ping-ponged between two LDS buffers (dynamic LDS, 8 N bytes), radix-4 stages then the radix-2
+// stage when log2 M is odd, the real-FFT post-processing bin by bin with the symmetric post
+// twiddles, |X| by the correctly rounded sqrt.  tw / rt are the spec's plain tables.  Each
+// butterfly and each bin evaluates exactly the expressions of oracle/o_fft.cpp stft_fft_complex /
+// stft_mag, so the magnitudes are bit-identical to the tuned kernels' (same spec).
+template <bool FRAME_MAX>
+__global__ __launch_bounds__(256) void k_stft_gen(int N, const float* __restrict__ samples,
+                                                  const uint64_t* __restrict__ frame_pfx, int n_tracks,
+                                                  uint64_t total_frames, const uint64_t* __restrict__ src_off,
+                                                  const float* __restrict__ gain, int hop,
+                                                  const float* __restrict__ window, const cx* __restrict__ tw,
+                                                  const cx* __restrict__ rt, float* __restrict__ mags,
+                                                  const uint64_t* __restrict__ mag_row0, int stride,
+                                                  float* __restrict__ frame_max) {
+    extern __shared__ c2 gen_lds[];
+    __shared__ float red[4];
+    const uint64_t g = xcd_block(blockIdx.x, gridDim.x);
+    if (g >= total_frames) return;  // whole workgroup: uniform
+    const int M = N >> 1, lgm = 31 - __builtin_clz((unsigned)M);
+    const int trk = find_track(frame_pfx, n_tracks, g);
+    const uint64_t f = g - frame_pfx[trk];
+    const float gn = gain[trk];
+    const float* x = samples + src_off[trk] + f * (uint64_t)hop;
+    c2* a = gen_lds;
+    c2* b = gen_lds + M;
+    for (int j = threadIdx.x; j < M; j += 256)
+        a[j] = c2{(x[2 * j] * gn) * window[2 * j], (x[2 * j + 1] * gn) * window[2 * j + 1]};
+    __syncthreads();
+    // radix-4 stages: (n, s) = (M, 1), (M/4, 4), ...; butterfly u = p s + q
+    int lgs = 0;
+    for (int lgn = lgm; lgn >= 2; lgn -= 2, lgs += 2) {
+        const int s = 1 << lgs, m = 1 << (lgn - 2), tstep = M >> lgn;
+        for (int u = threadIdx.x; u < (M >> 2); u += 256) {
+            const int q = u & (s - 1), p = u >> lgs;
+            c2 y0, y1, y2, y3;
+            const c2 va = a[q + s * p], vb = a[q + s * (p + m)], vc = a[q + s * (p + 2 * m)],
+                     vd = a[q + s * (p + 3 * m)];
+            if (p) {
+                const cx w1 = tw[p * tstep], w2 = tw[2 * p * tstep], w3 = tw[3 * p * tstep];
+                bfly4<true>(va, vb, vc, vd, c2{w1.re, w1.im}, c2{w2.re, w2.im}, c2{w3.re, w3.im}, y0, y1, y2, y3);
+            } else {
+                bfly4<false>(va, vb, vc, vd, c2{}, c2{}, c2{}, y0, y1, y2, y3);
+            }
+            const int o = q + s * 4 * p;
+            b[o] = y0;
+            b[o + s] = y1;
+            b[o + 2 * s] = y2;
+            b[o + 3 * s] = y3;
+        }
+        __syncthreads();
+        c2* t = a;
+        a = b;
+        b = t;
+    }
+    if (lgm & 1) {  // radix-2 stage: s = M/2
+        const int s = M >> 1;
+        for (int q = threadIdx.x; q < s; q += 256) {
+            const c2 va = a[q], vb = a[q + s];
+            b[q] = c2{va.x + vb.x, va.y + vb.y};
+            b[q + s] = c2{va.x - vb.x, va.y - vb.y};
+        }
+        __syncthreads();
+        a = b;
+    }
+    // post-processing, k = 0..M (oracle/o_fft.cpp stft_mag)
+    float* out = mags + (mag_row0[trk] + f) * (uint64_t)stride;
+    float mx = 0.0f;
+    for (int k = threadIdx.x; k <= M; k += 256) {
+        const c2 zk = a[k & (M - 1)], zr = a[(M - k) & (M - 1)];
+        const cx r = rt[k > (M >> 1) ? M - k : k];
+        const c2 w = k > (M >> 1) ? c2{-r.re, r.im} : c2{r.re, r.im};
+        const float sre = zk.x + zr.x, sim = zk.y - zr.y;
+        const float dre = zk.y + zr.y, dim = -(zk.x - zr.x);
+        const float yre = __builtin_fmaf(w.x, dre, __builtin_fmaf(-w.y, dim, sre));
+        const float yim = __builtin_fmaf(w.x, dim, __builtin_fmaf(w.y, dre, sim));
+        const float mag = 0x1p-33f * sqrt_cr(__builtin_fmaf(yre, yre, yim * yim));
+        out[k] = mag;
+        if (FRAME_MAX) mx = sd_maxf(mx, mag);
+    }
+    if (FRAME_MAX) {
+        mx = wave_max(mx);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            float m = red[0];
+            for (int i = 1; i < 4; i++) m = sd_maxf(m, red[i]);
+            frame_max[mag_row0[trk] + f] = m;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Sliding-strip STFT (the pipeline's kernel for hops that are a multiple of 2*TPF complex
 // values: 8192/512, 8192/1024, 2048/256, 2048/512, 2048/1024).  Same arithmetic as k_stft_mag,
 // different data movement, because the isolated profile of k_stft_mag showed it bound by what it
@@ -745,6 +840,9 @@ void stft_tables(int N, const std::vector<float>& tw, const std::vector<float>& 
     put(rtp, sbase + 8 * (size_t)TPF, &rt[2 * (size_t)(M / 2)]);
 }
 
+bool stft_tuned(int N) { return N == 2048 || N == 8192; }
+bool stft_size_ok(int N) { return N >= STFT_GEN_MIN && N <= STFT_GEN_MAX && (N & (N - 1)) == 0; }
+
 // hop = S * 2 * TPF complex values with a k_stft_slide instance
 bool stft_slide_ok(int nfft, int hop) {
     if (nfft == 8192) return hop == 512 || hop == 1024;
@@ -761,6 +859,26 @@ void launch_stft(int nfft, bool frame_max, const float* samples, const uint64_t*
                  hipStream_t st, const uint64_t* strip_pfx, uint64_t n_strips, uint32_t* redo) {
     if (total_frames == 0) return;
     const dim3 block(256);
+    // the general kernel: other sizes, and N = 8192 with frame maxima (a tempo-path frame_size of
+    // 8192; the tuned 8192 kernels serve the key path, which needs none)
+    if (stft_general(nfft, frame_max)) {
+        if (!stft_size_ok(nfft)) throw HipError("launch_stft: frame size not a power of two in [64, 16384]");
+        if (total_frames > 0xffffffffull) throw HipError("launch_stft: too many frames for one launch");
+        const size_t lds = (size_t)8 * (size_t)nfft;  // two buffers of N/2 complex values
+        static bool attr_set[2] = {false, false};
+        if (lds > 65536 && !attr_set[frame_max]) {
+            SDSP_HIP_CHECK(hipFuncSetAttribute(frame_max ? (const void*)k_stft_gen<true> : (const void*)k_stft_gen<false>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)(8 * STFT_GEN_MAX)));
+            attr_set[frame_max] = true;
+        }
+        if (frame_max)
+            hipLaunchKernelGGL(k_stft_gen<true>, dim3((unsigned)total_frames), block, lds, st, nfft, samples, frame_pfx,
+                               n_tracks, total_frames, src_off, gain, hop, window, twp, rtp, mags, mag_row0, stride, fmax);
+        else
+            hipLaunchKernelGGL(k_stft_gen<false>, dim3((unsigned)total_frames), block, lds, st, nfft, samples, frame_pfx,
+                               n_tracks, total_frames, src_off, gain, hop, window, twp, rtp, mags, mag_row0, stride, fmax);
+        return;
+    }
     if (strip_pfx && n_strips && redo && stft_slide_ok(nfft, hop)) {
         // redo[0] = 0; redo[1..] receives the frames the sliding kernel could not finish exactly
         SDSP_HIP_CHECK(hipMemsetAsync(redo, 0, sizeof(uint32_t), st));

@@ -47,6 +47,12 @@ static int env_stride(const char* name, int dflt, int min) {
 }
 static const int STRIDE2 = env_stride("SDSP_STRIDE2", 1028, 1025);  // 1025 bins
 static const int STRIDE8 = env_stride("SDSP_STRIDE8", 4160, 4097);  // 4097 bins
+// row stride of the tempo path's spectrogram for AnalysisConfig::frame_size (nb = fs/2 + 1 bins)
+static int base_stride(int fs) {
+    if (fs == 2048) return STRIDE2;
+    if (fs == 8192) return STRIDE8;
+    return (fs / 2 + 1 + 3) & ~3;
+}
 constexpr int SUPPORT_HMAX = 8;
 
 uint64_t next_pow2(uint64_t n) {
@@ -520,7 +526,8 @@ std::string unsupported(const sdsp_config& c, uint32_t sr) {
     if (c.enable_normalization && c.normalization != SDSP_NORM_PEAK && c.normalization != SDSP_NORM_RMS &&
         c.normalization != SDSP_NORM_LOUDNESS)
         return "unknown normalization method";
-    if (c.frame_size != 2048) return "frame_size other than 2048";
+    if (c.frame_size > (uint64_t)STFT_GEN_MAX || !stft_size_ok((int)c.frame_size))
+        return "frame_size not a power of two in [64, 16384]";
     if (c.hop_size == 0 || c.hop_size > 8192) return "hop_size outside 1..8192";
     if ((c.enable_hpss_onsets || c.enable_tempogram_percussive_fallback) && c.hpss_margin > 16) return "hpss_margin > 16";
     if (!(c.min_bpm > 0.0f && c.max_bpm > c.min_bpm && c.bpm_resolution > 0.0f)) return "BPM range/resolution";
@@ -562,8 +569,8 @@ struct TempoPassIn {
     std::vector<uint64_t> n_trim;
     bool want_onsets;  // hop-512 pass: also spectral/HFC onset features (SFO)
     int top_n, gate, cand_cap;
-    // a precomputed 2048-point spectrogram (rows at the pass's frame prefix, STRIDE2) and its frame
-    // maxima: the STFT is skipped (the percussive tempogram fallback runs on the HPSS output)
+    // a precomputed frame_size-point spectrogram (rows at the pass's frame prefix, stride s2_) and
+    // its frame maxima: the STFT is skipped (the percussive tempogram fallback runs on the HPSS output)
     const float* mags_in = nullptr;
     const float* fmax_in = nullptr;
     // escalation hops over the hop-512 spectrogram (rows base_row0[t] + frame): 1 = hop 1024, every
@@ -785,7 +792,14 @@ void print_debug(const sdsp_config& c, const TrackDbg& d) {
 class Pipeline {
    public:
     Pipeline(DeviceCtx& d, const sdsp_config& cfg, uint32_t sr, int stages = SDSP_STAGES_FULL)
-        : c_(d), d_(d), cfg_(cfg), sr_(sr), bpm_only_(stages == SDSP_STAGES_BPM_ONLY) {}
+        : c_(d),
+          d_(d),
+          cfg_(cfg),
+          sr_(sr),
+          bpm_only_(stages == SDSP_STAGES_BPM_ONLY),
+          fs_((int)std::min<uint64_t>(cfg.frame_size, STFT_GEN_MAX)),
+          nb_(fs_ / 2 + 1),
+          s2_(base_stride(fs_)) {}
 
     void run(const float* d_samples, const std::vector<uint64_t>& in_off, const std::vector<uint64_t>& n_raw,
              std::vector<TrackRes>& res);
@@ -798,6 +812,8 @@ class Pipeline {
     // SDSP_STAGES_BPM_ONLY: the tempo path alone (src/lib.rs:86-910); the key
     // stream and the beat grid are not run, their result fields keep their defaults
     bool bpm_only_ = false;
+    // the tempo path's STFT: frame size (AnalysisConfig::frame_size), bins, row stride
+    const int fs_, nb_, s2_;
     sdsp_stage_times times_{};
     // RMS / LUFS: gains (and LUFS status) of every track, folded once for the whole batch
     // before the sub-batches (the fold is a per-track sequential latency, not a throughput)
@@ -815,7 +831,7 @@ class Pipeline {
     struct KeyPending {
         std::unique_ptr<Timers> kt;
         KeyOut* d_kout = nullptr;
-    KeyDbg* d_kdbg = nullptr;
+        KeyDbg* d_kdbg = nullptr;
         std::vector<size_t> at;  // result slot of each key track
     };
     std::unique_ptr<KeyPending> key_pending_;
@@ -878,12 +894,12 @@ void Pipeline::run(const float* d_samples, const std::vector<uint64_t>& in_off, 
     for (size_t i = 0; i < T; i++) {
         if (res[i].status != SDSP_OK) continue;
         const double n = (double)n_raw[i];
-        need[i] = n / hop * (STRIDE2 * 4.0 * 1.3 + 4 * 70.0) + (bpm_only_ ? 0.0 : n / khop * STRIDE8 * 4.0 * ckpt_f) +
-                  (n / 256 + n / 1024) * STRIDE2 * 4.0 + 1e6;
+        need[i] = n / hop * (s2_ * 4.0 * 1.3 + 4 * 70.0) + (bpm_only_ ? 0.0 : n / khop * STRIDE8 * 4.0 * ckpt_f) +
+                  (n / 256 + n / 1024) * s2_ * 4.0 + 1e6;
         if (cfg_.enable_hpss_onsets || cfg_.enable_tempogram_percussive_fallback)  // H, P ping-pong + a copy
-            need[i] += n / hop * STRIDE2 * 4.0 * 5.0;
+            need[i] += n / hop * s2_ * 4.0 * 5.0;
         if (cfg_.enable_key_hpss_harmonic && !bpm_only_) need[i] += n / khop * 1024.0 * 4.0;
-        if (cfg_.enable_tempogram_multi_resolution && hop != 512) need[i] += n / 512 * STRIDE2 * 4.0 * 1.3;
+        if (cfg_.enable_tempogram_multi_resolution && hop != 512) need[i] += n / 512 * s2_ * 4.0 * 1.3;
         total_need += need[i];
     }
     const double parts = std::max(1.0, std::ceil(total_need / budget));
@@ -1036,7 +1052,7 @@ void Pipeline::legacy_select(const TempoPassIn& bin, const uint32_t* d_onsets, c
 
 void Pipeline::tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPassOut& o) {
     const int P_T = (int)in.src_off.size();
-    const int FS = 2048, hop = in.hop;
+    const int FS = fs_, hop = in.hop;
     // frames per pass-track
     o.fpfx.assign((size_t)P_T + 1, 0);
     std::vector<uint64_t> tpfx((size_t)P_T + 1, 0);
@@ -1077,21 +1093,21 @@ void Pipeline::tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPa
             osrc[(size_t)t] = in.src_off[(size_t)t] + (uint64_t)hop;
         }
         stft_frames = opfx[(size_t)P_T];
-        o.mags = c_.dev<float>(tag + "mags", std::max<uint64_t>(stft_frames, 1) * STRIDE2);
+        o.mags = c_.dev<float>(tag + "mags", std::max<uint64_t>(stft_frames, 1) * s2_);
         o.fmax = c_.dev<float>(tag + "fmax", std::max<uint64_t>(stft_frames, 1));
         uint64_t* d_opfx = c_.up(tag + "opfx", opfx);
         const std::vector<uint64_t> ostr = stft_strips(opfx);
         launch_stft(FS, true, in.samples, d_opfx, P_T, stft_frames, c_.up(tag + "osrc", osrc), d_gain, 2 * hop,
-                    tb.window.as<float>(), tb.stft_tw.as<cx>(), tb.stft_rt.as<cx>(), o.mags, d_opfx, STRIDE2, o.fmax,
+                    tb.window.as<float>(), stft_twp(tb, FS, true), stft_rtp(tb, FS, true), o.mags, d_opfx, s2_, o.fmax,
                     d_.stream, c_.up(tag + "ostrip", ostr), ostr.back(), c_.dev<uint32_t>(tag + "redo", stft_frames + 1));
         SDSP_HIP_CHECK(hipGetLastError());
         rm = RowMap{in.base_mags, o.mags, in.base_fmax, o.fmax, c_.up(tag + "brow", in.base_row0), d_opfx, 0, 1, 1};
     } else {
-        o.mags = c_.dev<float>(tag + "mags", total * STRIDE2);
+        o.mags = c_.dev<float>(tag + "mags", total * s2_);
         o.fmax = c_.dev<float>(tag + "fmax", total);
         const std::vector<uint64_t> str = stft_strips(o.fpfx);
         launch_stft(FS, true, in.samples, o.d_fpfx, P_T, total, d_src, d_gain, hop, tb.window.as<float>(),
-                    tb.stft_tw.as<cx>(), tb.stft_rt.as<cx>(), o.mags, o.d_fpfx, STRIDE2, o.fmax, d_.stream,
+                    stft_twp(tb, FS, true), stft_rtp(tb, FS, true), o.mags, o.d_fpfx, s2_, o.fmax, d_.stream,
                     c_.up(tag + "strip", str), str.back(), c_.dev<uint32_t>(tag + "redo", total + 1));
         SDSP_HIP_CHECK(hipGetLastError());
         stft_frames = total;
@@ -1102,13 +1118,13 @@ void Pipeline::tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPa
     if (stft_frames) {
         double inb = 0;
         for (int t = 0; t < P_T; t++) inb += 4.0 * (double)in.n_trim[(size_t)t];
-        o.stft_bytes = inb + 4.0 * (double)stft_frames * 1025.0;
+        o.stft_bytes = inb + 4.0 * (double)stft_frames * (double)nb_;
     }
     // features
-    const int B = 1025;
+    const int B = nb_;
     FeatParams fp{};
     fp.B = B;
-    fp.stride = STRIDE2;
+    fp.stride = s2_;
     fp.K = (int)std::max<uint64_t>(cfg_.tempogram_superflux_max_filter_bins, 1);
     const float fres = (float)sr_ / (float)((B - 1) * 2);
     const int b0 = std::min(1, B - 1);
@@ -1352,7 +1368,7 @@ void Pipeline::finish_key(std::vector<TrackRes>& res) {
 void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in_off, const std::vector<uint64_t>& n_raw,
                          const std::vector<int>& idx, std::vector<TrackRes>& res) {
     const int T = (int)idx.size();
-    const int FS = 2048;
+    const int FS = fs_;
     const int HOP = (int)cfg_.hop_size;
     hipStream_t st = d_.stream;
     HostTrace htr;
@@ -1707,7 +1723,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         const uint64_t totS = hpfx.back();
         if (NS > 0 && totS > 0) {
             std::vector<uint64_t> orow, vt(1, 0), rt(1, 0);
-            const uint64_t ncb = (1025 + HPSS_COLS - 1) / HPSS_COLS;
+            const uint64_t ncb = (nb_ + HPSS_COLS - 1) / HPSS_COLS;
             for (int k = 0; k < NS; k++) {
                 const uint64_t F = hpfx[(size_t)k + 1] - hpfx[(size_t)k];
                 orow.push_back(bo.fpfx[(size_t)S[(size_t)k]]);
@@ -1715,14 +1731,14 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
                 rt.push_back(rt.back() + (F + HPSS_ROW_FRAMES - 1) / HPSS_ROW_FRAMES);
             }
             HpssLaunch L{};
-            L.P.B = 1025;
-            L.P.stride = STRIDE2;
+            L.P.B = nb_;
+            L.P.stride = s2_;
             L.P.m = (int)cfg_.hpss_margin;
             L.orig = bo.mags;
             L.orig_row0 = c_.up("H.orow", orow);
             for (int q = 0; q < 2; q++) {
-                L.h[q] = c_.dev<float>("H.h" + std::to_string(q), totS * STRIDE2);
-                L.p[q] = c_.dev<float>("H.p" + std::to_string(q), totS * STRIDE2);
+                L.h[q] = c_.dev<float>("H.h" + std::to_string(q), totS * s2_);
+                L.p[q] = c_.dev<float>("H.p" + std::to_string(q), totS * s2_);
             }
             uint64_t* d_hpfx = c_.up("H.hpfx", hpfx);
             L.row0 = d_hpfx;
@@ -1737,7 +1753,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
             d_P0 = L.p[0];
             d_hpe = c_.dev<float>("H.e", totS);
             d_hfmax = c_.dev<float>("H.fmax", totS);
-            launch_hpss_rows(d_P0, d_hpfx, d_hpfx, c_.up("H.rt", rt), rt.back(), NS, STRIDE2, 1025, d_hpe, d_hfmax, st);
+            launch_hpss_rows(d_P0, d_hpfx, d_hpfx, c_.up("H.rt", rt), rt.back(), NS, s2_, nb_, d_hpe, d_hfmax, st);
             SDSP_HIP_CHECK(hipGetLastError());
             htr("HPSS");
         }
@@ -1994,13 +2010,13 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
             pin.cand_cap = bin.cand_cap;
             pin.gate = 0;
             if (hpss_on) {  // S holds every track: gather Q's rows (S == Q otherwise)
-                float* pq = c_.dev<float>("P.in", std::max<uint64_t>(qpfx.back(), 1) * STRIDE2);
+                float* pq = c_.dev<float>("P.in", std::max<uint64_t>(qpfx.back(), 1) * s2_);
                 float* pm = c_.dev<float>("P.inmax", std::max<uint64_t>(qpfx.back(), 1));
                 for (int k = 0; k < NQ; k++) {
                     const uint64_t F = qpfx[(size_t)k + 1] - qpfx[(size_t)k], r0 = bo.fpfx[(size_t)Q[(size_t)k]];
                     if (F == 0) continue;
-                    SDSP_HIP_CHECK(hipMemcpyAsync(pq + qpfx[(size_t)k] * STRIDE2, d_P0 + r0 * STRIDE2,
-                                                  F * STRIDE2 * sizeof(float), hipMemcpyDeviceToDevice, st));
+                    SDSP_HIP_CHECK(hipMemcpyAsync(pq + qpfx[(size_t)k] * s2_, d_P0 + r0 * s2_,
+                                                  F * s2_ * sizeof(float), hipMemcpyDeviceToDevice, st));
                     SDSP_HIP_CHECK(hipMemcpyAsync(pm + qpfx[(size_t)k], d_hfmax + r0, F * sizeof(float),
                                                   hipMemcpyDeviceToDevice, st));
                 }

@@ -78,11 +78,13 @@ FftTables& DeviceCtx::tables(int N, bool with_window) {
         std::vector<float> tw(2 * (size_t)(N / 2)), rt((size_t)N + 2), a, b;
         sdsp_fft_twiddles(N / 2, tw.data());
         sdsp_rfft_twiddles(N, rt.data());
-        stft_tables(N, tw, rt, &a, &b);
-        t->stft_tw.ensure(a.size() * 4);
-        t->stft_rt.ensure(b.size() * 4);
-        SDSP_HIP_CHECK(hipMemcpy(t->stft_tw.p, a.data(), a.size() * 4, hipMemcpyHostToDevice));
-        SDSP_HIP_CHECK(hipMemcpy(t->stft_rt.p, b.data(), b.size() * 4, hipMemcpyHostToDevice));
+        if (stft_tuned(N)) {  // k_stft_gen reads tw / rt as they are
+            stft_tables(N, tw, rt, &a, &b);
+            t->stft_tw.ensure(a.size() * 4);
+            t->stft_rt.ensure(b.size() * 4);
+            SDSP_HIP_CHECK(hipMemcpy(t->stft_tw.p, a.data(), a.size() * 4, hipMemcpyHostToDevice));
+            SDSP_HIP_CHECK(hipMemcpy(t->stft_rt.p, b.data(), b.size() * 4, hipMemcpyHostToDevice));
+        }
     }
     return *t;
 }
@@ -263,7 +265,7 @@ int32_t sdsp_last_stage_times(int32_t device, sdsp_stage_times* out) {
 int32_t sdsp_probe_stft(int32_t device, uint64_t nfft, uint64_t hop, uint64_t n_tracks, uint64_t len, int32_t reps,
                         int32_t stride, double* ms_per_launch, double* bytes_per_launch) {
     try {
-        if (!(nfft == 2048 || nfft == 8192) || len < nfft || hop == 0 || n_tracks == 0 || reps <= 0)
+        if (!stft_size_ok((int)std::min<uint64_t>(nfft, 1u << 30)) || len < nfft || hop == 0 || n_tracks == 0 || reps <= 0)
             return SDSP_ERR_INVALID_INPUT;
         DeviceCtx& c = device_ctx(device);
         std::lock_guard<std::mutex> lk(c.mu);
@@ -310,9 +312,9 @@ int32_t sdsp_probe_stft(int32_t device, uint64_t nfft, uint64_t hop, uint64_t n_
         SDSP_HIP_CHECK(hipEventCreate(&e0));
         SDSP_HIP_CHECK(hipEventCreate(&e1));
         auto launch = [&]() {
-            launch_stft((int)nfft, nfft == 2048, x.as<float>(), pfx.as<uint64_t>(), (int)n_tracks, total,
-                        off.as<uint64_t>(), g.as<float>(), (int)hop, tb.window.as<float>(), tb.stft_tw.as<cx>(),
-                        tb.stft_rt.as<cx>(), mags.as<float>(), row0.as<uint64_t>(), stride, fmax.as<float>(), c.stream,
+            launch_stft((int)nfft, nfft != 8192, x.as<float>(), pfx.as<uint64_t>(), (int)n_tracks, total,
+                        off.as<uint64_t>(), g.as<float>(), (int)hop, tb.window.as<float>(),
+                        stft_twp(tb, (int)nfft, nfft != 8192), stft_rtp(tb, (int)nfft, nfft != 8192), mags.as<float>(), row0.as<uint64_t>(), stride, fmax.as<float>(), c.stream,
                         frame_parallel ? nullptr : strips.as<uint64_t>(), sp.back(), redo.as<uint32_t>());
         };
         launch();  // warm: first touch of the output pages
@@ -338,7 +340,7 @@ int32_t sdsp_probe_stft(int32_t device, uint64_t nfft, uint64_t hop, uint64_t n_
 int32_t sdsp_debug_stft(const float* host_x, uint64_t n, uint64_t nfft, uint64_t hop, float gain, float* host_out,
                         float* host_frame_max, int32_t device) {
     try {
-        if (!(nfft == 2048 || nfft == 8192) || n < nfft || hop == 0) return SDSP_ERR_INVALID_INPUT;
+        if (!stft_size_ok((int)std::min<uint64_t>(nfft, 1u << 30)) || n < nfft || hop == 0) return SDSP_ERR_INVALID_INPUT;
         DeviceCtx& c = device_ctx(device);
         std::lock_guard<std::mutex> lk(c.mu);
         SDSP_HIP_CHECK(hipSetDevice(device));
@@ -367,15 +369,16 @@ int32_t sdsp_debug_stft(const float* host_x, uint64_t n, uint64_t nfft, uint64_t
         SDSP_HIP_CHECK(hipMemcpy(off.p, &o0, 8, hipMemcpyHostToDevice));
         SDSP_HIP_CHECK(hipMemcpy(g.p, &gain, 4, hipMemcpyHostToDevice));
         SDSP_HIP_CHECK(hipMemcpy(row0.p, &r0, 8, hipMemcpyHostToDevice));
-        launch_stft((int)nfft, nfft == 2048, x.as<float>(), pfx.as<uint64_t>(), 1, frames, off.as<uint64_t>(),
-                    g.as<float>(), (int)hop, tb.window.as<float>(), tb.stft_tw.as<cx>(), tb.stft_rt.as<cx>(), mags.as<float>(),
+        launch_stft((int)nfft, nfft != 8192, x.as<float>(), pfx.as<uint64_t>(), 1, frames, off.as<uint64_t>(),
+                    g.as<float>(), (int)hop, tb.window.as<float>(), stft_twp(tb, (int)nfft, nfft != 8192),
+                    stft_rtp(tb, (int)nfft, nfft != 8192), mags.as<float>(),
                     row0.as<uint64_t>(), stride, fmax.as<float>(), c.stream, frame_parallel ? nullptr : strips.as<uint64_t>(),
                     sp.back(), redo.as<uint32_t>());
         SDSP_HIP_CHECK(hipGetLastError());
         SDSP_HIP_CHECK(hipStreamSynchronize(c.stream));
         SDSP_HIP_CHECK(hipMemcpy2D(host_out, (size_t)bins * 4, mags.p, (size_t)stride * 4, (size_t)bins * 4,
                                    frames, hipMemcpyDeviceToHost));
-        if (host_frame_max && nfft == 2048)
+        if (host_frame_max && nfft != 8192)
             SDSP_HIP_CHECK(hipMemcpy(host_frame_max, fmax.p, frames * 4, hipMemcpyDeviceToHost));
         return SDSP_OK;
     } catch (const std::exception& e) {

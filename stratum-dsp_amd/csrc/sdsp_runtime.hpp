@@ -82,6 +82,21 @@ struct DeviceCtx {
 
 DeviceCtx& device_ctx(int device);
 
+// STFT sizes with the tuned kernels (k_stft_mag / k_stft_slide: N = 2048, 8192).  Other powers of
+// two in [STFT_GEN_MIN, STFT_GEN_MAX], and N = 8192 with frame maxima, run the general kernel
+// k_stft_gen, which reads the spec's plain tables (FftTables::tw / rt); stft_twp / stft_rtp pick
+// the tables launch_stft expects.
+constexpr int STFT_GEN_MIN = 64, STFT_GEN_MAX = 16384;
+bool stft_tuned(int N);
+bool stft_size_ok(int N);
+inline bool stft_general(int N, bool frame_max) { return !stft_tuned(N) || (N == 8192 && frame_max); }
+inline const cx* stft_twp(FftTables& t, int N, bool frame_max) {
+    return stft_general(N, frame_max) ? t.tw.as<cx>() : t.stft_tw.as<cx>();
+}
+inline const cx* stft_rtp(FftTables& t, int N, bool frame_max) {
+    return stft_general(N, frame_max) ? t.rt.as<cx>() : t.stft_rt.as<cx>();
+}
+
 // Per-thread STFT twiddle tables (k_stft.hip), built from the sdsp_fft_spec.h tables (tw: N/2
 // complex, rt: N/2+1 complex, interleaved) so every value is bit-identical to the spec's.
 void stft_tables(int N, const std::vector<float>& tw, const std::vector<float>& rt, std::vector<float>* twp,

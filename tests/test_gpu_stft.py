@@ -30,6 +30,34 @@ def test_stft_bit_exact(nfft, hop, frame_parallel, monkeypatch):
         assert np.array_equal(fmax, ref.max(axis=1))
 
 
+@pytest.mark.parametrize("nfft,hop", [(64, 16), (128, 37), (256, 128), (512, 256), (1024, 512), (1024, 441),
+                                      (4096, 512), (4096, 1000), (16384, 2048)])
+def test_stft_general_sizes_bit_exact(nfft, hop):
+    """k_stft_gen (frame sizes other than the tuned 2048 / 8192: AnalysisConfig::frame_size is a
+    free power of two): radix-4 stages, the radix-2 stage when log2(N/2) is odd (64, 256, 1024,
+    4096, 16384), odd hops (unaligned frames), 128 KB of LDS at N = 16384; bit-exact magnitudes and
+    frame maxima."""
+    rng = np.random.default_rng(nfft * 3 + hop)
+    x = (rng.standard_normal(44100 * 2) * 0.3).astype(np.float32)
+    x[20000:30000] = 0.0
+    x[40000:45000] = (rng.standard_normal(5000) * 1e-30).astype(np.float32)
+    gain = np.float32(0.8912509)
+    got, fmax = sdsp.debug_stft(x, nfft, hop, gain)
+    ref = oracle.stft((x * gain).astype(np.float32), nfft, hop)
+    assert got.shape == ref.shape
+    mism = np.count_nonzero(got.view(np.uint32) != ref.view(np.uint32))
+    assert mism == 0, f"{mism} of {ref.size} magnitudes differ (max abs diff {np.max(np.abs(got - ref))})"
+    assert np.array_equal(fmax, ref.max(axis=1))
+
+
+@pytest.mark.parametrize("nfft", [32, 3000, 32768])
+def test_stft_sizes_refused(nfft):
+    """Sizes outside the powers of two in [64, 16384] are refused with INVALID_INPUT."""
+    x = np.zeros(70000, np.float32)
+    with pytest.raises(sdsp.AnalysisError):
+        sdsp.debug_stft(x, nfft, 512)
+
+
 @pytest.mark.parametrize("nfft,hop", [(2048, 512), (8192, 512), (2048, 256)])
 def test_stft_silence_and_subnormal_scale(nfft, hop):
     """Digital silence (|X|^2 = 0: the fast sqrt's zero case) and frames of ~1e-30-scale samples
