@@ -4,9 +4,11 @@
 // Per sub-batch (sized to an HBM budget), the host plans ragged per-track frame ranges and
 // launches:
 //   A  peak/gain, silence RMS, trim                      -> host reads trim bounds (sync 1)
-//   E  key, forked onto the key stream: STFT 8192/512 -> harmonic mask (in place) -> HPCP ->
+//   E  key, forked onto the key stream: STFT 8192/512 (key_stft_frame_size / hop; the tempo
+//      path's frame_size / hop_size without the override) -> harmonic mask (in place) -> HPCP ->
 //      key vote (runs under B-D)
-//   B  energy RMS + energy-flux onsets; STFT 2048/512; frame features; spectral/HFC onsets;
+//   B  energy RMS + energy-flux onsets; STFT 2048/512 (frame_size / hop_size); frame features;
+//      spectral/HFC onsets;
 //      consensus; novelty (5 variants); FFT + ACF tempograms; candidate scoring + gate
 //                                                        -> host reads estimates (sync 2)
 //   C  escalation for ambiguous tracks: STFT 2048/256 and 2048/1024 of those tracks, the same
@@ -52,6 +54,15 @@ static int base_stride(int fs) {
     if (fs == 2048) return STRIDE2;
     if (fs == 8192) return STRIDE8;
     return (fs / 2 + 1 + 3) & ~3;
+}
+// the key spectrogram's frame size and hop (src/lib.rs:985-1009): the override's, else the tempo
+// path's frame_size / hop_size (whose spectrogram the reference reuses; the engine recomputes it
+// on the key stream, bit-identical by the STFT spec)
+static uint64_t key_fft(const sdsp_config& c) {
+    return c.enable_key_stft_override ? std::max<uint64_t>(c.key_stft_frame_size, 256) : c.frame_size;
+}
+static uint64_t key_hop(const sdsp_config& c) {
+    return c.enable_key_stft_override ? std::max<uint64_t>(c.key_stft_hop_size, 1) : c.hop_size;
 }
 constexpr int SUPPORT_HMAX = 8;
 
@@ -224,9 +235,9 @@ void band_bins(int B, float fres, float fmin, float fmax, int* lo, int* hi) {
 
 // estimate_tuning_offset_semitones_from_spectrogram over [80, 2000] Hz (src/lib.rs:1101-1109,
 // extractor.rs:98-140): the band is every bin with fmin <= f <= fmax
-TuningParams tuning_params(const sdsp_config& c, uint32_t sr, int B, float fres) {
+TuningParams tuning_params(const sdsp_config& c, uint32_t sr, int B, float fres, int stride) {
     TuningParams t{};
-    t.stride = STRIDE8;
+    t.stride = stride;
     const float fmin = sd_maxf(80.0f, 20.0f);
     const float fmax = sd_clampf(2000.0f, fmin + 1.0f, (float)sr / 2.0f);
     t.lo = 1;
@@ -249,10 +260,10 @@ TuningParams tuning_params(const sdsp_config& c, uint32_t sr, int B, float fres)
 
 // k_chroma parameters: mode 0 frame_to_chroma_tuned (extractor.rs:393-481), mode 1 the
 // log-frequency conversion (extractor.rs:701-828, fmin 100, fmax 5000 from src/lib.rs:1068-1073)
-ChromaParams chroma_params(const sdsp_config& c, uint32_t sr, int mode, int B, float fres) {
+ChromaParams chroma_params(const sdsp_config& c, uint32_t sr, int mode, int B, float fres, int stride) {
     ChromaParams p{};
     p.B = B;
-    p.stride = STRIDE8;
+    p.stride = stride;
     p.fres = fres;
     p.soft = c.soft_chroma_mapping ? 1 : 0;
     p.sigma = c.soft_mapping_sigma;
@@ -287,10 +298,10 @@ ChromaParams chroma_params(const sdsp_config& c, uint32_t sr, int mode, int B, f
 }
 
 // k_hpcp_x parameters (extractor.rs:529-680 with whitening, :1154-1244 bass blend)
-HpcpXParams hpcp_x_params(const sdsp_config& c, uint32_t sr, int B, float fres, bool whiten) {
+HpcpXParams hpcp_x_params(const sdsp_config& c, uint32_t sr, int B, float fres, bool whiten, int stride) {
     HpcpXParams h{};
     h.B = B;
-    h.stride = STRIDE8;
+    h.stride = stride;
     h.fres = fres;
     h.fmin = sd_maxf(100.0f, 20.0f);
     h.fmax = sd_minf(5000.0f, (float)sr / 2.0f);
@@ -325,10 +336,10 @@ HpcpXParams hpcp_x_params(const sdsp_config& c, uint32_t sr, int B, float fres, 
 
 // harmonic_spectrogram_hpss_median_mask's band and windows (extractor.rs:1400-1420, with
 // fmin 100 / fmax 5000 from src/lib.rs:1014-1024); nb = 0 when the band is empty
-KeyHpssParams key_hpss_params(const sdsp_config& c, uint32_t sr, int B, float fres) {
+KeyHpssParams key_hpss_params(const sdsp_config& c, uint32_t sr, int B, float fres, int stride) {
     KeyHpssParams k{};
     k.B = B;
-    k.stride = STRIDE8;
+    k.stride = stride;
     const float fmin = sd_maxf(100.0f, 20.0f);
     const float fmax = sd_clampf(5000.0f, fmin + 1.0f, (float)sr / 2.0f);
     int64_t bs = sd_f2i64(__builtin_floorf(fmin / fres)), be = sd_f2i64(__builtin_ceilf(fmax / fres));
@@ -346,18 +357,19 @@ KeyHpssParams key_hpss_params(const sdsp_config& c, uint32_t sr, int B, float fr
 // Configuration support that depends on the sample rate.
 std::string unsupported_sr(const sdsp_config& c, uint32_t sr) {
     if (sr == 0) return "";
-    const int B8 = 8192 / 2 + 1;
-    const float fres = (float)sr / 8192.0f;
+    const int kfs = (int)std::min<uint64_t>(key_fft(c), STFT_GEN_MAX);
+    const int B8 = kfs / 2 + 1, ks = base_stride(kfs);
+    const float fres = (float)sr / (float)kfs;
     if (c.enable_key_log_frequency) {
-        const ChromaParams p = chroma_params(c, sr, 1, B8, fres);
+        const ChromaParams p = chroma_params(c, sr, 1, B8, fres, ks);
         if (p.n_log <= 0) return "degenerate key log-frequency range (sample rate too low)";
         if ((size_t)(p.hi - p.lo + 1) * sizeof(ChromaBin) > 65536) return "log-frequency chroma band > 3276 bins";
     } else if (c.enable_key_tuning_compensation) {
-        const TuningParams t = tuning_params(c, sr, B8, fres);
+        const TuningParams t = tuning_params(c, sr, B8, fres, ks);
         if (t.hi - t.lo + 1 > 4096) return "tuning band > 4096 bins";
     }
     if (!c.enable_key_log_frequency && !c.enable_key_hpcp) {
-        const ChromaParams p = chroma_params(c, sr, 0, B8, fres);
+        const ChromaParams p = chroma_params(c, sr, 0, B8, fres, ks);
         if ((size_t)(p.hi - p.lo + 1) * sizeof(ChromaBin) > 65536) return "chroma band > 3276 bins (sample rate too low)";
     }
     return "";
@@ -545,9 +557,9 @@ std::string unsupported(const sdsp_config& c, uint32_t sr) {
     if (c.enable_tempogram_mel_novelty && std::max<uint64_t>(c.tempogram_mel_n_mels, 4) > (uint64_t)FT_MELMAX)
         return "tempogram_mel_n_mels > 48";
     if (c.tempogram_mel_max_filter_bins > 16) return "tempogram_mel_max_filter_bins > 16";
-    if (!c.enable_key_stft_override || std::max<uint64_t>(c.key_stft_frame_size, 256) != 8192)
-        return "key STFT other than 8192";
-    if (c.key_stft_hop_size == 0) return "key_stft_hop_size 0";
+    if (key_fft(c) > (uint64_t)STFT_GEN_MAX || !stft_size_ok((int)key_fft(c)))
+        return "key STFT frame size not a power of two in [256, 16384]";
+    if (c.enable_key_stft_override && c.key_stft_hop_size == 0) return "key_stft_hop_size 0";
     if (c.enable_key_hpss_harmonic && (c.key_hpss_time_margin > 16 || c.key_hpss_freq_margin > 16))
         return "key_hpss_time_margin / key_hpss_freq_margin > 16";
     if (c.key_spectrogram_smooth_margin > 31) return "key_spectrogram_smooth_margin > 31";
@@ -799,7 +811,10 @@ class Pipeline {
           bpm_only_(stages == SDSP_STAGES_BPM_ONLY),
           fs_((int)std::min<uint64_t>(cfg.frame_size, STFT_GEN_MAX)),
           nb_(fs_ / 2 + 1),
-          s2_(base_stride(fs_)) {}
+          s2_(base_stride(fs_)),
+          kfs_((int)std::min<uint64_t>(key_fft(cfg), STFT_GEN_MAX)),
+          khop_((int)std::min<uint64_t>(std::max<uint64_t>(key_hop(cfg), 1), INT32_MAX)),
+          ks_(base_stride(kfs_)) {}
 
     void run(const float* d_samples, const std::vector<uint64_t>& in_off, const std::vector<uint64_t>& n_raw,
              std::vector<TrackRes>& res);
@@ -814,6 +829,8 @@ class Pipeline {
     bool bpm_only_ = false;
     // the tempo path's STFT: frame size (AnalysisConfig::frame_size), bins, row stride
     const int fs_, nb_, s2_;
+    // the key path's STFT: frame size, hop, row stride (key_fft / key_hop)
+    const int kfs_, khop_, ks_;
     sdsp_stage_times times_{};
     // RMS / LUFS: gains (and LUFS status) of every track, folded once for the whole batch
     // before the sub-batches (the fold is a per-track sequential latency, not a throughput)
@@ -874,7 +891,7 @@ void Pipeline::run(const float* d_samples, const std::vector<uint64_t>& in_off, 
         }
         if (const char* e = std::getenv("SDSP_HBM_BUDGET_GB")) budget = std::max(1.0, std::atof(e)) * 1e9;
     }
-    const uint64_t hop = cfg_.hop_size, khop = std::max<uint64_t>(cfg_.key_stft_hop_size, 1);
+    const uint64_t hop = cfg_.hop_size, khop = (uint64_t)khop_;
     std::vector<int> cur;
     double acc = 0;
     auto flush = [&]() {
@@ -894,7 +911,7 @@ void Pipeline::run(const float* d_samples, const std::vector<uint64_t>& in_off, 
     for (size_t i = 0; i < T; i++) {
         if (res[i].status != SDSP_OK) continue;
         const double n = (double)n_raw[i];
-        need[i] = n / hop * (s2_ * 4.0 * 1.3 + 4 * 70.0) + (bpm_only_ ? 0.0 : n / khop * STRIDE8 * 4.0 * ckpt_f) +
+        need[i] = n / hop * (s2_ * 4.0 * 1.3 + 4 * 70.0) + (bpm_only_ ? 0.0 : n / khop * ks_ * 4.0 * ckpt_f) +
                   (n / 256 + n / 1024) * s2_ * 4.0 + 1e6;
         if (cfg_.enable_hpss_onsets || cfg_.enable_tempogram_percussive_fallback)  // H, P ping-pong + a copy
             need[i] += n / hop * s2_ * 4.0 * 5.0;
@@ -1464,7 +1481,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     // stream right after trimming and joined before the results are read back: its
     // bandwidth-bound STFT/mask/HPCP kernels run under the latency-bound tempo and beat
     // kernels of the main stream.
-    const int KFS = 8192, KHOP = (int)std::max<uint64_t>(cfg_.key_stft_hop_size, 1);
+    const int KFS = kfs_, KHOP = khop_;
     std::vector<int> K;  // positions in R
     std::vector<uint64_t> kpfx(1, 0), ktile(1, 0), kseg(1, 0), ksrc;
     std::vector<float> kgain;
@@ -1543,13 +1560,13 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         for (int k = 0; k < NK; k++) kid[(size_t)k] = k;
         d_kid = c_.up(EP + "kid", kid);
         FftTables& t8 = d_.tables(KFS, true);
-        mags8 = c_.dev<float>("E.mags8", total8 * STRIDE8);
+        mags8 = c_.dev<float>("E.mags8", total8 * ks_);
         // uploads above were queued on the main stream: order the key stream after them
         kt.mark(7);
         SDSP_HIP_CHECK(hipStreamWaitEvent(st2, kt.ev[7], 0));
         kt.mark(0, sk);
-        launch_stft(KFS, false, d_samples, d_kpfx, NK, total8, d_ksrc, d_kgain, KHOP, t8.window.as<float>(), t8.stft_tw.as<cx>(),
-                    t8.stft_rt.as<cx>(), mags8, d_kpfx, STRIDE8, nullptr, sk, d_kstr, kstr.back(),
+        launch_stft(KFS, false, d_samples, d_kpfx, NK, total8, d_ksrc, d_kgain, KHOP, t8.window.as<float>(),
+                    stft_twp(t8, KFS, false), stft_rtp(t8, KFS, false), mags8, d_kpfx, ks_, nullptr, sk, d_kstr, kstr.back(),
                     c_.dev<uint32_t>("E.redo", total8 + 1));
         SDSP_HIP_CHECK(hipGetLastError());
         kt.mark(1, sk);
@@ -1567,13 +1584,13 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         const bool plain_hpcp = !use_log && cfg_.enable_key_hpcp && !tuned && !whiten && !cfg_.enable_key_hpcp_bass_blend;
         const bool fuse_mask = std::getenv("SDSP_KEY_FUSE") != nullptr && !cfg_.enable_key_hpss_harmonic &&
                                cfg_.enable_key_harmonic_mask && plain_hpcp && !cfg_.enable_key_beat_synchronous &&
-                               mask_fused_ok(B8, STRIDE8, (int)std::min<uint64_t>(cfg_.key_spectrogram_smooth_margin, 1 << 20),
+                               mask_fused_ok(B8, ks_, (int)std::min<uint64_t>(cfg_.key_spectrogram_smooth_margin, 1 << 20),
                                              cfg_.key_harmonic_mask_power,
                                              (int)std::max<uint64_t>(std::min<uint64_t>(cfg_.key_hpcp_peaks_per_frame, 1 << 20), 1));
         if (fuse_mask) {
             // the mask runs in launch_hpcp_masked below
         } else if (cfg_.enable_key_hpss_harmonic) {
-            const KeyHpssParams kh = key_hpss_params(cfg_, sr_, B8, fres8);
+            const KeyHpssParams kh = key_hpss_params(cfg_, sr_, B8, fres8, ks_);
             if (kh.nb > 0) {  // an empty band returns the spectrogram unchanged (extractor.rs:1408-1410)
                 std::vector<uint64_t> moff(1, 0), mt(1, 0), at(1, 0);
                 for (int k = 0; k < NK; k++) {
@@ -1594,14 +1611,14 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
                 launch_key_hpss(mags8, d_kpfx, d_mt, mt.back(), d_at, at.back(), d_moff, d_kid, NK, kh, d_kmask, st2);
             }
         } else if (cfg_.enable_key_harmonic_mask)
-            launch_mask(mags8, STRIDE8, B8, d_kpfx, d_kid, NK, (int)cfg_.key_spectrogram_smooth_margin,
+            launch_mask(mags8, ks_, B8, d_kpfx, d_kid, NK, (int)cfg_.key_spectrogram_smooth_margin,
                         cfg_.key_harmonic_mask_power, st2);
         else if (cfg_.enable_key_spectrogram_time_smoothing)
-            launch_mask(mags8, STRIDE8, B8, d_kpfx, d_kid, NK, (int)cfg_.key_spectrogram_smooth_margin,
+            launch_mask(mags8, ks_, B8, d_kpfx, d_kid, NK, (int)cfg_.key_spectrogram_smooth_margin,
                         cfg_.key_harmonic_mask_power, st2, true);
         // tuning offset per track (:1097-1119)
         if (tuned) {
-            TuningParams tp = tuning_params(cfg_, sr_, B8, fres8);
+            TuningParams tp = tuning_params(cfg_, sr_, B8, fres8, ks_);
             d_tune = c_.dev<float>("E.tune", (size_t)NK);
             launch_tuning(mags8, d_kpfx, d_kid, NK, tp, d_tune, st2);
             SDSP_HIP_CHECK(hipGetLastError());
@@ -1609,15 +1626,15 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         float* d_chroma = c_.dev<float>("E.chroma", total8 * 12);
         float* d_energy = c_.dev<float>("E.energy", total8);
         if (use_log) {  // :1120-1131
-            const ChromaParams cp = chroma_params(cfg_, sr_, 1, B8, fres8);
+            const ChromaParams cp = chroma_params(cfg_, sr_, 1, B8, fres8, ks_);
             launch_chroma(1, mags8, d_kpfx, d_ktile, d_kid, NK, ktile.back(), cp, nullptr, d_chroma, d_energy, st2);
         } else if (cfg_.enable_key_hpcp && (d_tune || whiten || cfg_.enable_key_hpcp_bass_blend)) {  // :1133-1168
-            const HpcpXParams hx = hpcp_x_params(cfg_, sr_, B8, fres8, whiten);
+            const HpcpXParams hx = hpcp_x_params(cfg_, sr_, B8, fres8, whiten, ks_);
             launch_hpcp_x(mags8, d_kpfx, d_ktile, d_kid, NK, ktile.back(), hx, d_tune, d_chroma, d_energy, st2);
         } else if (cfg_.enable_key_hpcp) {
             HpcpParams hp{};
             hp.B = B8;
-            hp.stride = STRIDE8;
+            hp.stride = ks_;
             hp.pk_lo = 1;
             hp.pk_hi = 0;
             band_bins(B8, fres8, sd_maxf(100.0f, 20.0f), sd_minf(5000.0f, (float)sr_ / 2.0f), &hp.pk_lo, &hp.pk_hi);
@@ -1638,13 +1655,13 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
                 float* d_ckpt = c_.dev<float>("E.kckpt", kspfx.back() * KEY_CKPT_STRIDE);
                 kt.mark(11);  // the segment prefix upload is on the main stream
                 SDSP_HIP_CHECK(hipStreamWaitEvent(st2, kt.ev[11], 0));
-                launch_hpcp_masked(mags8, STRIDE8, d_kpfx, d_ktile, d_kspfx, d_ckpt, d_kid, NK, ktile.back(), hp, d_ht,
+                launch_hpcp_masked(mags8, ks_, d_kpfx, d_ktile, d_kspfx, d_ckpt, d_kid, NK, ktile.back(), hp, d_ht,
                                    d_chroma, d_energy, st2);
             } else {
                 launch_hpcp(mags8, d_kpfx, d_ktile, d_kid, NK, ktile.back(), hp, d_ht, d_chroma, d_energy, st2);
             }
         } else {  // :1169-1197 (the tuned variant only when |offset| > 1e-6)
-            const ChromaParams cp = chroma_params(cfg_, sr_, 0, B8, fres8);
+            const ChromaParams cp = chroma_params(cfg_, sr_, 0, B8, fres8, ks_);
             launch_chroma(0, mags8, d_kpfx, d_ktile, d_kid, NK, ktile.back(), cp, d_tune, d_chroma, d_energy, st2);
         }
         SDSP_HIP_CHECK(hipGetLastError());
@@ -2167,7 +2184,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         const int NS = (int)sel.size();
         if (NS > 0) {
             const uint64_t total8 = kpfx.back();
-            ChromaParams cp = chroma_params(cfg_, sr_, 0, B8, fres8);
+            ChromaParams cp = chroma_params(cfg_, sr_, 0, B8, fres8, ks_);
             cp.gate_small = 0;  // extract_beat_synchronous_chroma takes the offset as is
             float* fc = c_.dev<float>("E.bs_fc", total8 * 12);
             float* fe = c_.dev<float>("E.bs_fe", total8);
