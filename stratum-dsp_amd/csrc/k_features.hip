@@ -8,9 +8,12 @@
 //   MEL[m][t] = sum_k L_t[k] * w_{k,m}  (HTK triangles, bins ascending)               MelFilterbank::apply_logmag :174-190
 //   with L = ln(1 + max(X, 0)), v in {full, low, mid, high}.
 //
-// Each workgroup owns FT_FRAMES consecutive frames of one track, one thread per frame, so
+// Each workgroup owns FT_STEP consecutive frames of one track, one thread per frame, so
 // every per-frame fold runs in exactly the reference's bin order (bit-identical to the CPU
-// restatement).  Bins are streamed through two circular LDS windows of W columns (slot =
+// restatement).  Each wave covers 63 frames in lanes 1-63; lane 0 is a helper holding the frame
+// before the wave's first.  The spectral flux needs X/max of every frame twice (as frame t and as
+// frame t-1 of the next); each lane divides its own frame's bins once and takes the previous
+// frame's quotients from lane - 1 (DPP wave shift), halving the per-bin IEEE divisions.  Bins are streamed through two circular LDS windows of W columns (slot =
 // bin mod W): raw magnitudes and their logs.  Each step loads the CW bins K ahead of the
 // ones it processes (coalesced row segments, log computed once per element), so the
 // SuperFlux max filter over [b-K, b+K] of the previous frame always finds its halo resident
@@ -41,7 +44,7 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
                                                         float* __restrict__ SFO, float* __restrict__ MEL,
                                                         uint64_t total) {
     static_assert((W & (W - 1)) == 0, "W must be a power of two");
-    constexpr int ROWS = FT_FRAMES + 1;
+    constexpr int ROWS = FT_STEP + 1;
     constexpr int LS = W + 1;
     __shared__ float Mt[ROWS][LS];
     __shared__ float Lt[ROWS][LS];
@@ -52,11 +55,14 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
     const uint64_t gb = blockIdx.x;
     const int trk = find_track(tile_pfx, T, gb);
     const int64_t F = (int64_t)(frame_pfx[trk + 1] - frame_pfx[trk]);
-    const int64_t f0 = (int64_t)(gb - tile_pfx[trk]) * FT_FRAMES;
+    const int64_t f0 = (int64_t)(gb - tile_pfx[trk]) * FT_STEP;
     const uint64_t g0 = frame_pfx[trk];
     const int i = threadIdx.x;
-    const int64_t f = f0 + i;
-    const bool valid = f < F;
+    const bool helper = (i & 63) == 0;
+    const int ro = 63 * (i >> 6) + (i & 63);  // this lane's row; row r <-> frame f0 - 1 + r
+    const int64_t f = f0 - 1 + ro;
+    const bool own_ok = f >= 0 && f < F;
+    const bool valid = !helper && f < F;  // ro >= 1 here, so f >= 0
     const bool has_prev = valid && f >= 1;
     const int K = KK > 0 ? KK : P.K, B = P.B;
     const uint64_t g = g0 + (uint64_t)f;
@@ -96,11 +102,10 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
         const uint64_t r = row_of(fr, &odd);
         return odd ? rm.fmaxB[r] : rm.fmaxA[r];
     };
-    const float mx_c = valid ? fmax_of(f) : 0.0f;
-    const float mx_p = has_prev ? fmax_of(f - 1) : 0.0f;
-    const bool cn = mx_c > EPS, pn = mx_p > EPS;
+    const float mx_c = own_ok ? fmax_of(f) : 0.0f;
+    const bool cn = mx_c > EPS;
 
-    // rows f0-1 .. f0+FT_FRAMES-1 of the track; row r <-> frame f0-1+r
+    // rows f0-1 .. f0+FT_STEP-1 of the track; row r <-> frame f0-1+r
     const int64_t r_lo = f0 >= 1 ? 0 : 1;
     const int64_t r_hi = F - f0 + 1 < ROWS ? F - f0 + 1 : ROWS;  // rows [r_lo, r_hi) exist
     const int sub = i / CW, jj = i % CW;
@@ -165,14 +170,14 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
         float Rw[KK > 0 ? CW + 2 * KK : 1];
         if (KK > 0 && has_prev) {
 #pragma unroll
-            for (int q = 0; q < (KK > 0 ? CW + 2 * KK : 1); q++) Rw[q] = Lt[i][(c0 - KK + q) & (W - 1)];
+            for (int q = 0; q < (KK > 0 ? CW + 2 * KK : 1); q++) Rw[q] = Lt[ro - 1][(c0 - KK + q) & (W - 1)];
         }
 #pragma unroll
         for (int j = 0; j < CW; j++) {
             if (j >= nb) break;
             const int b = c0 + j;
             const int s = b & (W - 1);
-            const float m = Mt[i + 1][s];
+            const float m = Mt[ro][s];
             const float ee = m * m;
             const float hh = (float)b * m * m;
             e[0] += ee;
@@ -186,7 +191,12 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
                 eb += ee;
                 hb += hh;
             }
-            const float lc = Lt[i + 1][s];
+            const float lc = Lt[ro][s];
+            // X/max of this lane's frame, and of the previous frame from lane - 1 (its frame is
+            // f - 1 for every lane that reads it: lanes 1-63; the helper's value is unused)
+            const float cv = cn ? m / mx_c : 0.0f;
+            const float pv = __builtin_bit_cast(
+                float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, cv), 0x138 /* wave_shr:1 */, 0xf, 0xf, false));
 #ifndef SDSP_EXP_FT_NOMEL
             if (P.n_mels > 0) {
 #else
@@ -212,14 +222,6 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
                 }
             }
             if (has_prev) {
-                const float mp = Mt[i][s];
-#ifdef SDSP_EXP_FT_NODIV
-                const float pv = pn ? mp * mx_p : 0.0f;
-                const float cv = cn ? m * mx_c : 0.0f;
-#else
-                const float pv = pn ? mp / mx_p : 0.0f;
-                const float cv = cn ? m / mx_c : 0.0f;
-#endif
                 const float d = max_bnn(cv - pv, 0.0f);
                 so += d * d;
                 // SuperFlux, full band window [b-K, b+K] clipped to [0, B).  Every L >= +0 and
@@ -237,7 +239,7 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
 #pragma unroll
                     for (int q = 1; q <= 2 * KK; q++) pm = max_bnn(pm, Rw[j + q]);
                 } else {
-                    for (int q = lo; q < hi; q++) pm = max_bnn(pm, Lt[i][q & (W - 1)]);  // L is never NaN
+                    for (int q = lo; q < hi; q++) pm = max_bnn(pm, Lt[ro - 1][q & (W - 1)]);  // L is never NaN
                 }
                 const float df = max_bnn(lc - pm, 0.0f);
                 const float df2 = df * df;
@@ -253,7 +255,7 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
                             for (int q = 0; q <= 2 * KK; q++)
                                 if (b - KK + q >= lb && b - KK + q < hbd) pmb = max_bnn(pmb, Rw[j + q]);
                         } else {
-                            for (int q = lb; q < hbd; q++) pmb = max_bnn(pmb, Lt[i][q & (W - 1)]);
+                            for (int q = lb; q < hbd; q++) pmb = max_bnn(pmb, Lt[ro - 1][q & (W - 1)]);
                         }
                         const float db = max_bnn(lc - pmb, 0.0f);
                         sb += db * db;

@@ -30,6 +30,9 @@ struct MelPlan {
 };
 constexpr int PK_CH = 16384;  // samples per k_peak_abs workgroup
 constexpr int FT_FRAMES = 256;
+// frames per k_features tile: lane 0 of each wave is a helper that computes the normalised
+// magnitudes of the frame before the wave's first (k_features.hip)
+constexpr int FT_STEP = FT_FRAMES - FT_FRAMES / 64;
 // Where k_features finds frame f of item k: row (f even ? A : B) r0 + (f >> 1) * step, with
 // rB0 = rowB0[k] or rowA0[k] + offB.  Compact spectrogram: A = B, rowA0 = frame prefix, offB = 1,
 // steps 2.  The escalation hops reuse the hop-512 rows: hop 1024 frame v is hop-512 frame 2v;

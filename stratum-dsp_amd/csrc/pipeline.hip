@@ -1078,7 +1078,7 @@ void Pipeline::tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPa
         const uint64_t n = in.n_trim[(size_t)t];
         const uint64_t F = n >= (uint64_t)FS ? (n - FS) / (uint64_t)hop + 1 : 0;
         o.fpfx[(size_t)t + 1] = o.fpfx[(size_t)t] + F;
-        tpfx[(size_t)t + 1] = tpfx[(size_t)t] + (F + FT_FRAMES - 1) / FT_FRAMES;
+        tpfx[(size_t)t + 1] = tpfx[(size_t)t] + (F + FT_STEP - 1) / FT_STEP;
         o.active_h[(size_t)t] = F >= 2;
     }
     const uint64_t total = o.fpfx[(size_t)P_T];
