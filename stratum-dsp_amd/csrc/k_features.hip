@@ -168,9 +168,25 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
         if (__builtin_amdgcn_ballot_w64(valid) == 0) continue;
         // KK > 0: previous frame's L for bins [c0 - KK, c0 + CW + KK) (0 outside [0, B))
         float Rw[KK > 0 ? CW + 2 * KK : 1];
+        // with 2 KK = CW, the window maxima over [j, j + 2 KK] of Rw, j < CW, split at CW into a
+        // suffix max of Rw[j..CW) and a prefix max of Rw[CW..j+2KK] (exact: max is a selection,
+        // and every L >= +0): 3 CW - 2 max operations instead of 2 KK CW
+        constexpr bool VHK = KK > 0 && 2 * KK == CW;
+        float Wm[VHK ? CW : 1];
         if (KK > 0 && has_prev) {
 #pragma unroll
             for (int q = 0; q < (KK > 0 ? CW + 2 * KK : 1); q++) Rw[q] = Lt[ro - 1][(c0 - KK + q) & (W - 1)];
+            if constexpr (VHK) {
+                float suf[CW], pre[CW];
+                suf[CW - 1] = Rw[CW - 1];
+#pragma unroll
+                for (int q = CW - 2; q >= 0; q--) suf[q] = max_bnn(Rw[q], suf[q + 1]);
+                pre[0] = Rw[CW];
+#pragma unroll
+                for (int q = 1; q < CW; q++) pre[q] = max_bnn(pre[q - 1], Rw[CW + q]);
+#pragma unroll
+                for (int q = 0; q < CW; q++) Wm[q] = max_bnn(suf[q], pre[q]);
+            }
         }
 #pragma unroll
         for (int j = 0; j < CW; j++) {
@@ -235,9 +251,13 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
 #else
                 if constexpr (KK > 0) {
 #endif
-                    pm = Rw[j];
+                    if constexpr (VHK) {
+                        pm = Wm[j];
+                    } else {
+                        pm = Rw[j];
 #pragma unroll
-                    for (int q = 1; q <= 2 * KK; q++) pm = max_bnn(pm, Rw[j + q]);
+                        for (int q = 1; q <= 2 * KK; q++) pm = max_bnn(pm, Rw[j + q]);
+                    }
                 } else {
                     for (int q = lo; q < hi; q++) pm = max_bnn(pm, Lt[ro - 1][q & (W - 1)]);  // L is never NaN
                 }
