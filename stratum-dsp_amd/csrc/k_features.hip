@@ -173,9 +173,12 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
         // and every L >= +0): 3 CW - 2 max operations instead of 2 KK CW
         constexpr bool VHK = KK > 0 && 2 * KK == CW;
         float Wm[VHK ? CW : 1];
-        if (KK > 0 && has_prev) {
+        // every lane walks the flux terms (no divergent branch per bin); lanes without a previous
+        // frame read row max(ro - 1, 0) and their sums are never stored
+        const int rp = ro > 0 ? ro - 1 : 0;
+        if (KK > 0) {
 #pragma unroll
-            for (int q = 0; q < (KK > 0 ? CW + 2 * KK : 1); q++) Rw[q] = Lt[ro - 1][(c0 - KK + q) & (W - 1)];
+            for (int q = 0; q < (KK > 0 ? CW + 2 * KK : 1); q++) Rw[q] = Lt[rp][(c0 - KK + q) & (W - 1)];
             if constexpr (VHK) {
                 float suf[CW], pre[CW];
                 suf[CW - 1] = Rw[CW - 1];
@@ -225,19 +228,19 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
                     accB = 0.0f;
                     mA++;
                 }
-                // novelty.rs:181-186 skips v <= 0; adding +0 to a non-negative sum is exact
-                if (lc > 0.0f) {
-                    if (mp.w0 != 0.0f) {
-                        if (mp.s0 == 0) accA += lc * mp.w0;
-                        else accB += lc * mp.w0;
-                    }
-                    if (mp.w1 != 0.0f) {
-                        if (mp.s1 == 0) accA += lc * mp.w1;
-                        else accB += lc * mp.w1;
-                    }
+                // novelty.rs:181-186 skips v <= 0.  Here v = lc >= +0 always (sd_maxf maps NaN to 0,
+                // as f32::max), so the skipped terms are +0 * w = +0, and adding +0 to a
+                // non-negative sum is exact: no per-lane branch
+                if (mp.w0 != 0.0f) {
+                    if (mp.s0 == 0) accA += lc * mp.w0;
+                    else accB += lc * mp.w0;
+                }
+                if (mp.w1 != 0.0f) {
+                    if (mp.s1 == 0) accA += lc * mp.w1;
+                    else accB += lc * mp.w1;
                 }
             }
-            if (has_prev) {
+            {
                 const float d = max_bnn(cv - pv, 0.0f);
                 so += d * d;
                 // SuperFlux, full band window [b-K, b+K] clipped to [0, B).  Every L >= +0 and
@@ -259,7 +262,7 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
                         for (int q = 1; q <= 2 * KK; q++) pm = max_bnn(pm, Rw[j + q]);
                     }
                 } else {
-                    for (int q = lo; q < hi; q++) pm = max_bnn(pm, Lt[ro - 1][q & (W - 1)]);  // L is never NaN
+                    for (int q = lo; q < hi; q++) pm = max_bnn(pm, Lt[rp][q & (W - 1)]);  // L is never NaN
                 }
                 const float df = max_bnn(lc - pm, 0.0f);
                 const float df2 = df * df;
@@ -275,7 +278,7 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
                             for (int q = 0; q <= 2 * KK; q++)
                                 if (b - KK + q >= lb && b - KK + q < hbd) pmb = max_bnn(pmb, Rw[j + q]);
                         } else {
-                            for (int q = lb; q < hbd; q++) pmb = max_bnn(pmb, Lt[ro - 1][q & (W - 1)]);
+                            for (int q = lb; q < hbd; q++) pmb = max_bnn(pmb, Lt[rp][q & (W - 1)]);
                         }
                         const float db = max_bnn(lc - pmb, 0.0f);
                         sb += db * db;
