@@ -191,6 +191,44 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
                 for (int q = 0; q < CW; q++) Wm[q] = max_bnn(suf[q], pre[q]);
             }
         }
+        if constexpr (VHK) {
+            // fast chunk (most bins: above the mel and sub-band ranges, or inside one band away
+            // from its edges): the same per-bin arithmetic with the band and mel bookkeeping
+            // hoisted to the chunk, so the walk issues no scalar work per bin
+            const int cf = P.chunk_flags[c0 / CW];
+            if (cf & FT_CHUNK_FAST) {
+                const int vbc = cf & 3;
+                if (vbc != cur) {
+                    flush();
+                    cur = vbc;
+                }
+#pragma unroll
+                for (int j = 0; j < CW; j++) {
+                    const int b = c0 + j;
+                    const int s = b & (W - 1);
+                    const float m = Mt[ro][s];
+                    const float ee = m * m;
+                    const float hh = (float)b * m * m;
+                    e[0] += ee;
+                    h[0] += hh;
+                    const float lc = Lt[ro][s];
+                    const float cv = cn ? m / mx_c : 0.0f;
+                    const float pv = __builtin_bit_cast(
+                        float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, cv), 0x138, 0xf, 0xf, false));
+                    const float d = max_bnn(cv - pv, 0.0f);
+                    so += d * d;
+                    const float df = max_bnn(lc - Wm[j], 0.0f);
+                    const float df2 = df * df;
+                    sx[0] += df2;
+                    if (vbc) {
+                        eb += ee;
+                        hb += hh;
+                        sb += df2;
+                    }
+                }
+                continue;
+            }
+        }
 #pragma unroll
         for (int j = 0; j < CW; j++) {
             if (j >= nb) break;

@@ -19,7 +19,12 @@ struct FeatParams {
     int bs[4], be[4];  // band [start, end) for v = full, low, mid, high
     int band_on[4];    // variant enabled (full always)
     int n_mels;
+    // per 8-bin chunk of k_features<8, 16, 4> (host-built, feat_chunk_flags): bits 0-1 the band
+    // of every bin of the chunk, bit 2 = FT_CHUNK_FAST (one band, no band-edge clipping of the
+    // SuperFlux window, no mel work, full chunk)
+    const int* chunk_flags;
 };
+constexpr int FT_CHUNK_FAST = 4;
 // per-bin mel accumulation plan (k_features): flush `nflush` finished mels before the bin,
 // then, in the reference's contribution order, add L*w0 to accumulator s0 and L*w1 to s1
 // (accumulator 0 = mel mA, 1 = mel mA+1; w = 0 means no contribution)

@@ -1172,6 +1172,34 @@ void Pipeline::tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPa
     std::vector<MelPlan> mplan = mel_plan(mt, B, &merr);
     if (!merr.empty()) throw HipError(merr);
     MelPlan* d_mplan = c_.up(tag + "melplan", mplan);
+    // k_features' per-chunk flags (8-bin chunks of the <8, 16, 4> walk; see FeatParams)
+    {
+        auto band_of = [&](int b) {
+            int v = 0;
+            for (int q = 3; q >= 1; q--)
+                if (fp.band_on[q] && b >= fp.bs[q] && b < fp.be[q]) v = q;
+            return v;
+        };
+        std::vector<int> cf((size_t)(B + 7) / 8 + 1, 0);
+        for (int c0 = 0; c0 < B; c0 += 8) {
+            const int v0 = band_of(c0);
+            bool fast = fp.K == 4 && c0 + 8 <= B;
+            for (int b = c0; fast && b < c0 + 8; b++) {
+                const int v = band_of(b);
+                if (v != v0) fast = false;
+                if (v) {
+                    const int lo = b - fp.K < 0 ? 0 : b - fp.K, hi = b + fp.K + 1 < B ? b + fp.K + 1 : B;
+                    if (lo < fp.bs[v] || hi > fp.be[v]) fast = false;
+                }
+                if (fp.n_mels > 0) {
+                    const MelPlan& q = mplan[(size_t)b];
+                    if (q.nflush != 0 || q.w0 != 0.0f || q.w1 != 0.0f) fast = false;
+                }
+            }
+            cf[(size_t)c0 / 8] = v0 | (fast ? FT_CHUNK_FAST : 0);
+        }
+        fp.chunk_flags = c_.up(tag + "ftchunk", cf);
+    }
     o.E = c_.dev<float>(tag + "E", 4 * total);
     o.H = c_.dev<float>(tag + "H", 4 * total);
     o.SFX = c_.dev<float>(tag + "SFX", 4 * total);
