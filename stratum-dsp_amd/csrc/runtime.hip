@@ -3,6 +3,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <utility>
 #include <vector>
 
 #include "../../include/sdsp_fft_spec.h"
@@ -31,6 +32,7 @@ DeviceCtx& device_ctx(int device) {
         int lo = 0, hi = 0;
         SDSP_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
         if (std::getenv("SDSP_EQUAL_PRIORITY")) lo = hi = 0;
+        if (std::getenv("SDSP_KEY_PRIORITY")) std::swap(lo, hi);  // experiment: the key stream first
         SDSP_HIP_CHECK(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi));
         // SDSP_KEY_CU_FRAC=f (experiment): the key stream runs on a fixed fraction f of the CUs,
         // spread evenly over CU ids, and the main stream on the rest
