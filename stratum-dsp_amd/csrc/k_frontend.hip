@@ -11,6 +11,8 @@
 // The normalised signal is never materialised: every consumer reads raw*gain (one f32
 // multiply, exactly the value the reference stores in place).
 #include "block_utils.hpp"
+#include <cstdlib>
+
 #include "kernels.hpp"
 
 namespace sdsp {
@@ -659,9 +661,119 @@ __global__ __launch_bounds__(256) void k_frame_rms(const float* __restrict__ x,
     rms[g] = len > 0 ? __builtin_sqrtf(sum / (float)len) : 0.0f;
 }
 
+// Frame RMS as a stream (the default when fs = G * hop, G in {1, 2, 4, 8}, hop a multiple of 32):
+// one lane owns RUN = 4 G consecutive frames of a track and reads their samples once, in order
+// (RUN 4 G: the shortest run whose (G - 1) / RUN re-read stays small; 8 and 16 measured best for
+// the trim (G = 2) and energy (G = 4) passes against 8 / 16 / 32);
+// G frames are in progress at any sample, each in its own accumulator, and every sample's
+// square is added to all G of them.  Frame j is reset when its first hop-segment starts and
+// stored after its G-th, so each accumulator is the frame's own sequential fold in sample order
+// (bit-identical to k_frame_rms, which re-reads every sample G times from L2; its overlap
+// re-reads mostly miss L2, 33 % hits).  Samples past the track's end load as 0 and add +0.
+template <int G>
+__global__ __launch_bounds__(256) void k_frame_rms_run(const float* __restrict__ x, const uint64_t* __restrict__ src_off,
+                                                       const float* __restrict__ gain, const uint64_t* __restrict__ n_len,
+                                                       const uint64_t* __restrict__ frame_pfx, int T, uint64_t total,
+                                                       int fs, int hop, float* __restrict__ rms) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    constexpr int RUN = 4 * G;
+    const uint64_t u0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * RUN;
+    if (u0 >= total) return;
+    const uint64_t u1 = u0 + RUN < total ? u0 + RUN : total;
+    uint64_t g = u0;
+    int trk = find_track(frame_pfx, T, g);
+    while (g < u1) {  // one piece per track the run touches
+        while (g >= frame_pfx[trk + 1]) trk++;
+        const uint64_t f0 = g - frame_pfx[trk];
+        const uint64_t gend = u1 < frame_pfx[trk + 1] ? u1 : frame_pfx[trk + 1];
+        const int nf = (int)(gend - g);
+        const uint64_t n = n_len[trk];
+        const uint64_t s0 = f0 * (uint64_t)hop;  // the piece's first sample (track-relative)
+        const uint64_t a0 = src_off[trk] + s0;   // its float index in x
+        const int d = (int)(a0 & 3u);
+        const uint64_t blk0 = (a0 - (uint64_t)d) >> 2;
+        const uint64_t last = (src_off[trk] + (n > 0 ? n - 1 : 0)) >> 2;  // last block holding a sample
+        const int64_t ls = (int64_t)(n - s0);                               // samples left in the track
+        const f4* q = reinterpret_cast<const f4*>(x);
+        const float gn = gain[trk];
+        float acc[G];
+#pragma unroll
+        for (int r = 0; r < G; r++) acc[r] = 0.0f;
+        auto load = [&](uint64_t bi) { return q[bi < last ? bi : last]; };
+        // the piece's samples as one stream of 16-B blocks (stream position p of block element e:
+        // 4 (block - blk0) + e - d), 8 blocks per step with the next 8 in flight; every hop / 32
+        // steps a segment ends: frame sg - G is stored and frame sg starts in its accumulator
+        const int nseg = nf + G - 1;
+        const int spseg = hop >> 5;  // 8-block steps per segment
+        f4 buf[9];
+#pragma unroll
+        for (int e = 0; e < 9; e++) buf[e] = load(blk0 + (uint64_t)e);
+        uint64_t bi = blk0 + 9;
+        for (int sg = 0; sg <= nseg; sg++) {
+#pragma unroll
+            for (int r = 0; r < G; r++) {
+                if (sg % G != r) continue;  // wave-uniform
+                if (sg >= G && sg - G < nf) {
+                    const uint64_t fj = f0 + (uint64_t)(sg - G);
+                    const uint64_t st = fj * (uint64_t)hop;
+                    const uint64_t en = st + (uint64_t)fs < n ? st + (uint64_t)fs : n;
+                    const int len = en > st ? (int)(en - st) : 0;
+                    rms[frame_pfx[trk] + fj] = len > 0 ? __builtin_sqrtf(acc[r] / (float)len) : 0.0f;
+                }
+                acc[r] = 0.0f;
+            }
+            if (sg == nseg) break;
+            const int64_t p0 = (int64_t)sg * hop;
+            if (p0 >= ls) continue;  // past the track: every remaining term is +0
+            for (int c = 0; c < spseg; c++) {
+                f4 nb[8];
+#pragma unroll
+                for (int e = 0; e < 8; e++) nb[e] = load(bi + (uint64_t)e);
+#pragma unroll
+                for (int e = 0; e < 8; e++) {
+                    const f4 cur = buf[e], nxt = buf[e + 1];
+                    float v[4];
+                    v[0] = d == 0 ? cur.x : d == 1 ? cur.y : d == 2 ? cur.z : cur.w;
+                    v[1] = d == 0 ? cur.y : d == 1 ? cur.z : d == 2 ? cur.w : nxt.x;
+                    v[2] = d == 0 ? cur.z : d == 1 ? cur.w : d == 2 ? nxt.x : nxt.y;
+                    v[3] = d == 0 ? cur.w : d == 1 ? nxt.x : d == 2 ? nxt.y : nxt.z;
+                    const int64_t pk = p0 + 32 * c + 4 * e;
+#pragma unroll
+                    for (int w = 0; w < 4; w++) {
+                        const float y = (pk + w < ls ? v[w] : 0.0f) * gn;
+                        const float yy = y * y;
+#pragma unroll
+                        for (int t = 0; t < G; t++) acc[t] += yy;
+                    }
+                }
+                buf[0] = buf[8];
+#pragma unroll
+                for (int e = 0; e < 8; e++) buf[e + 1] = nb[e];
+                bi += 8;
+            }
+        }
+        g = gend;
+    }
+}
+
 void launch_frame_rms(const float* x, const uint64_t* src_off, const float* gain, const uint64_t* n_len,
                       const uint64_t* frame_pfx, int T, uint64_t total, int fs, int hop, float* rms, hipStream_t st) {
     if (total == 0) return;
+    static const bool per_frame = std::getenv("SDSP_RMS_PER_FRAME") != nullptr;  // A/B: k_frame_rms
+    const int G = hop > 0 && fs % hop == 0 ? fs / hop : 0;
+    if (!per_frame && hop % 32 == 0 && (G == 1 || G == 2 || G == 4 || G == 8)) {
+        const uint64_t per_wg = 256 * 4 * (uint64_t)G;  // frames per workgroup: 256 lanes x RUN
+        const dim3 grid((unsigned)((total + per_wg - 1) / per_wg));
+        if (G == 1)
+            hipLaunchKernelGGL(k_frame_rms_run<1>, grid, dim3(256), 0, st, x, src_off, gain, n_len, frame_pfx, T, total, fs, hop, rms);
+        else if (G == 2)
+            hipLaunchKernelGGL(k_frame_rms_run<2>, grid, dim3(256), 0, st, x, src_off, gain, n_len, frame_pfx, T, total, fs, hop, rms);
+        else if (G == 4)
+            hipLaunchKernelGGL(k_frame_rms_run<4>, grid, dim3(256), 0, st, x, src_off, gain, n_len, frame_pfx, T, total, fs, hop, rms);
+        else
+            hipLaunchKernelGGL(k_frame_rms_run<8>, grid, dim3(256), 0, st, x, src_off, gain, n_len, frame_pfx, T, total, fs, hop, rms);
+        return;
+    }
     hipLaunchKernelGGL(k_frame_rms, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, x, src_off, gain, n_len,
                        frame_pfx, T, total, fs, hop, rms);
 }
