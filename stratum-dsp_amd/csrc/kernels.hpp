@@ -252,7 +252,7 @@ void launch_loudness_gain(const float* x, const uint64_t* in_off, const uint64_t
                           int T, uint64_t n_chunks, unsigned int* peak_bits, const LoudnessParams& P, float* gain,
                           int* status, hipStream_t st);
 void launch_frame_rms(const float* x, const uint64_t* src_off, const float* gain, const uint64_t* n_len,
-                      const uint64_t* frame_pfx, int T, uint64_t total, int fs, int hop, float* rms, hipStream_t st);
+                      const uint64_t* frame_pfx, int T, uint64_t total, int fs, int hop, float* rms, hipStream_t st, bool per_frame_kernel = false);
 void launch_trim(const float* rms, const uint64_t* frame_pfx, int T, const uint64_t* n_raw, int hop, float thr,
                  uint64_t min_frames, int enable, uint64_t* trim_start, uint64_t* trim_end, hipStream_t st);
 void launch_energy_onsets(const float* rms, const uint64_t* frame_pfx, const uint64_t* n_trim, int hop, float factor,

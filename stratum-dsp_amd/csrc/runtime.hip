@@ -1,5 +1,6 @@
 // runtime.hip — device contexts, FFT tables, C ABI housekeeping (config defaults, result
 // ownership, version) and stage probes.  The analyze pipeline itself is in pipeline.hip.
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -7,6 +8,7 @@
 #include <vector>
 
 #include "../../include/sdsp_fft_spec.h"
+#include "kernels.hpp"
 #include "sdsp_runtime.hpp"
 
 namespace sdsp {
@@ -385,6 +387,51 @@ int32_t sdsp_debug_stft(const float* host_x, uint64_t n, uint64_t nfft, uint64_t
         return SDSP_OK;
     } catch (const std::exception& e) {
         std::fprintf(stderr, "sdsp_debug_stft: %s\n", e.what());
+        return SDSP_ERR_PROCESSING;
+    }
+}
+
+// Stage probe: frame RMS (k_frame_rms_run / k_frame_rms) of n_tracks host tracks packed in one
+// buffer (track t = host_x[offs[t] .. offs[t] + lens[t])), frames of fs samples every hop, the
+// silence-trimming framing (a track shorter than fs has one frame of its length).  Writes the
+// frames of all tracks in order to host_out (sum of frame counts).  per_frame = 1 forces the
+// per-frame kernel.
+int32_t sdsp_debug_frame_rms(const float* host_x, uint64_t n_total, const uint64_t* offs, const uint64_t* lens,
+                             const float* gains, uint64_t n_tracks, uint64_t fs, uint64_t hop, int32_t per_frame,
+                             float* host_out, int32_t device) {
+    try {
+        if (n_tracks == 0 || fs == 0 || hop == 0 || fs > (1u << 20) || hop > (1u << 20)) return SDSP_ERR_INVALID_INPUT;
+        for (uint64_t t = 0; t < n_tracks; t++)
+            if (offs[t] + lens[t] > n_total) return SDSP_ERR_INVALID_INPUT;
+        DeviceCtx& c = device_ctx(device);
+        std::lock_guard<std::mutex> lk(c.mu);
+        SDSP_HIP_CHECK(hipSetDevice(device));
+        std::vector<uint64_t> pfx(n_tracks + 1, 0);
+        for (uint64_t t = 0; t < n_tracks; t++) {
+            const uint64_t n = lens[t];
+            pfx[t + 1] = pfx[t] + (n >= fs ? (n - fs) / hop + 1 : (n > 0 ? 1 : 0));
+        }
+        const uint64_t total = pfx[n_tracks];
+        DevBuf x, p, o, l, g, out;
+        x.ensure(std::max<uint64_t>(n_total, 1) * 4);
+        p.ensure(pfx.size() * 8);
+        o.ensure(n_tracks * 8);
+        l.ensure(n_tracks * 8);
+        g.ensure(n_tracks * 4);
+        out.ensure(std::max<uint64_t>(total, 1) * 4);
+        if (n_total) SDSP_HIP_CHECK(hipMemcpy(x.p, host_x, n_total * 4, hipMemcpyHostToDevice));
+        SDSP_HIP_CHECK(hipMemcpy(p.p, pfx.data(), pfx.size() * 8, hipMemcpyHostToDevice));
+        SDSP_HIP_CHECK(hipMemcpy(o.p, offs, n_tracks * 8, hipMemcpyHostToDevice));
+        SDSP_HIP_CHECK(hipMemcpy(l.p, lens, n_tracks * 8, hipMemcpyHostToDevice));
+        SDSP_HIP_CHECK(hipMemcpy(g.p, gains, n_tracks * 4, hipMemcpyHostToDevice));
+        launch_frame_rms(x.as<float>(), o.as<uint64_t>(), g.as<float>(), l.as<uint64_t>(), p.as<uint64_t>(),
+                         (int)n_tracks, total, (int)fs, (int)hop, out.as<float>(), c.stream, per_frame != 0);
+        SDSP_HIP_CHECK(hipGetLastError());
+        SDSP_HIP_CHECK(hipStreamSynchronize(c.stream));
+        if (total) SDSP_HIP_CHECK(hipMemcpy(host_out, out.p, total * 4, hipMemcpyDeviceToHost));
+        return SDSP_OK;
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "sdsp_debug_frame_rms: %s\n", e.what());
         return SDSP_ERR_PROCESSING;
     }
 }

@@ -64,6 +64,10 @@ def lib():
         L.sdsp_last_stage_times.restype = C.c_int32
         L.sdsp_debug_stft.argtypes = [fp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_float, fp, fp, C.c_int32]
         L.sdsp_debug_stft.restype = C.c_int32
+        u64p = C.POINTER(C.c_uint64)
+        L.sdsp_debug_frame_rms.argtypes = [fp, C.c_uint64, u64p, u64p, fp, C.c_uint64, C.c_uint64, C.c_uint64,
+                                           C.c_int32, fp, C.c_int32]
+        L.sdsp_debug_frame_rms.restype = C.c_int32
         L.sdsp_device_count.restype = C.c_int32
         L.sdsp_device_malloc.argtypes = [C.c_int32, C.c_uint64, C.POINTER(C.c_void_p)]
         L.sdsp_device_free.argtypes = [C.c_int32, C.c_void_p]
@@ -307,6 +311,25 @@ def device_count():
 def synchronize(device=0):
     if lib().sdsp_device_synchronize(device) != 0:
         raise RuntimeError("sdsp_device_synchronize failed")
+
+
+def debug_frame_rms(tracks, gains, fs, hop, per_frame=False, device=0):
+    """Frame RMS of each track (silence-trimming framing), concatenated over tracks."""
+    arrs = [np.ascontiguousarray(t, dtype=np.float32) for t in tracks]
+    lens = np.array([a.size for a in arrs], np.uint64)
+    offs = np.zeros(len(arrs), np.uint64)
+    if len(arrs) > 1:
+        offs[1:] = np.cumsum(lens)[:-1]
+    x = np.concatenate(arrs) if arrs else np.zeros(0, np.float32)
+    frames = sum(((int(n) - fs) // hop + 1) if n >= fs else (1 if n > 0 else 0) for n in lens)
+    out = np.empty(max(frames, 1), np.float32)
+    g = np.ascontiguousarray(gains, dtype=np.float32)
+    u64p = C.POINTER(C.c_uint64)
+    st = lib().sdsp_debug_frame_rms(_fp(x), x.size, offs.ctypes.data_as(u64p), lens.ctypes.data_as(u64p), _fp(g),
+                                    len(arrs), fs, hop, 1 if per_frame else 0, _fp(out), device)
+    if st != 0:
+        raise AnalysisError(st, "debug_frame_rms failed")
+    return out[:frames]
 
 
 def debug_stft(x, nfft, hop, gain=1.0, device=0):
