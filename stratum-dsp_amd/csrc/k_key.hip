@@ -702,10 +702,33 @@ __global__ __launch_bounds__(256) void k_key_vote(const int* __restrict__ tracks
     }
     // median smoothing, window 5 (src/lib.rs:1211-1213 -> smoothing.rs:37-94)
     float* cs_all = chroma_s + g0 * 12;
+    // interior frames: the 5 values sorted by odd-even transposition (adjacent compare-exchanges
+    // that swap only when the later value is strictly smaller: a stable sort, so its output equals
+    // the insertion sort's element for element), branch-free; the edges keep the insertion sort
+    auto cx = [](float& a, float& b) {
+        const bool sw = b < a;
+        const float lo = sw ? b : a, hi = sw ? a : b;
+        a = lo;
+        b = hi;
+    };
     for (int64_t q = threadIdx.x; q < F_all * 12; q += blockDim.x) {
-        const int64_t f = q / 12;
-        const int s = (int)(q % 12);
-        if (F_all > 5) {
+        const int64_t f = (int64_t)((uint32_t)q / 12u);  // F_all * 12 < 2^32
+        const int s = (int)((uint32_t)q - 12u * (uint32_t)f);
+        if (F_all > 5 && f >= 2 && f + 2 < F_all) {
+            const float* c = cr + (f - 2) * 12 + s;
+            float v0 = c[0], v1 = c[12], v2 = c[24], v3 = c[36], v4 = c[48];
+#pragma unroll
+            for (int r = 0; r < 5; r++) {
+                if (r % 2 == 0) {
+                    cx(v0, v1);
+                    cx(v2, v3);
+                } else {
+                    cx(v1, v2);
+                    cx(v3, v4);
+                }
+            }
+            cs_all[q] = v2;
+        } else if (F_all > 5) {
             float v[5];
             int n = 0;
             for (int o = -2; o <= 2; o++) {
@@ -811,21 +834,26 @@ __global__ __launch_bounds__(256) void k_key_vote(const int* __restrict__ tracks
         }
         dbg[it].key = key;
     };
+    // Both folds below skip frames of weight <= 0 (detector.rs:992, 351).  Every term is >= +0
+    // (chroma, templates and weights are non-negative), so a skipped frame is folded as +0, which
+    // leaves the sum bit-identical; the loops then carry no branch and their loads pipeline
+    // across frames.
     auto wsd = [&](int64_t f0, int64_t n, int row) {  // weighted_sum_dot, detector.rs:984-1001
         float a = 0.0f;
         const float* t = tpl[row];
+        float tr[12];
+#pragma unroll
+        for (int k = 0; k < 12; k++) tr[k] = t[k];
+#pragma unroll 4
         for (int64_t f = f0; f < f0 + n; f++) {
             const float* c = cs + f * 12;
+            float d = 0.0f;
+#pragma unroll
+            for (int k = 0; k < 12; k++) d += c[k] * tr[k];
             if (use_w) {
                 const float wt = w[f];
-                if (wt > 0.0f) {
-                    float d = 0.0f;
-                    for (int k = 0; k < 12; k++) d += c[k] * t[k];
-                    a += wt * d;
-                }
+                a += wt > 0.0f ? wt * d : 0.0f;
             } else {
-                float d = 0.0f;
-                for (int k = 0; k < 12; k++) d += c[k] * t[k];
                 a += d;
             }
         }
@@ -835,13 +863,11 @@ __global__ __launch_bounds__(256) void k_key_vote(const int* __restrict__ tracks
     auto avg_sum = [&](int64_t f0, int64_t n, int i) {
         if (!use_w && i == 12) return (float)n;
         float a = 0.0f;
+#pragma unroll 4
         for (int64_t f = f0; f < f0 + n; f++) {
             const float wt = use_w ? w[f] : 1.0f;
-            if (use_w && wt <= 0.0f) continue;
-            if (i == 12)
-                a += wt;
-            else
-                a += use_w ? wt * cs[f * 12 + i] : cs[f * 12 + i];
+            const float term = i == 12 ? wt : (use_w ? wt * cs[f * 12 + i] : cs[f * 12 + i]);
+            a += (use_w && wt <= 0.0f) ? 0.0f : term;
         }
         return a;
     };
