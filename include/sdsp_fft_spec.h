@@ -48,6 +48,10 @@
  *     Y = 2^33 X: |X|^2 * 2^66 stays above the subnormal range for any audible input, the range in
  *     which the kernels' fast correctly rounded sqrt is exact, and the scaling itself changes no
  *     rounding (powers of two commute with round-to-nearest away from subnormals);
+ *   - overflow rule: if some fma(Y.re, Y.re, Y.im * Y.im) of a frame is +inf (|X| >= 2^31, e.g.
+ *     unnormalised int-scale PCM), the whole frame is evaluated again with the windowed samples
+ *     times 2^-33 (so Y = X, the reference's own range: extractor.rs:352 overflows only where
+ *     re*re + im*im does) and |X[k]| = sqrt(fma(Y.re, Y.re, Y.im * Y.im));
  * FMA is a single rounding on both sides (gfx950 v_fma_f32 / x86 vfmadd), so the STFT stays
  * bit-identical between the CPU restatement and the kernels, at about two thirds of the
  * general section's arithmetic.  tests/test_spec.py checks it against numpy float64 too.

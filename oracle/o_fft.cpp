@@ -169,12 +169,16 @@ static void stft_fft_complex(std::vector<Cx>& x, std::vector<Cx>& y) {
 // component), |X[k]| = 2^-33 * sqrt(fma(Y.re, Y.re, Y.im * Y.im)) (the frame carries the window's
 // 2^32, so Y = 2^33 X); the post twiddles are symmetric,
 // rt[M-k] = (-rt[k].re, rt[k].im) for 0 <= k < M/2.
-static void stft_mag(const float* x, size_t n, float* mag, std::vector<Cx>& z, std::vector<Cx>& tmp) {
+// `post` is 2^-33 for the scaled evaluation and 1 for the overflow rule's (compute_stft); the
+// return value tells whether some fma(Y.re, Y.re, Y.im * Y.im) overflowed to +inf.
+static bool stft_mag(const float* x, size_t n, float* mag, std::vector<Cx>& z, std::vector<Cx>& tmp,
+                     float post = 0x1p-33f) {
     const size_t M = n / 2;
     z.resize(M);
     for (size_t j = 0; j < M; j++) z[j] = {x[2 * j], x[2 * j + 1]};
     stft_fft_complex(z, tmp);
     const std::vector<Cx>& rt = rtwiddles(n);
+    bool ovf = false;
     for (size_t k = 0; k <= M; k++) {
         const Cx Zk = z[k % M];
         const Cx Zr = z[(M - k) % M];
@@ -184,8 +188,11 @@ static void stft_mag(const float* x, size_t n, float* mag, std::vector<Cx>& z, s
         const float dre = Zk.im + Zr.im, dim = -(Zk.re - Zr.re);
         const float yre = std::fma(w.re, dre, std::fma(-w.im, dim, sre));
         const float yim = std::fma(w.re, dim, std::fma(w.im, dre, sim));
-        mag[k] = 0x1p-33f * std::sqrt(std::fma(yre, yre, yim * yim));
+        const float e = std::fma(yre, yre, yim * yim);
+        ovf |= e == INFINITY;
+        mag[k] = post * std::sqrt(e);
     }
+    return ovf;
 }
 
 // extractor.rs:301-359
@@ -205,7 +212,13 @@ Spec compute_stft(const float* s, size_t n_samples, size_t frame_size, size_t ho
     for (size_t f = 0; f < n_frames; f++) {
         const float* fr = s + f * hop;
         for (size_t i = 0; i < frame_size; i++) buf[i] = fr[i] * window[i];
-        stft_mag(buf.data(), frame_size, out.row(f), z, tmp);
+        if (stft_mag(buf.data(), frame_size, out.row(f), z, tmp)) {
+            // the overflow rule (sdsp_fft_spec.h STFT section): some |Y|^2 = 2^66 |X|^2 overflowed,
+            // so the frame is evaluated again in the reference's own range, Y = X
+            // (extractor.rs:352 overflows only where (re*re + im*im) itself does)
+            for (size_t i = 0; i < frame_size; i++) buf[i] = (fr[i] * window[i]) * 0x1p-33f;
+            stft_mag(buf.data(), frame_size, out.row(f), z, tmp, 1.0f);
+        }
     }
     return out;
 }

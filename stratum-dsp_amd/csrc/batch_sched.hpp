@@ -80,13 +80,16 @@ inline size_t run_chunked(size_t n_chunks, std::vector<ChunkDevice>& devs,
                     std::unique_lock<std::mutex> lk(mu);
                     cv.wait(lk, [&] { return ready[s] < 0; });
                 }
+                bool staged = true;
                 try {
                     dv.stage(s, c);
-                } catch (const std::exception& e) {
+                } catch (...) {  // any exception type: a std::thread must not let one escape
+                    staged = false;
+                }
+                if (!staged) {
                     // this device cannot stage: hand the chunk back and stop copying for it
                     std::lock_guard<std::mutex> lk(fmu);
                     orphans.push_back(c);
-                    (void)e;
                     break;
                 }
                 {
@@ -112,10 +115,19 @@ inline size_t run_chunked(size_t n_chunks, std::vector<ChunkDevice>& devs,
                 if (ready[s] < 0) break;  // copier finished and nothing staged
                 c = ready[s];
             }
+            std::string why;
+            bool ok = true;
             try {
                 dv.analyze(s, (size_t)c);
             } catch (const std::exception& e) {
-                fail_one((size_t)c, e.what());
+                ok = false;
+                why = e.what();
+            } catch (...) {
+                ok = false;
+                why = "unknown exception";
+            }
+            if (!ok) {
+                fail_one((size_t)c, why);
                 try {
                     if (dv.drain) dv.drain();
                 } catch (...) {
@@ -150,12 +162,22 @@ inline size_t run_chunked(size_t n_chunks, std::vector<ChunkDevice>& devs,
             } catch (const std::exception& e) {
                 why = e.what();
                 continue;
+            } catch (...) {
+                why = "unknown exception";
+                continue;
             }
+            bool threw = false;
             try {
                 dv.analyze(0, c);
                 ok = true;
             } catch (const std::exception& e) {
                 why = e.what();
+                threw = true;
+            } catch (...) {
+                why = "unknown exception";
+                threw = true;
+            }
+            if (threw) {
                 try {
                     if (dv.drain) dv.drain();
                 } catch (...) {

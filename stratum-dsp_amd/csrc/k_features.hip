@@ -139,11 +139,7 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
             const int r = sub + u * RSTEP;
             if (r < ROWS) {
                 Mt[r][slot] = nx[u];
-#ifdef SDSP_EXP_FT_NOLOG
-                Lt[r][slot] = nx[u] * 0.5f;
-#else
                 Lt[r][slot] = sd_logf_ge1(1.0f + sd_maxf(nx[u], 0.0f), ltab);
-#endif
             }
         }
     };
@@ -229,8 +225,7 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
                 continue;
             }
         }
-#pragma unroll
-        for (int j = 0; j < CW; j++) {
+        for (int j = 0; j < CW; j++) {  // not unrolled: the early exit keeps it a loop
             if (j >= nb) break;
             const int b = c0 + j;
             const int s = b & (W - 1);
@@ -254,11 +249,7 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
             const float cv = cn ? m / mx_c : 0.0f;
             const float pv = __builtin_bit_cast(
                 float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, cv), 0x138 /* wave_shr:1 */, 0xf, 0xf, false));
-#ifndef SDSP_EXP_FT_NOMEL
             if (P.n_mels > 0) {
-#else
-            if (false) {
-#endif
                 const MelPlan mp = mel[b];
                 for (int q = 0; q < mp.nflush; q++) {
                     if (valid) MEL[(uint64_t)mA * total + g] = accA;
@@ -287,11 +278,7 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
                 const int lo = b - K < 0 ? 0 : b - K;
                 const int hi = b + K + 1 < B ? b + K + 1 : B;
                 float pm = 0.0f;
-#ifdef SDSP_EXP_FT_NOSF
-                if (false) {
-#else
                 if constexpr (KK > 0) {
-#endif
                     if constexpr (VHK) {
                         pm = Wm[j];
                     } else {

@@ -653,7 +653,6 @@ __global__ __launch_bounds__(256) void k_frame_rms(const float* __restrict__ x,
             }
             j += RMS_U;
             if (!more) break;
-#pragma unroll
             for (int u = 0; u < RMS_U; u++) cur[u] = nxt[u];
         }
     }
@@ -760,8 +759,7 @@ void launch_frame_rms(const float* x, const uint64_t* src_off, const float* gain
                       const uint64_t* frame_pfx, int T, uint64_t total, int fs, int hop, float* rms, hipStream_t st,
                       bool per_frame_kernel) {
     if (total == 0) return;
-    static const bool per_frame_env = std::getenv("SDSP_RMS_PER_FRAME") != nullptr;  // A/B: k_frame_rms
-    const bool per_frame = per_frame_kernel || per_frame_env;
+    const bool per_frame = per_frame_kernel;  // the debug probe selects the per-frame kernel
     const int G = hop > 0 && fs % hop == 0 ? fs / hop : 0;
     if (!per_frame && hop % 32 == 0 && (G == 1 || G == 2 || G == 4 || G == 8)) {
         const uint64_t per_wg = 256 * 4 * (uint64_t)G;  // frames per workgroup: 256 lanes x RUN

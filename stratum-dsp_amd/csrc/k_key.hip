@@ -330,163 +330,6 @@ __global__ __launch_bounds__(HP_FRAMES) SDSP_HPCP_ATTR void k_hpcp(const float* 
 }
 
 // ----------------------------------------------------------------------------------------
-// Harmonic time mask fused into the HPCP pass (the default key path: margin M = 12, power 2).
-//
-// The mask of frame t needs the per-bin prefix P[j] = x[0] + ... + x[j-1], folded in frame
-// order from the start of the track (extractor.rs:1276-1279), at j = t+M+1 and t-M.  That fold
-// is sequential per bin, but it is a plain recursion: started from the exact value P[j0], the
-// walk P[j+1] = P[j] + x[j] reproduces every later prefix bit for bit.  So:
-//  * k_mask_ckpt streams each track's raw spectrogram once, one lane per 4 bins, and stores the
-//    checkpoints C[s] = P[KM_SEG s - M] (s >= 1; C[0] = 0 = the prefix of the frames before the
-//    track, which contribute x = 0);
-//  * k_hpcp_masked stages, per 16-bin chunk, the raw rows f0-M .. f0+HP_FRAMES+M-1 of its tile
-//    in LDS (rows outside the track as 0, which leaves a prefix unchanged), and thread
-//    (segment sg, column jj) walks the KM_SEG + 2M prefixes of its segment from C[sg] and masks
-//    its KM_SEG frames (mask_elem, the same arithmetic as k_mask_r) into the tile the HPCP walk
-//    reads.
-// The masked spectrogram is never written: per track the key path reads the raw spectrogram
-// twice (253.8 MB each, plus the halo rows and 1/16 of a row per frame of checkpoints) instead
-// of reading it twice and writing it once (k_mask_r in place, then k_hpcp).
-constexpr int KM_SEG = KEY_CKPT_SEG;      // frames per mask segment (one checkpoint each)
-constexpr int KM_CKS = KEY_CKPT_STRIDE;   // checkpoint row stride in floats (covers 16-bin chunks of 4097 bins)
-static_assert(HP_FRAMES == KM_SEG * HP_CW, "one mask segment per (segment, column) thread");
-
-template <int M>
-__global__ __launch_bounds__(64) void k_mask_ckpt(const float* __restrict__ mags, int stride, int B,
-                                                  const uint64_t* __restrict__ frame_pfx,
-                                                  const uint64_t* __restrict__ seg_pfx, const int* __restrict__ tracks,
-                                                  int blocks_per_track, float* __restrict__ ckpt) {
-    typedef float f4 __attribute__((ext_vector_type(4)));
-    static_assert(M >= 1 && M < KM_SEG, "one checkpoint per segment, M < KM_SEG");
-    const int it = blockIdx.x / blocks_per_track;
-    const int trk = tracks[it];
-    const int b = ((blockIdx.x % blocks_per_track) * 64 + (int)threadIdx.x) * 4;  // bins b .. b+3
-    const int64_t F = (int64_t)(frame_pfx[trk + 1] - frame_pfx[trk]);
-    if (b >= B || F <= 0) return;
-    // b + 3 may pass B - 1 (the last group): those lanes fold the rows' padding columns, which
-    // stay inside the row stride, and their checkpoints are never read
-    const f4* col = reinterpret_cast<const f4*>(mags + frame_pfx[trk] * (uint64_t)stride + b);
-    const uint64_t rs = (uint64_t)stride / 4;
-    f4* ck = reinterpret_cast<f4*>(ckpt + seg_pfx[it] * (uint64_t)KM_CKS + b);
-    constexpr uint64_t cks = KM_CKS / 4;
-    const int64_t NS = (F + KM_SEG - 1) / KM_SEG;
-    f4 P = {0.0f, 0.0f, 0.0f, 0.0f};
-    ck[0] = P;
-    // block s covers frames [KM_SEG (s-1) - M, KM_SEG s - M); after it P = C[s].  The next
-    // block's KM_SEG rows are loaded while this one is folded.
-    f4 cur[KM_SEG], nxt[KM_SEG];
-    auto load = [&](int64_t s, f4 (&v)[KM_SEG]) {
-        const int64_t j0 = KM_SEG * (s - 1) - M;
-#pragma unroll
-        for (int u = 0; u < KM_SEG; u++) {
-            const int64_t j = j0 + u;
-            v[u] = j >= 0 ? col[(uint64_t)j * rs] : f4{0.0f, 0.0f, 0.0f, 0.0f};
-        }
-    };
-    if (NS > 1) load(1, cur);
-    for (int64_t s = 1; s < NS; s++) {
-        if (s + 1 < NS) load(s + 1, nxt);
-#pragma unroll
-        for (int u = 0; u < KM_SEG; u++) P = P + cur[u];  // four independent f32 folds, frame order
-        ck[(uint64_t)s * cks] = P;
-#pragma unroll
-        for (int u = 0; u < KM_SEG; u++) cur[u] = nxt[u];
-    }
-}
-
-template <int KCAP, int M>
-__global__ __launch_bounds__(HP_FRAMES) __attribute__((amdgpu_waves_per_eu(3))) void k_hpcp_masked(const float* __restrict__ mags,
-                                                           const float* __restrict__ ckpt,
-                                                           const uint64_t* __restrict__ frame_pfx,
-                                                           const uint64_t* __restrict__ tile_pfx,
-                                                           const uint64_t* __restrict__ seg_pfx,
-                                                           const int* __restrict__ tracks, int n_items, HpcpParams P,
-                                                           const HarmEntry* __restrict__ harm,
-                                                           float* __restrict__ chroma, float* __restrict__ energy) {
-    constexpr int XR = HP_FRAMES + 2 * M;  // staged raw rows: frames f0-M .. f0+HP_FRAMES+M-1
-    __shared__ float X[XR][HP_CW + 1];
-    __shared__ float tile[HP_FRAMES][HP_CW + 1];
-    // neighbouring tiles share halo rows: keep them on one XCD (its L2)
-    const uint64_t gb = xcd_block(blockIdx.x, gridDim.x);
-    const int it = find_track(tile_pfx, n_items, gb);
-    const int trk = tracks[it];
-    const int64_t F = (int64_t)(frame_pfx[trk + 1] - frame_pfx[trk]);
-    const int64_t f0 = (int64_t)(gb - tile_pfx[it]) * HP_FRAMES;
-    const int i = threadIdx.x;
-    const int64_t f = f0 + i;
-    const bool valid = f < F;
-    const uint64_t g0 = frame_pfx[trk];
-    HpcpFrame<KCAP> hf;
-    hf.init();
-    // staging: thread (sub, jj) loads rows sub + HP_CW u of column jj; the same (sub, jj) is the
-    // mask segment sub (frames t0 .. t0+KM_SEG-1) and its column
-    const int sub = i / HP_CW, jj = i % HP_CW;
-    constexpr int NLD = (XR + HP_CW - 1) / HP_CW;
-    const int64_t t0 = f0 + (int64_t)KM_SEG * sub;
-    const bool seg_ok = t0 < F;
-    const float* ckp = ckpt + (seg_pfx[it] + (uint64_t)(f0 / KM_SEG) + (uint64_t)sub) * (uint64_t)KM_CKS + jj;
-    const float* colp = mags + g0 * (uint64_t)P.stride + jj;
-    float nx[NLD], ckn = 0.0f;
-    auto load_chunk = [&](int c0) {
-        const bool col_ok = c0 + jj < P.B;
-#pragma unroll
-        for (int u = 0; u < NLD; u++) {
-            const int r = sub + u * HP_CW;
-            const int64_t j = f0 - M + r;
-            nx[u] = (r < XR && col_ok && j >= 0 && j < F) ? colp[(uint64_t)j * (uint64_t)P.stride + c0] : 0.0f;
-        }
-        ckn = (seg_ok && col_ok) ? ckp[c0] : 0.0f;
-    };
-    const float inv_w = 1.0f / (float)(2 * M + 1);
-    load_chunk(0);
-    for (int c0 = 0; c0 < P.B; c0 += HP_CW) {
-        __syncthreads();  // the previous chunk's mask and walk are done with X and tile
-#pragma unroll
-        for (int u = 0; u < NLD; u++) {
-            const int r = sub + u * HP_CW;
-            if (r < XR) X[r][jj] = nx[u];
-        }
-        const float ck = ckn;
-        __syncthreads();
-        if (c0 + HP_CW < P.B) load_chunk(c0 + HP_CW);
-        if (seg_ok) {
-            // the prefixes P[t0-M+q], q = 0 .. KM_SEG+2M, of column jj, walked once in frame
-            // order from the checkpoint: the first KM_SEG are kept (the windows' lower ends),
-            // the upper ends P[t+M+1] are taken as the walk passes them.  X row r <-> frame
-            // f0 - M + r, so frame t0 - M + q is row KM_SEG sub + q.
-            const float* xc = &X[KM_SEG * sub][jj];
-            constexpr int XS = HP_CW + 1;
-            float lo[KM_SEG];
-            float p = ck;
-#pragma unroll
-            for (int q = 0; q < KM_SEG; q++) {
-                lo[q] = p;
-                p = p + xc[q * XS];
-            }
-#pragma unroll
-            for (int q = KM_SEG; q < 2 * M + 1; q++) p = p + xc[q * XS];
-#pragma unroll
-            for (int o = 0; o < KM_SEG; o++) {  // p = P[t+M+1], t = t0 + o
-                const int64_t t = t0 + o;
-                if (t < F) {
-                    const int64_t st = t >= M ? t - M : 0;
-                    const int64_t en = t + M + 1 < F ? t + M + 1 : F;
-                    tile[KM_SEG * sub + o][jj] = mask_elem<M, 2>(p - lo[o], en - st, xc[(o + M) * XS], 2.0f, inv_w);
-                }
-                if (o + 1 < KM_SEG) p = p + xc[(o + 2 * M + 1) * XS];
-            }
-        }
-        __syncthreads();
-        if (!valid) continue;
-        hf.walk(tile[i], c0, P.B - c0 < HP_CW ? P.B - c0 : HP_CW, P);
-    }
-    __syncthreads();
-    static_assert(sizeof(tile) >= sizeof(float) * 12 * HP_FRAMES, "pc fits the tile");
-    if (!valid) return;
-    hf.finish(reinterpret_cast<float(*)[HP_FRAMES]>(&tile[0][0]), i, P, harm, chroma, energy, g0 + (uint64_t)f);
-}
-
-// ----------------------------------------------------------------------------------------
 __device__ void key_from_raw(const float raw[24], float sorted[24], int order[24]) {
     float sc[24];
     for (int k = 0; k < 24; k++) sc[k] = raw[k];
@@ -1090,33 +933,6 @@ void launch_hpcp(const float* mags, const uint64_t* frame_pfx, const uint64_t* t
     else
         hipLaunchKernelGGL(k_hpcp<HP_KMAX>, grid, block, 0, st, mags, frame_pfx, tile_pfx, tracks, n_items, P, harm,
                            chroma, energy);
-}
-// k_mask_ckpt + k_hpcp_masked (margin 12, power 2; mask_fused_ok): seg_pfx = per-item prefix of
-// ceil(F / KM_SEG), ckpt = seg_pfx[n_items] rows of KM_CKS floats
-bool mask_fused_ok(int B, int stride, int margin, float power, int K) {
-    return margin == 12 && sd_maxf(power, 1.0f) == 2.0f && K <= HP_KMAX && B <= KM_CKS && stride % 4 == 0 &&
-           B <= stride;
-}
-void launch_hpcp_masked(const float* mags, int stride, const uint64_t* frame_pfx, const uint64_t* tile_pfx,
-                        const uint64_t* seg_pfx, float* ckpt, const int* tracks, int n_items, uint64_t n_tiles,
-                        const HpcpParams& P, const HarmEntry* harm, float* chroma, float* energy, hipStream_t st) {
-    if (n_items == 0 || n_tiles == 0) return;
-    const int bpt = (P.B + 255) / 256;
-    hipLaunchKernelGGL(k_mask_ckpt<12>, dim3(n_items * bpt), dim3(64), 0, st, mags, stride, P.B, frame_pfx, seg_pfx,
-                       tracks, bpt, ckpt);
-    const dim3 grid((unsigned)n_tiles), block(HP_FRAMES);
-    if (P.K <= 8)
-        hipLaunchKernelGGL((k_hpcp_masked<8, 12>), grid, block, 0, st, mags, ckpt, frame_pfx, tile_pfx, seg_pfx, tracks,
-                           n_items, P, harm, chroma, energy);
-    else if (P.K <= 16)
-        hipLaunchKernelGGL((k_hpcp_masked<16, 12>), grid, block, 0, st, mags, ckpt, frame_pfx, tile_pfx, seg_pfx,
-                           tracks, n_items, P, harm, chroma, energy);
-    else if (P.K <= 24)
-        hipLaunchKernelGGL((k_hpcp_masked<24, 12>), grid, block, 0, st, mags, ckpt, frame_pfx, tile_pfx, seg_pfx,
-                           tracks, n_items, P, harm, chroma, energy);
-    else
-        hipLaunchKernelGGL((k_hpcp_masked<HP_KMAX, 12>), grid, block, 0, st, mags, ckpt, frame_pfx, tile_pfx, seg_pfx,
-                           tracks, n_items, P, harm, chroma, energy);
 }
 void launch_key_vote(const int* tracks, int n_items, const uint64_t* frame_pfx, float* chroma_raw,
                      const float* energy, float* chroma_s, float* weights, float* seg_scratch, const uint64_t* seg_off,

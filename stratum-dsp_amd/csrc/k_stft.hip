@@ -80,19 +80,10 @@ __device__ __forceinline__ void bfly4(c2 a, c2 b, c2 c, c2 d, c2 w1, c2 w2, c2 w
     }
 }
 
-#ifdef SDSP_EXP_NOPAD
-__device__ __forceinline__ int lpad(int i) { return i; }
-#define P17 16
-#define P272 256
-#define PADSHIFT 0
-#define STFT_ATTR __attribute__((amdgpu_waves_per_eu(5, 8)))
-#else
 __device__ __forceinline__ int lpad(int i) { return i + (i >> 4); }
 #define P17 17
 #define P272 272
 #define PADSHIFT 1
-#define STFT_ATTR
-#endif
 
 // Barrier over the threads of one frame: a frame of TPF = 64 threads is one wave, whose LDS
 // operations complete in order, so a wave-scope fence + wave barrier replaces the workgroup
@@ -158,10 +149,6 @@ __device__ __forceinline__ bool sqrt_fast_missed(uint32_t lo, uint32_t hi) {
 // have p = 0, so they carry no products.
 template <bool LAST>
 __device__ __forceinline__ void radix16(c2 v[16], const c2 w[15]) {
-#ifdef SDSP_EXP_NOFFT  // ablation: data movement only
-    for (int k = 0; k < 16; k++) v[k].x += w[k % 15].y;
-    return;
-#endif
     c2 u[16];
 #pragma unroll
     for (int jp = 0; jp < 4; jp++) {
@@ -214,150 +201,140 @@ __device__ __forceinline__ void stft_mag_frame(const float* __restrict__ samples
     const __amdgpu_buffer_rsrc_t rrt = rsrc_of(rtp, 8u * (S::RT_SPECIAL + 4));
     const int vo = 8 * lt;  // every table below is [item][lane] with 8-byte entries
 
-    c2 v[16], w[15];
-    // pass 1 (n = M, s = 1, p' = lt): z[idx] = (x[2idx], x[2idx+1]) * gain * window, idx = lt + TPF k
+    // The overflow rule of the STFT section (sdsp_fft_spec.h): the frame is evaluated with the
+    // window's 2^32 (pre = 1, |X| = 2^-33 sqrt(.)); if some |Y|^2 overflowed to +inf, the whole
+    // frame is evaluated again with the windowed samples times 2^-33 (Y = X, the reference's own
+    // range, src/features/chroma/extractor.rs:352) and |X| = sqrt(.).
+    float pre = 1.0f, post = 0x1p-33f, mx = 0.0f;
+    for (int attempt = 0; attempt < 2; attempt++) {
+        bool ovf = false;
+        c2 v[16], w[15];
+        // pass 1 (n = M, s = 1, p' = lt): z[idx] = (x[2idx], x[2idx+1]) * gain * window, idx = lt + TPF k
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const c2 xs = ld_c2(rx, vo, 8 * TPF * k);
-#ifdef SDSP_EXP_NOTAB  // ablation: no window / twiddle table reads
-        const c2 ws = {1.0f + k, 0.5f};
-#else
-        const c2 ws = ld_c2(rw, vo, 8 * TPF * k);
-#endif
-        v[k] = {(xs.x * gn) * ws.x, (xs.y * gn) * ws.y};
-    }
+        for (int k = 0; k < 16; k++) {
+            const c2 xs = ld_c2(rx, vo, 8 * TPF * k);
+            const c2 ws = ld_c2(rw, vo, 8 * TPF * k);
+            v[k] = {((xs.x * gn) * ws.x) * pre, ((xs.y * gn) * ws.y) * pre};
+        }
 #pragma unroll
-    for (int j = 0; j < 15; j++)
-#ifdef SDSP_EXP_NOTAB
-        w[j] = c2{0.25f * j, 1.0f - 0.5f * j};
-#else
-        w[j] = ld_c2(rtw, vo, 8 * TPF * j);
-#endif
-    radix16<false>(v, w);
-    {
-        const int b0 = P17 * lt;  // lpad(16 lt + k) = 17 lt + k
+        for (int j = 0; j < 15; j++)
+            w[j] = ld_c2(rtw, vo, 8 * TPF * j);
+        radix16<false>(v, w);
+        {
+            const int b0 = P17 * lt;  // lpad(16 lt + k) = 17 lt + k
 #pragma unroll
-        for (int k = 0; k < 16; k++) buf[b0 + k] = v[k];
-    }
-    frame_sync<TPF>();
-    // further radix-16 passes: (n, s) = (M/16, 16), (M/256, 256)
+            for (int k = 0; k < 16; k++) buf[b0 + k] = v[k];
+        }
+        frame_sync<TPF>();
+        // further radix-16 passes: (n, s) = (M/16, 16), (M/256, 256)
 #pragma unroll
-    for (int pass = 1; pass < S::NPASS; pass++) {
-        const int s = pass == 1 ? 16 : 256;
-        const int m1 = (pass == 1 ? M / 16 : M / 256) / 16;  // n / 16
-        const int q = lt % s, pp = pass == 2 ? 0 : lt / s;  // lt < TPF = 256 = s on pass 2
-        // reads x[q + s pp + s m1 k]; s m1 is a multiple of 16, so lpad = lpad(q + s pp) + (17/16) s m1 k
-        const int rb = lpad(q + s * pp), rs = s * m1 + PADSHIFT * (s * m1) / 16;
+        for (int pass = 1; pass < S::NPASS; pass++) {
+            const int s = pass == 1 ? 16 : 256;
+            const int m1 = (pass == 1 ? M / 16 : M / 256) / 16;  // n / 16
+            const int q = lt % s, pp = pass == 2 ? 0 : lt / s;  // lt < TPF = 256 = s on pass 2
+            // reads x[q + s pp + s m1 k]; s m1 is a multiple of 16, so lpad = lpad(q + s pp) + (17/16) s m1 k
+            const int rb = lpad(q + s * pp), rs = s * m1 + PADSHIFT * (s * m1) / 16;
 #pragma unroll
-        for (int j = 0; j < 15; j++) {
-            // pass 1: one entry per p' (TPF/16 of them, shared by 16 lanes); pass 2: p' = 0 for
-            // every lane, so the 15 twiddles are wave-uniform scalar loads
-            if (pass == 1)
-#ifdef SDSP_EXP_NOTAB
-                w[j] = c2{0.125f * j, 1.0f - 0.25f * j};
-#else
-                w[j] = ld_c2(rtw, 8 * pp, 8 * (15 * TPF + j * (TPF / 16)));
-#endif
-            else {
-                const cx t = twp[15 * TPF + 15 * (TPF / 16) + j];
-                w[j] = c2{t.re, t.im};
+            for (int j = 0; j < 15; j++) {
+                // pass 1: one entry per p' (TPF/16 of them, shared by 16 lanes); pass 2: p' = 0 for
+                // every lane, so the 15 twiddles are wave-uniform scalar loads
+                if (pass == 1) {
+                    w[j] = ld_c2(rtw, 8 * pp, 8 * (15 * TPF + j * (TPF / 16)));
+                } else {
+                    const cx t = twp[15 * TPF + 15 * (TPF / 16) + j];
+                    w[j] = c2{t.re, t.im};
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 16; k++) v[k] = buf[rb + rs * k];
+            frame_sync<TPF>();
+            if (pass == 2)
+                radix16<true>(v, w);
+            else
+                radix16<false>(v, w);
+            // writes z[q + 16 s pp + s k]:  s = 16 -> (q + 272 pp) + 17 k;  s = 256 (pp = 0) -> lpad(q) + 272 k
+            if (s == 16) {
+                const int wb = q + P272 * pp;
+#pragma unroll
+                for (int k = 0; k < 16; k++) buf[wb + P17 * k] = v[k];
+            } else {  // s = 256 only for M = 4096 (m1 = 1): z[q + 256 k], lpad = lpad(q) + 272 k
+#pragma unroll
+                for (int k = 0; k < 16; k++) buf[rb + P272 * k] = v[k];
+            }
+            frame_sync<TPF>();
+        }
+        // trailing radix-4 stage (M = 16^2 * 4): n = 4, s = M/4, p = 0 (no products)
+        if constexpr (M == 1024) {
+            constexpr int s = M / 4;
+#pragma unroll
+            for (int r = 0; r < s / TPF; r++) {
+                const int q = lt + TPF * r;
+                const int b = lpad(q);  // lpad(q + j s) = b + 272 j (s = 256)
+                c2 y0, y1, y2, y3;
+                bfly4<false>(buf[b], buf[b + P272], buf[b + 2 * P272], buf[b + 3 * P272], c2{}, c2{}, c2{}, y0, y1, y2, y3);
+                buf[b] = y0;
+                buf[b + P272] = y1;
+                buf[b + 2 * P272] = y2;
+                buf[b + 3 * P272] = y3;
+            }
+            frame_sync<TPF>();
+        }
+        // real-FFT post-processing, |X[k]|, k = 0..M (sdsp_fft_spec.h, STFT section):
+        //   S = Z[k] + conj(Z[M-k]),  D = Z[k] - conj(Z[M-k]),  D' = (D.im, -D.re),
+        //   Y = S + rt[k] D' in FMA form,  |X[k]| = 0.5 * sqrt(fma(Y.re, Y.re, Y.im * Y.im)).
+        // Bins k and M-k read the same pair (Z[k], Z[M-k]); the partner's S and D' are the
+        // conjugates of this bin's (exactly, up to the sign of zero, which |X| cannot see), so each
+        // pair is read and combined once.
+        float* out = mags + (mag_row0[trk] + f) * (uint64_t)stride;
+        mx = 0.0f;
+        auto mag_of = [&](float sx, float sy, float dx, float dy, c2 wt) {  // S = (sx, sy), D' = (dx, dy)
+            const float yx = __builtin_fmaf(wt.x, dx, __builtin_fmaf(-wt.y, dy, sx));
+            const float yy = __builtin_fmaf(wt.x, dy, __builtin_fmaf(wt.y, dx, sy));
+            const float e = __builtin_fmaf(yx, yx, yy * yy);
+            ovf |= e == __builtin_huge_valf();
+            return post * sqrt_cr(e);
+        };
+        auto put = [&](int k, float mag) {
+            if (live) out[k] = mag;
+            if (FRAME_MAX) mx = sd_maxf(mx, mag);
+        };
+        struct SD {
+            float sx, sy, dx, dy;
+        };
+        auto pair_sd = [&](int ik, int ir) {  // LDS indices of Z[k], Z[M-k]
+            const c2 Zk = buf[ik];
+            const c2 Zr = buf[ir];
+            // S = Zk + conj(Zr);  D = Zk - conj(Zr);  D' = (D.im, -D.re)
+            return SD{Zk.x + Zr.x, Zk.y - Zr.y, Zk.y + Zr.y, -(Zk.x - Zr.x)};
+        };
+        c2 wk[S::NPAIR], wm[S::NPAIR];
+#pragma unroll
+        for (int j = 0; j < S::NPAIR; j++) {
+            wk[j] = ld_c2(rrt, vo, 8 * TPF * (2 * j));
+            wm[j] = ld_c2(rrt, vo, 8 * TPF * (2 * j + 1));
+        }
+#pragma unroll
+        for (int j = 0; j < S::NPAIR; j++) {
+            const int k = 1 + lt + TPF * j;  // k < M/2 except possibly on the last j
+            if (j + 1 < S::NPAIR || k < M / 2) {
+                const SD a = pair_sd(lpad(k), lpad(M - k));
+                put(k, mag_of(a.sx, a.sy, a.dx, a.dy, wk[j]));
+                put(M - k, mag_of(a.sx, -a.sy, a.dx, -a.dy, wm[j]));
             }
         }
-#pragma unroll
-        for (int k = 0; k < 16; k++) v[k] = buf[rb + rs * k];
-        frame_sync<TPF>();
-        if (pass == 2)
-            radix16<true>(v, w);
-        else
-            radix16<false>(v, w);
-        // writes z[q + 16 s pp + s k]:  s = 16 -> (q + 272 pp) + 17 k;  s = 256 (pp = 0) -> lpad(q) + 272 k
-        if (s == 16) {
-            const int wb = q + P272 * pp;
-#pragma unroll
-            for (int k = 0; k < 16; k++) buf[wb + P17 * k] = v[k];
-        } else {  // s = 256 only for M = 4096 (m1 = 1): z[q + 256 k], lpad = lpad(q) + 272 k
-#pragma unroll
-            for (int k = 0; k < 16; k++) buf[rb + P272 * k] = v[k];
+        if (lt == 0) {  // k = 0 and k = M both read (Z[0], Z[0]); k = M/2 reads (Z[M/2], Z[M/2])
+            const SD a = pair_sd(0, 0);
+            put(0, mag_of(a.sx, a.sy, a.dx, a.dy, ld_c2(rrt, 0, 8 * S::RT_SPECIAL)));
+            put(M, mag_of(a.sx, a.sy, a.dx, a.dy, ld_c2(rrt, 0, 8 * (S::RT_SPECIAL + 1))));
+        } else if (lt == 1) {
+            const SD a = pair_sd(lpad(M / 2), lpad(M / 2));
+            put(M / 2, mag_of(a.sx, a.sy, a.dx, a.dy, ld_c2(rrt, 0, 8 * (S::RT_SPECIAL + 2))));
         }
-        frame_sync<TPF>();
-    }
-    // trailing radix-4 stage (M = 16^2 * 4): n = 4, s = M/4, p = 0 (no products)
-    if constexpr (M == 1024) {
-        constexpr int s = M / 4;
-#pragma unroll
-        for (int r = 0; r < s / TPF; r++) {
-            const int q = lt + TPF * r;
-            const int b = lpad(q);  // lpad(q + j s) = b + 272 j (s = 256)
-            c2 y0, y1, y2, y3;
-            bfly4<false>(buf[b], buf[b + P272], buf[b + 2 * P272], buf[b + 3 * P272], c2{}, c2{}, c2{}, y0, y1, y2, y3);
-            buf[b] = y0;
-            buf[b + P272] = y1;
-            buf[b + 2 * P272] = y2;
-            buf[b + 3 * P272] = y3;
-        }
-        frame_sync<TPF>();
-    }
-    // real-FFT post-processing, |X[k]|, k = 0..M (sdsp_fft_spec.h, STFT section):
-    //   S = Z[k] + conj(Z[M-k]),  D = Z[k] - conj(Z[M-k]),  D' = (D.im, -D.re),
-    //   Y = S + rt[k] D' in FMA form,  |X[k]| = 0.5 * sqrt(fma(Y.re, Y.re, Y.im * Y.im)).
-    // Bins k and M-k read the same pair (Z[k], Z[M-k]); the partner's S and D' are the
-    // conjugates of this bin's (exactly, up to the sign of zero, which |X| cannot see), so each
-    // pair is read and combined once.
-    float* out = mags + (mag_row0[trk] + f) * (uint64_t)stride;
-    float mx = 0.0f;
-    auto mag_of = [&](float sx, float sy, float dx, float dy, c2 wt) {  // S = (sx, sy), D' = (dx, dy)
-        const float yx = __builtin_fmaf(wt.x, dx, __builtin_fmaf(-wt.y, dy, sx));
-        const float yy = __builtin_fmaf(wt.x, dy, __builtin_fmaf(wt.y, dx, sy));
-#ifdef SDSP_EXP_NOSQRT  // ablation: hardware sqrt, not correctly rounded
-        return 0x1p-33f * __builtin_amdgcn_sqrtf(__builtin_fmaf(yx, yx, yy * yy));
-#else
-        return 0x1p-33f * sqrt_cr(__builtin_fmaf(yx, yx, yy * yy));
-#endif
-    };
-    auto put = [&](int k, float mag) {
-#ifdef SDSP_EXP_NOSTORE  // ablation: no global stores
-        if (live && mag == 1234.5f) out[k] = mag;
-#else
-        if (live) out[k] = mag;
-#endif
-        if (FRAME_MAX) mx = sd_maxf(mx, mag);
-    };
-    struct SD {
-        float sx, sy, dx, dy;
-    };
-    auto pair_sd = [&](int ik, int ir) {  // LDS indices of Z[k], Z[M-k]
-        const c2 Zk = buf[ik];
-        const c2 Zr = buf[ir];
-        // S = Zk + conj(Zr);  D = Zk - conj(Zr);  D' = (D.im, -D.re)
-        return SD{Zk.x + Zr.x, Zk.y - Zr.y, Zk.y + Zr.y, -(Zk.x - Zr.x)};
-    };
-    c2 wk[S::NPAIR], wm[S::NPAIR];
-#pragma unroll
-    for (int j = 0; j < S::NPAIR; j++) {
-#ifdef SDSP_EXP_NOTAB
-        wk[j] = c2{0.3f * j, 0.7f};
-        wm[j] = c2{0.7f, 0.3f * j};
-#else
-        wk[j] = ld_c2(rrt, vo, 8 * TPF * (2 * j));
-        wm[j] = ld_c2(rrt, vo, 8 * TPF * (2 * j + 1));
-#endif
-    }
-#pragma unroll
-    for (int j = 0; j < S::NPAIR; j++) {
-        const int k = 1 + lt + TPF * j;  // k < M/2 except possibly on the last j
-        if (j + 1 < S::NPAIR || k < M / 2) {
-            const SD a = pair_sd(lpad(k), lpad(M - k));
-            put(k, mag_of(a.sx, a.sy, a.dx, a.dy, wk[j]));
-            put(M - k, mag_of(a.sx, -a.sy, a.dx, -a.dy, wm[j]));
-        }
-    }
-    if (lt == 0) {  // k = 0 and k = M both read (Z[0], Z[0]); k = M/2 reads (Z[M/2], Z[M/2])
-        const SD a = pair_sd(0, 0);
-        put(0, mag_of(a.sx, a.sy, a.dx, a.dy, ld_c2(rrt, 0, 8 * S::RT_SPECIAL)));
-        put(M, mag_of(a.sx, a.sy, a.dx, a.dy, ld_c2(rrt, 0, 8 * (S::RT_SPECIAL + 1))));
-    } else if (lt == 1) {
-        const SD a = pair_sd(lpad(M / 2), lpad(M / 2));
-        put(M / 2, mag_of(a.sx, a.sy, a.dx, a.dy, ld_c2(rrt, 0, 8 * (S::RT_SPECIAL + 2))));
+        const bool any = TPF == 64 ? __builtin_amdgcn_ballot_w64(ovf) != 0 : __syncthreads_or(ovf) != 0;
+        if (!any) break;
+        frame_sync<TPF>();  // this attempt's LDS reads are done before the next one's writes
+        pre = 0x1p-33f;
+        post = 1.0f;
     }
     if (FRAME_MAX) {
         if constexpr (TPF == 64) {
@@ -380,7 +357,7 @@ __device__ __forceinline__ void stft_mag_frame(const float* __restrict__ samples
 // kernel's list: redo[0] = count, then global frame indices) it recomputes only the listed frames,
 // grid-striding over the list.
 template <int NFFT, bool FRAME_MAX>
-__global__ __launch_bounds__(256) STFT_ATTR void k_stft_mag(const float* __restrict__ samples,
+__global__ __launch_bounds__(256) void k_stft_mag(const float* __restrict__ samples,
                                                   const uint64_t* __restrict__ frame_pfx, int n_tracks,
                                                   uint64_t total_frames, const uint64_t* __restrict__ src_off,
                                                   const float* __restrict__ gain, int hop,
@@ -430,61 +407,71 @@ __global__ __launch_bounds__(256) void k_stft_gen(int N, const float* __restrict
     const uint64_t f = g - frame_pfx[trk];
     const float gn = gain[trk];
     const float* x = samples + src_off[trk] + f * (uint64_t)hop;
-    c2* a = gen_lds;
-    c2* b = gen_lds + M;
-    for (int j = threadIdx.x; j < M; j += 256)
-        a[j] = c2{(x[2 * j] * gn) * window[2 * j], (x[2 * j + 1] * gn) * window[2 * j + 1]};
-    __syncthreads();
-    // radix-4 stages: (n, s) = (M, 1), (M/4, 4), ...; butterfly u = p s + q
-    int lgs = 0;
-    for (int lgn = lgm; lgn >= 2; lgn -= 2, lgs += 2) {
-        const int s = 1 << lgs, m = 1 << (lgn - 2), tstep = M >> lgn;
-        for (int u = threadIdx.x; u < (M >> 2); u += 256) {
-            const int q = u & (s - 1), p = u >> lgs;
-            c2 y0, y1, y2, y3;
-            const c2 va = a[q + s * p], vb = a[q + s * (p + m)], vc = a[q + s * (p + 2 * m)],
-                     vd = a[q + s * (p + 3 * m)];
-            if (p) {
-                const cx w1 = tw[p * tstep], w2 = tw[2 * p * tstep], w3 = tw[3 * p * tstep];
-                bfly4<true>(va, vb, vc, vd, c2{w1.re, w1.im}, c2{w2.re, w2.im}, c2{w3.re, w3.im}, y0, y1, y2, y3);
-            } else {
-                bfly4<false>(va, vb, vc, vd, c2{}, c2{}, c2{}, y0, y1, y2, y3);
+    // the STFT section's overflow rule (see stft_mag_frame)
+    float pre = 1.0f, post = 0x1p-33f, mx = 0.0f;
+    for (int attempt = 0; attempt < 2; attempt++) {
+        bool ovf = false;
+        c2* a = gen_lds;
+        c2* b = gen_lds + M;
+        for (int j = threadIdx.x; j < M; j += 256)
+            a[j] = c2{((x[2 * j] * gn) * window[2 * j]) * pre, ((x[2 * j + 1] * gn) * window[2 * j + 1]) * pre};
+        __syncthreads();
+        // radix-4 stages: (n, s) = (M, 1), (M/4, 4), ...; butterfly u = p s + q
+        int lgs = 0;
+        for (int lgn = lgm; lgn >= 2; lgn -= 2, lgs += 2) {
+            const int s = 1 << lgs, m = 1 << (lgn - 2), tstep = M >> lgn;
+            for (int u = threadIdx.x; u < (M >> 2); u += 256) {
+                const int q = u & (s - 1), p = u >> lgs;
+                c2 y0, y1, y2, y3;
+                const c2 va = a[q + s * p], vb = a[q + s * (p + m)], vc = a[q + s * (p + 2 * m)],
+                         vd = a[q + s * (p + 3 * m)];
+                if (p) {
+                    const cx w1 = tw[p * tstep], w2 = tw[2 * p * tstep], w3 = tw[3 * p * tstep];
+                    bfly4<true>(va, vb, vc, vd, c2{w1.re, w1.im}, c2{w2.re, w2.im}, c2{w3.re, w3.im}, y0, y1, y2, y3);
+                } else {
+                    bfly4<false>(va, vb, vc, vd, c2{}, c2{}, c2{}, y0, y1, y2, y3);
+                }
+                const int o = q + s * 4 * p;
+                b[o] = y0;
+                b[o + s] = y1;
+                b[o + 2 * s] = y2;
+                b[o + 3 * s] = y3;
             }
-            const int o = q + s * 4 * p;
-            b[o] = y0;
-            b[o + s] = y1;
-            b[o + 2 * s] = y2;
-            b[o + 3 * s] = y3;
+            __syncthreads();
+            c2* t = a;
+            a = b;
+            b = t;
         }
-        __syncthreads();
-        c2* t = a;
-        a = b;
-        b = t;
-    }
-    if (lgm & 1) {  // radix-2 stage: s = M/2
-        const int s = M >> 1;
-        for (int q = threadIdx.x; q < s; q += 256) {
-            const c2 va = a[q], vb = a[q + s];
-            b[q] = c2{va.x + vb.x, va.y + vb.y};
-            b[q + s] = c2{va.x - vb.x, va.y - vb.y};
+        if (lgm & 1) {  // radix-2 stage: s = M/2
+            const int s = M >> 1;
+            for (int q = threadIdx.x; q < s; q += 256) {
+                const c2 va = a[q], vb = a[q + s];
+                b[q] = c2{va.x + vb.x, va.y + vb.y};
+                b[q + s] = c2{va.x - vb.x, va.y - vb.y};
+            }
+            __syncthreads();
+            a = b;
         }
-        __syncthreads();
-        a = b;
-    }
-    // post-processing, k = 0..M (oracle/o_fft.cpp stft_mag)
-    float* out = mags + (mag_row0[trk] + f) * (uint64_t)stride;
-    float mx = 0.0f;
-    for (int k = threadIdx.x; k <= M; k += 256) {
-        const c2 zk = a[k & (M - 1)], zr = a[(M - k) & (M - 1)];
-        const cx r = rt[k > (M >> 1) ? M - k : k];
-        const c2 w = k > (M >> 1) ? c2{-r.re, r.im} : c2{r.re, r.im};
-        const float sre = zk.x + zr.x, sim = zk.y - zr.y;
-        const float dre = zk.y + zr.y, dim = -(zk.x - zr.x);
-        const float yre = __builtin_fmaf(w.x, dre, __builtin_fmaf(-w.y, dim, sre));
-        const float yim = __builtin_fmaf(w.x, dim, __builtin_fmaf(w.y, dre, sim));
-        const float mag = 0x1p-33f * sqrt_cr(__builtin_fmaf(yre, yre, yim * yim));
-        out[k] = mag;
-        if (FRAME_MAX) mx = sd_maxf(mx, mag);
+        // post-processing, k = 0..M (oracle/o_fft.cpp stft_mag)
+        float* out = mags + (mag_row0[trk] + f) * (uint64_t)stride;
+        mx = 0.0f;
+        for (int k = threadIdx.x; k <= M; k += 256) {
+            const c2 zk = a[k & (M - 1)], zr = a[(M - k) & (M - 1)];
+            const cx r = rt[k > (M >> 1) ? M - k : k];
+            const c2 w = k > (M >> 1) ? c2{-r.re, r.im} : c2{r.re, r.im};
+            const float sre = zk.x + zr.x, sim = zk.y - zr.y;
+            const float dre = zk.y + zr.y, dim = -(zk.x - zr.x);
+            const float yre = __builtin_fmaf(w.x, dre, __builtin_fmaf(-w.y, dim, sre));
+            const float yim = __builtin_fmaf(w.x, dim, __builtin_fmaf(w.y, dre, sim));
+            const float e = __builtin_fmaf(yre, yre, yim * yim);
+            ovf |= e == __builtin_huge_valf();
+            const float mag = post * sqrt_cr(e);
+            out[k] = mag;
+            if (FRAME_MAX) mx = sd_maxf(mx, mag);
+        }
+        if (!__syncthreads_or(ovf)) break;
+        pre = 0x1p-33f;
+        post = 1.0f;
     }
     if (FRAME_MAX) {
         mx = wave_max(mx);
@@ -572,6 +559,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     constexpr int PADM = M + PADSHIFT * M / 16;  // padded LDS slots per frame buffer
     static_assert(SH::NPASS > 0 && S >= 1 && S <= 16, "supported: N = 2048, 8192; hop = S * 2 * TPF");
     __shared__ c2 lds[FPB * 2 * PADM];
+    __shared__ uint32_t miss_flag[2];  // N = 8192: frame i's "some wave missed" flag at [i & 1]
 
     const int lt = threadIdx.x % TPF;
     const int fl = threadIdx.x / TPF;
@@ -580,6 +568,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const uint64_t strip =
         (uint64_t)__builtin_amdgcn_readfirstlane((int)((uint64_t)xcd_block(blockIdx.x, gridDim.x) * FPB + fl));
     if (strip >= n_strips) return;  // only whole frame groups: a wave (TPF = 64) or the workgroup (FPB = 1)
+    if (TPF == 256 && threadIdx.x < 2) miss_flag[threadIdx.x] = 0;  // ordered by frame 0's barriers
     const int trk = find_track(strip_pfx, n_tracks, strip);
     const uint64_t F = frame_pfx[trk + 1] - frame_pfx[trk];
     const uint64_t f0 = (strip - strip_pfx[trk]) * (uint64_t)STRIP_T;
@@ -656,6 +645,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
         for (int k = 0; k < 16; k++) bufA[P17 * lt + k] = v[k];
         frame_sync<TPF>();
+        if constexpr (TPF == 256) {
+            // frame i - 1's flag is final (its waves set it before this barrier); cleared before
+            // this frame's second barrier, so before frame i + 1 can set it again
+            if (threadIdx.x == 0 && i > 0 && miss_flag[(i - 1) & 1]) {
+                miss_flag[(i - 1) & 1] = 0;
+                redo[1 + atomicAdd(redo, 1u)] = (uint32_t)(frame_pfx[trk] + f - 1);
+            }
+        }
         // pass 2 (n = M/16, s = 16): A -> B
         {
             constexpr int s2 = 16, m1 = (M / 16) / 16;
@@ -677,19 +674,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         float* out = mags + (mag_row0[trk] + f) * (uint64_t)stride;
         float mx = 0.0f;
         uint32_t lo = 0xFFFFFFFFu, hi = 0u;
-#ifdef SDSP_EXP_NOSQRT
-        auto sq = [&](float yx, float yy) { return 0x1p-33f * __builtin_amdgcn_sqrtf(__builtin_fmaf(yx, yx, yy * yy)); };
-#else
         auto sq = [&](float yx, float yy) { return 0x1p-33f * sqrt_fast(__builtin_fmaf(yx, yx, yy * yy), lo, hi); };
-#endif
         // frame maximum: magnitudes are +0 or positive, so v_max_f32 (IEEE maxNum: a NaN operand
         // yields the other) is sd_maxf here except for the payload of an all-NaN row
         auto put = [&](int k, float mag) {
-#ifdef SDSP_EXP_NOSTORE
-            if (mag == 1234.5f) out[k] = mag;
-#else
             out[k] = mag;
-#endif
             if (FRAME_MAX) mx = __builtin_fmaxf(mx, mag);
         };
         // one pair: own bin k from Zk, partner bin M-k from Zr, post twiddle w = rt[k]
@@ -746,17 +735,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             for (int j = 0; j < 4; j++) pair(Bv[j], B2[3 - j], wk[4 + j], colB + 256 * j);
             if (self0) single(A[2], rtH, M / 2);
         }
-#ifndef SDSP_EXP_NOSQRT
-        // a magnitude^2 of subnormal scale (or inf / NaN) somewhere in the wave: the frame goes on
+        // a magnitude^2 of subnormal scale (or inf / NaN) somewhere in the frame: the frame goes on
         // the redo list, which k_stft_mag recomputes with the general sqrt right after this kernel
-        // (stream order), overwriting the whole row.  A frame may be listed by several waves.
-        if (__builtin_expect(__builtin_amdgcn_ballot_w64(sqrt_fast_missed(lo, hi)) != 0, 0)) {
-            if ((threadIdx.x & 63) == 0) {
-                const uint32_t at = atomicAdd(redo, 1u);
-                redo[1 + at] = (uint32_t)(frame_pfx[trk] + f);
-            }
+        // (stream order), overwriting the whole row.  Each frame is listed at most once, so the
+        // list never holds more entries than the launch has frames: one wave per frame (N = 2048)
+        // appends directly; the 4 waves of an 8192-point frame OR a flag in LDS, which thread 0
+        // reads after the next frame's first barrier (or after the strip) and appends.
+        const bool missed = __builtin_amdgcn_ballot_w64(sqrt_fast_missed(lo, hi)) != 0;
+        if constexpr (TPF == 64) {
+            if (__builtin_expect(missed, 0) && lt == 0) redo[1 + atomicAdd(redo, 1u)] = (uint32_t)(frame_pfx[trk] + f);
+        } else {
+            if (__builtin_expect(missed, 0) && (threadIdx.x & 63) == 0) atomicOr(&miss_flag[i & 1], 1u);
         }
-#endif
         if constexpr (FRAME_MAX) {
             static_assert(!FRAME_MAX || TPF == 64, "frame maxima: one wave per frame");
             mx = wave_max(mx);
@@ -767,6 +757,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int k = 0; k < 16 - S; k++) ring[k] = ring[k + S];
 #pragma unroll
         for (int s2 = 0; s2 < S; s2++) ring[16 - S + s2] = {nxt[s2].x * gn, nxt[s2].y * gn};
+    }
+    if constexpr (TPF == 256) {  // the strip's last frame
+        __syncthreads();
+        if (threadIdx.x == 0 && miss_flag[(nf - 1) & 1]) redo[1 + atomicAdd(redo, 1u)] = (uint32_t)(frame_pfx[trk] + f0 + nf - 1);
     }
 }
 
@@ -865,12 +859,11 @@ void launch_stft(int nfft, bool frame_max, const float* samples, const uint64_t*
         if (!stft_size_ok(nfft)) throw HipError("launch_stft: frame size not a power of two in [64, 16384]");
         if (total_frames > 0xffffffffull) throw HipError("launch_stft: too many frames for one launch");
         const size_t lds = (size_t)8 * (size_t)nfft;  // two buffers of N/2 complex values
-        static bool attr_set[2] = {false, false};
-        if (lds > 65536 && !attr_set[frame_max]) {
+        // set on every large launch: the attribute is per device, and several device workers may
+        // launch at once (a process-wide "done" flag would race and skip the other devices)
+        if (lds > 65536)
             SDSP_HIP_CHECK(hipFuncSetAttribute(frame_max ? (const void*)k_stft_gen<true> : (const void*)k_stft_gen<false>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)(8 * STFT_GEN_MAX)));
-            attr_set[frame_max] = true;
-        }
         if (frame_max)
             hipLaunchKernelGGL(k_stft_gen<true>, dim3((unsigned)total_frames), block, lds, st, nfft, samples, frame_pfx,
                                n_tracks, total_frames, src_off, gain, hop, window, twp, rtp, mags, mag_row0, stride, fmax);

@@ -314,13 +314,6 @@ void launch_beat_sync(const int* tracks, int n_items, const uint64_t* frame_pfx,
 void launch_hpcp(const float* mags, const uint64_t* frame_pfx, const uint64_t* tile_pfx, const int* tracks,
                  int n_items, uint64_t n_tiles, const HpcpParams& P, const HarmEntry* harm, float* chroma,
                  float* energy, hipStream_t st);
-// harmonic time mask fused into the HPCP pass (k_key.hip): prefix checkpoints every KM_SEG
-// frames (seg_pfx = per-item prefix of ceil(F / 16); ckpt = seg_pfx[n_items] rows of 4160 floats)
-constexpr int KEY_CKPT_SEG = 16, KEY_CKPT_STRIDE = 4160;
-bool mask_fused_ok(int B, int stride, int margin, float power, int K);
-void launch_hpcp_masked(const float* mags, int stride, const uint64_t* frame_pfx, const uint64_t* tile_pfx,
-                        const uint64_t* seg_pfx, float* ckpt, const int* tracks, int n_items, uint64_t n_tiles,
-                        const HpcpParams& P, const HarmEntry* harm, float* chroma, float* energy, hipStream_t st);
 void launch_key_vote(const int* tracks, int n_items, const uint64_t* frame_pfx, float* chroma_raw,
                      const float* energy, float* chroma_s, float* weights, float* seg_scratch, const uint64_t* seg_off,
                      const float* tmpl, const KeyParams& P, KeyOut* out, hipStream_t st, KeyDbg* dbg = nullptr);

@@ -40,15 +40,9 @@ namespace {
 
 // Spectrogram row strides (floats; multiples of 4 for 16-B rows).  The key spectrogram's rows
 // are 16 KiB + 256 B apart: at 16 KiB + 16 B the mask's column streams (one 256-B row segment
-// per wave per frame) run 1.5x slower (profiles/README.md, stride sweep).  SDSP_STRIDE2 /
-// SDSP_STRIDE8 override them for layout experiments.
-static int env_stride(const char* name, int dflt, int min) {
-    const char* e = std::getenv(name);
-    const int v = e ? std::atoi(e) : dflt;
-    return v >= min && v % 4 == 0 ? v : dflt;
-}
-static const int STRIDE2 = env_stride("SDSP_STRIDE2", 1028, 1025);  // 1025 bins
-static const int STRIDE8 = env_stride("SDSP_STRIDE8", 4160, 4097);  // 4097 bins
+// per wave per frame) run 1.5x slower (profiles/README.md, stride sweep of round 2).
+constexpr int STRIDE2 = 1028;  // 1025 bins
+constexpr int STRIDE8 = 4160;  // 4097 bins
 // row stride of the tempo path's spectrogram for AnalysisConfig::frame_size (nb = fs/2 + 1 bins)
 static int base_stride(int fs) {
     if (fs == 2048) return STRIDE2;
@@ -842,18 +836,6 @@ class Pipeline {
 
     void sub_batch(const float* d_samples, const std::vector<uint64_t>& in_off, const std::vector<uint64_t>& n_raw,
                    const std::vector<int>& idx, std::vector<TrackRes>& res);
-    // SDSP_KEY_DEFER=1: the key results of a sub-batch are joined late, so its key-stream tail
-    // (mask, HPCP, vote) runs under the next sub-batch's tempo path.  Uploads read by the key
-    // stream and the key output live in per-parity buffers (E0.*, E1.*) for that.
-    struct KeyPending {
-        std::unique_ptr<Timers> kt;
-        KeyOut* d_kout = nullptr;
-        KeyDbg* d_kdbg = nullptr;
-        std::vector<size_t> at;  // result slot of each key track
-    };
-    std::unique_ptr<KeyPending> key_pending_;
-    int sb_parity_ = 0;
-    void finish_key(std::vector<TrackRes>& res);
     void tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPassOut& out);
     void legacy_select(const TempoPassIn& bin, const uint32_t* d_onsets, const uint64_t* d_on_off, const int* d_on_n,
                        const std::vector<int>& R, const std::vector<int>& idx, std::vector<TrackRes>& res,
@@ -907,11 +889,10 @@ void Pipeline::run(const float* d_samples, const std::vector<uint64_t>& in_off, 
     // short last sub-batch runs at a fraction of the chip)
     std::vector<double> need(T, 0.0);
     double total_need = 0;
-    const double ckpt_f = std::getenv("SDSP_KEY_FUSE") ? 1.0 + 1.0 / KEY_CKPT_SEG : 1.0;  // + prefix checkpoints
     for (size_t i = 0; i < T; i++) {
         if (res[i].status != SDSP_OK) continue;
         const double n = (double)n_raw[i];
-        need[i] = n / hop * (s2_ * 4.0 * 1.3 + 4 * 70.0) + (bpm_only_ ? 0.0 : n / khop * ks_ * 4.0 * ckpt_f) +
+        need[i] = n / hop * (s2_ * 4.0 * 1.3 + 4 * 70.0) + (bpm_only_ ? 0.0 : n / khop * ks_ * 4.0) +
                   (n / 256 + n / 1024) * s2_ * 4.0 + 1e6;
         if (cfg_.enable_hpss_onsets || cfg_.enable_tempogram_percussive_fallback)  // H, P ping-pong + a copy
             need[i] += n / hop * s2_ * 4.0 * 5.0;
@@ -934,7 +915,6 @@ void Pipeline::run(const float* d_samples, const std::vector<uint64_t>& in_off, 
         cum += need[i];
     }
     flush();
-    finish_key(res);
     times_.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     d_.last = times_;
 }
@@ -1391,25 +1371,6 @@ struct HostTrace {
     }
 };
 
-void Pipeline::finish_key(std::vector<TrackRes>& res) {
-    if (!key_pending_) return;
-    KeyPending& kp = *key_pending_;
-    SDSP_HIP_CHECK(hipStreamWaitEvent(d_.stream, kp.kt->ev[2], 0));
-    const std::vector<KeyOut> kout = c_.down(kp.d_kout, kp.at.size());
-    for (size_t k = 0; k < kp.at.size(); k++) {
-        TrackRes& r = res[kp.at[k]];
-        const KeyOut& ko = kout[k];
-        if (!ko.ok) continue;
-        r.key_mode = ko.mode;
-        r.key_tonic = ko.tonic;
-        r.key_conf = ko.conf;
-        r.key_clarity = ko.clarity;
-    }
-    times_.stft8192_ms += kp.kt->ms(0, 1);
-    times_.key_ms += kp.kt->ms(1, 2);
-    key_pending_.reset();
-}
-
 void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in_off, const std::vector<uint64_t>& n_raw,
                          const std::vector<int>& idx, std::vector<TrackRes>& res) {
     const int T = (int)idx.size();
@@ -1553,19 +1514,11 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     std::unique_ptr<Timers> ktp(new Timers());
     Timers& kt = *ktp;
     kt.init(d_);
-    // per-parity names of what the main stream uploads for the key stream (see KeyPending)
-    sb_parity_ ^= 1;
-    const std::string EP = sb_parity_ ? "E1." : "E0.";
+    // what the main stream uploads for the key stream (read by it before the sub-batch's join)
+    const std::string EP = "E.";
     // SDSP_SERIAL_STREAMS=1 keeps the key path on the main stream (per-kernel profiling)
     static const bool serial_streams = std::getenv("SDSP_SERIAL_STREAMS") != nullptr;
-    // SDSP_KEY_STFT_FIRST=1 (schedule experiment): the 8192-point STFT on the main stream ahead
-    // of the tempo path, so only the HBM-bound mask / HPCP / vote kernels share the chip with the
-    // tempo kernels.  Measured slower (606 vs 558 ms per 1024-track step, tools/bench_ab.sh): the
-    // tempo path's latency-bound chains overlap the STFT's VALU work better than the mask's
-    // long-lived waves, so by default the STFT runs on the key stream beside the tempo path.
-    static const bool key_stft_first = std::getenv("SDSP_KEY_STFT_FIRST") != nullptr;
     hipStream_t st2 = serial_streams ? st : d_.stream2;
-    hipStream_t sk = key_stft_first ? st : st2;
     float* d_tune = nullptr;  // per key track tuning offset (tuning compensation)
     float* mags8 = nullptr;
     uint64_t* d_kpfx = nullptr;
@@ -1592,32 +1545,18 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         // uploads above were queued on the main stream: order the key stream after them
         kt.mark(7);
         SDSP_HIP_CHECK(hipStreamWaitEvent(st2, kt.ev[7], 0));
-        kt.mark(0, sk);
+        kt.mark(0, st2);
         launch_stft(KFS, false, d_samples, d_kpfx, NK, total8, d_ksrc, d_kgain, KHOP, t8.window.as<float>(),
-                    stft_twp(t8, KFS, false), stft_rtp(t8, KFS, false), mags8, d_kpfx, ks_, nullptr, sk, d_kstr, kstr.back(),
+                    stft_twp(t8, KFS, false), stft_rtp(t8, KFS, false), mags8, d_kpfx, ks_, nullptr, st2, d_kstr, kstr.back(),
                     c_.dev<uint32_t>("E.redo", total8 + 1));
         SDSP_HIP_CHECK(hipGetLastError());
-        kt.mark(1, sk);
-        if (sk != st2) SDSP_HIP_CHECK(hipStreamWaitEvent(st2, kt.ev[1], 0));
-        // key spectrogram conditioning (src/lib.rs:1011-1060).  SDSP_KEY_FUSE=1 (experiment): on
-        // the default path (harmonic time mask, margin 12, power 2, then plain HPCP, whose masked
-        // spectrogram nothing else reads) the mask runs inside the HPCP pass (launch_hpcp_masked)
-        // instead of in place over HBM.  It moves a third less HBM data but measured slower
-        // (0.192 vs 0.175 ms per 3-min track, 1757 vs 1796 tracks/s): the mask's
-        // two divisions per element, hidden under k_mask_r's memory time, land on the VALU-bound
-        // HPCP walk.  The default stays k_mask_r in place, then k_hpcp.
+        kt.mark(1, st2);
+        // key spectrogram conditioning (src/lib.rs:1011-1060): the mask runs in place over HBM
+        // (k_mask_r), then HPCP reads the masked spectrogram (DESIGN.md §4 on the fused variant)
         const bool use_log = cfg_.enable_key_log_frequency;  // :1062-1095
         const bool tuned = cfg_.enable_key_tuning_compensation && !use_log;
         const bool whiten = cfg_.enable_key_hpcp_whitening && cfg_.key_hpcp_whitening_smooth_bins >= 3;
-        const bool plain_hpcp = !use_log && cfg_.enable_key_hpcp && !tuned && !whiten && !cfg_.enable_key_hpcp_bass_blend;
-        const bool fuse_mask = std::getenv("SDSP_KEY_FUSE") != nullptr && !cfg_.enable_key_hpss_harmonic &&
-                               cfg_.enable_key_harmonic_mask && plain_hpcp && !cfg_.enable_key_beat_synchronous &&
-                               mask_fused_ok(B8, ks_, (int)std::min<uint64_t>(cfg_.key_spectrogram_smooth_margin, 1 << 20),
-                                             cfg_.key_harmonic_mask_power,
-                                             (int)std::max<uint64_t>(std::min<uint64_t>(cfg_.key_hpcp_peaks_per_frame, 1 << 20), 1));
-        if (fuse_mask) {
-            // the mask runs in launch_hpcp_masked below
-        } else if (cfg_.enable_key_hpss_harmonic) {
+        if (cfg_.enable_key_hpss_harmonic) {
             const KeyHpssParams kh = key_hpss_params(cfg_, sr_, B8, fres8, ks_);
             if (kh.nb > 0) {  // an empty band returns the spectrogram unchanged (extractor.rs:1408-1410)
                 std::vector<uint64_t> moff(1, 0), mt(1, 0), at(1, 0);
@@ -1675,19 +1614,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
             // the table upload is queued on the main stream: order the key stream after it
             kt.mark(10);
             SDSP_HIP_CHECK(hipStreamWaitEvent(st2, kt.ev[10], 0));
-            if (fuse_mask) {
-                std::vector<uint64_t> kspfx(1, 0);  // mask segments (prefix checkpoints) per key track
-                for (int k = 0; k < NK; k++)
-                    kspfx.push_back(kspfx.back() + (kpfx[(size_t)k + 1] - kpfx[(size_t)k] + KEY_CKPT_SEG - 1) / KEY_CKPT_SEG);
-                uint64_t* d_kspfx = c_.up(EP + "kseg_pfx", kspfx);
-                float* d_ckpt = c_.dev<float>("E.kckpt", kspfx.back() * KEY_CKPT_STRIDE);
-                kt.mark(11);  // the segment prefix upload is on the main stream
-                SDSP_HIP_CHECK(hipStreamWaitEvent(st2, kt.ev[11], 0));
-                launch_hpcp_masked(mags8, ks_, d_kpfx, d_ktile, d_kspfx, d_ckpt, d_kid, NK, ktile.back(), hp, d_ht,
-                                   d_chroma, d_energy, st2);
-            } else {
-                launch_hpcp(mags8, d_kpfx, d_ktile, d_kid, NK, ktile.back(), hp, d_ht, d_chroma, d_energy, st2);
-            }
+            launch_hpcp(mags8, d_kpfx, d_ktile, d_kid, NK, ktile.back(), hp, d_ht, d_chroma, d_energy, st2);
         } else {  // :1169-1197 (the tuned variant only when |offset| > 1e-6)
             const ChromaParams cp = chroma_params(cfg_, sr_, 0, B8, fres8, ks_);
             launch_chroma(0, mags8, d_kpfx, d_ktile, d_kid, NK, ktile.back(), cp, d_tune, d_chroma, d_energy, st2);
@@ -2159,21 +2086,8 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     SDSP_HIP_CHECK(hipGetLastError());
     tm.mark(5);
     tm.mark(6);
-    // the previous sub-batch's key results (its key work ran ahead of this one's on the key stream)
-    finish_key(res);
     const bool beat_sync = cfg_.enable_key_beat_synchronous && !cfg_.enable_key_log_frequency;
-    // SDSP_KEY_DEFER=1 (experiment): join this sub-batch's key stream one sub-batch late.  Both
-    // streams then stay busy 95 % of the span instead of 85 %, but the step does not get shorter
-    // (1,918-1,953 vs 1,927-1,933 tracks/s, alternating runs on one box): the chip is saturated,
-    // and the extra overlap only slows each kernel down.
-    const bool defer_key =
-        NK > 0 && !beat_sync && !serial_streams && !dbg_on && std::getenv("SDSP_KEY_DEFER") != nullptr;
-    if (defer_key) {
-        key_pending_.reset(new KeyPending());
-        key_pending_->kt = std::move(ktp);
-        key_pending_->d_kout = d_kout;
-        for (int k = 0; k < NK; k++) key_pending_->at.push_back((size_t)idx[(size_t)R[(size_t)K[(size_t)k]]]);
-    } else if (NK > 0) {  // join the key stream
+    if (NK > 0) {  // join the key stream
         SDSP_HIP_CHECK(hipStreamWaitEvent(st, kt.ev[2], 0));
         kout = c_.down(d_kout, (size_t)NK);
         htr("E join");
@@ -2282,7 +2196,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
             }
         }
     }
-    for (int k = 0; k < NK && !defer_key; k++) {
+    for (int k = 0; k < NK; k++) {
         TrackRes& r = res[(size_t)idx[(size_t)R[(size_t)K[(size_t)k]]]];
         const KeyOut& ko = kout[(size_t)k];
         if (!ko.ok) continue;
@@ -2381,13 +2295,12 @@ void fill_result(const TrackRes& r, uint32_t sr, float ms, sdsp_result* o) {
 
 // One device-resident batch on `device`.  The engine's main stream first waits for `user_stream`
 // (everything queued on it so far) and for `wait_ev` (a copy's completion), whichever are given.
-int32_t run_device(int device, const float* d_samples, const uint64_t* offsets, const uint64_t* lens, uint64_t n,
-                   uint32_t sr, const sdsp_config* cfg, void* user_stream, sdsp_result* outs,
-                   int stages = SDSP_STAGES_FULL, hipEvent_t wait_ev = nullptr) {
+// The batch on a context whose mutex the caller holds (run_device, and sdsp_analyze_audio's
+// direct path, which stages its one track into a context buffer under the same lock).
+int32_t run_locked(DeviceCtx& d, const float* d_samples, const uint64_t* offsets, const uint64_t* lens, uint64_t n,
+                   uint32_t sr, const sdsp_config* cfg, void* user_stream, sdsp_result* outs, int stages,
+                   hipEvent_t wait_ev) {
     if (stages != SDSP_STAGES_FULL && stages != SDSP_STAGES_BPM_ONLY) throw HipError("unknown stage mask");
-    DeviceCtx& d = device_ctx(device);
-    std::lock_guard<std::mutex> lk(d.mu);
-    SDSP_HIP_CHECK(hipSetDevice(device));
     if (user_stream) {
         hipEvent_t ev;
         SDSP_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
@@ -2407,10 +2320,77 @@ int32_t run_device(int device, const float* d_samples, const uint64_t* offsets, 
     return SDSP_OK;
 }
 
+int32_t run_device(int device, const float* d_samples, const uint64_t* offsets, const uint64_t* lens, uint64_t n,
+                   uint32_t sr, const sdsp_config* cfg, void* user_stream, sdsp_result* outs,
+                   int stages = SDSP_STAGES_FULL, hipEvent_t wait_ev = nullptr) {
+    DeviceCtx& d = device_ctx(device);
+    std::lock_guard<std::mutex> lk(d.mu);
+    SDSP_HIP_CHECK(hipSetDevice(device));
+    return run_locked(d, d_samples, offsets, lens, n, sr, cfg, user_stream, outs, stages, wait_ev);
+}
+
 }  // namespace
 }  // namespace sdsp
 
 using namespace sdsp;
+
+namespace sdsp {
+namespace {
+struct Slot {
+    float* d = nullptr;
+    uint64_t cap = 0;  // floats
+    hipEvent_t ready = nullptr;
+};
+// A device's staging area: its copy stream and two HBM slots.  Areas are pooled per device and
+// reused by later calls (grow-only slots, like the engine's own buffers), so a repeated call
+// creates no stream, event or allocation; concurrent callers on one device take separate areas.
+struct DeviceStage {
+    int dev = 0;
+    hipStream_t copy = nullptr;
+    Slot slot[2];
+};
+std::mutex g_stage_mu;
+std::map<int, std::vector<DeviceStage*>>* g_stage_free = new std::map<int, std::vector<DeviceStage*>>();  // never freed:
+// the areas outlive the call and are released with the process (no HIP calls at static teardown)
+DeviceStage* stage_acquire(int dev) {
+    std::lock_guard<std::mutex> lk(g_stage_mu);
+    auto& v = (*g_stage_free)[dev];
+    if (!v.empty()) {
+        DeviceStage* ds = v.back();
+        v.pop_back();
+        return ds;
+    }
+    DeviceStage* ds = new DeviceStage();
+    ds->dev = dev;
+    return ds;
+}
+void stage_release(DeviceStage* ds) {
+    if (ds->copy) {  // nothing may still be copying into the slots the next caller receives
+        (void)hipSetDevice(ds->dev);
+        (void)hipStreamSynchronize(ds->copy);
+    }
+    std::lock_guard<std::mutex> lk(g_stage_mu);
+    (*g_stage_free)[ds->dev].push_back(ds);
+}
+// SDSP_DEVICE_LIST=a,b,... (test hook): the worker devices of sdsp_analyze_batch, repeats allowed
+// (two workers on device 0 exercise the multi-device chunk path on a one-GPU box)
+std::vector<int> device_list_override(int ndev) {
+    std::vector<int> devs;
+    const char* e = std::getenv("SDSP_DEVICE_LIST");
+    if (!e) return devs;
+    for (const char* p = e; *p;) {
+        char* end = nullptr;
+        const long v = std::strtol(p, &end, 10);
+        if (end == p) break;
+        if (v >= 0 && v < ndev) devs.push_back((int)v);
+        p = *end == ',' ? end + 1 : end;
+        if (end == p && *p) break;
+    }
+    return devs;
+}
+}  // namespace
+}  // namespace sdsp
+
 
 extern "C" {
 
@@ -2442,30 +2422,6 @@ int32_t sdsp_analyze_batch_device_ex(const float* d_samples, const uint64_t* off
 // thread stages the next chunk into the second of two HBM slots (its own stream, completion
 // signalled by an event the engine's stream waits on) while the device analyses the current one.
 // The queue itself is batch_sched.hpp (host-only, tested with fake devices).
-namespace {
-struct Slot {
-    float* d = nullptr;
-    uint64_t cap = 0;  // floats
-    hipEvent_t ready = nullptr;
-};
-struct DeviceStage {
-    int dev = 0;
-    hipStream_t copy = nullptr;
-    Slot slot[2];
-    ~DeviceStage() {
-        if (copy) {
-            (void)hipSetDevice(dev);
-            (void)hipStreamSynchronize(copy);
-        }
-        for (auto& sl : slot) {
-            if (sl.d) (void)hipFree(sl.d);
-            if (sl.ready) (void)hipEventDestroy(sl.ready);
-        }
-        if (copy) (void)hipStreamDestroy(copy);
-    }
-};
-}  // namespace
-
 int32_t sdsp_analyze_batch(const float* const* tracks, const uint64_t* lens, uint64_t n_tracks, uint32_t sample_rate,
                            const sdsp_config* cfg, uint32_t device_mask, sdsp_result* outs) {
     std::vector<int> devs;
@@ -2478,12 +2434,17 @@ int32_t sdsp_analyze_batch(const float* const* tracks, const uint64_t* lens, uin
         }
         return SDSP_ERR_PROCESSING;
     }
-    for (int d = 0; d < ndev && d < 32; d++)
-        if (device_mask == 0 ? d == 0 : ((device_mask >> d) & 1u)) devs.push_back(d);
+    devs = device_list_override(ndev);
+    if (devs.empty())
+        for (int d = 0; d < ndev && d < 32; d++)
+            if (device_mask == 0 ? d == 0 : ((device_mask >> d) & 1u)) devs.push_back(d);
     if (devs.empty()) devs.push_back(0);
     uint64_t max_tracks = 512;
     if (const char* e = std::getenv("SDSP_BATCH_CHUNK_TRACKS")) max_tracks = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
     const std::vector<uint64_t> cb = plan_chunks(lens, n_tracks, max_tracks, (uint64_t)2 << 30 /* 8 GB of f32 */);
+    // test hook: the chunk whose analysis throws (the per-chunk failure path)
+    const char* fe = std::getenv("SDSP_TEST_FAIL_CHUNK");
+    const long fail_chunk = fe ? std::atol(fe) : -1;
     const size_t n_chunks = cb.size() - 1;
     // every result starts as an error; run_device overwrites the tracks it analyses
     auto mark_failed = [&](size_t c, const std::string& what) {
@@ -2494,12 +2455,11 @@ int32_t sdsp_analyze_batch(const float* const* tracks, const uint64_t* lens, uin
         }
     };
     for (size_t c = 0; c < n_chunks; c++) mark_failed(c, "track not analysed");
-    std::vector<std::unique_ptr<DeviceStage>> stg;
+    std::vector<DeviceStage*> stg;
     std::vector<ChunkDevice> cds;
     for (int dev : devs) {
-        stg.emplace_back(new DeviceStage());
-        DeviceStage* ds = stg.back().get();
-        ds->dev = dev;
+        stg.push_back(stage_acquire(dev));
+        DeviceStage* ds = stg.back();
         ChunkDevice cd;
         cd.stage = [ds, &cb, tracks, lens](int s, size_t c) {
             SDSP_HIP_CHECK(hipSetDevice(ds->dev));
@@ -2512,8 +2472,10 @@ int32_t sdsp_analyze_batch(const float* const* tracks, const uint64_t* lens, uin
                 if (sl.d) SDSP_HIP_CHECK(hipFree(sl.d));
                 sl.d = nullptr;
                 sl.cap = 0;
-                SDSP_HIP_CHECK(hipMalloc(&sl.d, std::max<uint64_t>(tot, 1) * sizeof(float)));
-                sl.cap = std::max<uint64_t>(tot, 1);
+                const uint64_t want = std::max<uint64_t>(tot + tot / 8, 1);  // grow-only, with slack
+                SDSP_HIP_CHECK(hipMalloc(&sl.d, want * sizeof(float)));
+                note_alloc(want * sizeof(float));
+                sl.cap = want;
             }
             uint64_t o = 0;
             for (uint64_t i = cb[c]; i < cb[c + 1]; i++) {
@@ -2524,7 +2486,8 @@ int32_t sdsp_analyze_batch(const float* const* tracks, const uint64_t* lens, uin
             }
             SDSP_HIP_CHECK(hipEventRecord(sl.ready, ds->copy));
         };
-        cd.analyze = [ds, &cb, lens, sample_rate, cfg, outs](int s, size_t c) {
+        cd.analyze = [ds, &cb, lens, sample_rate, cfg, outs, fail_chunk](int s, size_t c) {
+            if ((long)c == fail_chunk) throw HipError("injected chunk failure (SDSP_TEST_FAIL_CHUNK)");
             const uint64_t a = cb[c], b = cb[c + 1];
             std::vector<uint64_t> off(b - a), ln(b - a);
             uint64_t tot = 0;
@@ -2546,7 +2509,7 @@ int32_t sdsp_analyze_batch(const float* const* tracks, const uint64_t* lens, uin
         std::fprintf(stderr, "sdsp_analyze_batch: %s\n", what.c_str());
         mark_failed(c, what);
     });
-    stg.clear();
+    for (DeviceStage* ds : stg) stage_release(ds);
     return failed ? SDSP_ERR_PROCESSING : SDSP_OK;
 }
 
@@ -2559,9 +2522,31 @@ int32_t sdsp_analyze_audio(const float* samples, uint64_t n_samples, uint32_t sa
         out->status = SDSP_ERR_INVALID_INPUT;
         return SDSP_ERR_INVALID_INPUT;
     }
-    const float* const tr[1] = {samples};
-    const uint64_t ln[1] = {n_samples};
-    int32_t rc = sdsp_analyze_batch(tr, ln, 1, sample_rate, cfg, 1u, out);
+    // one track: staged into a context buffer on the engine's stream under the context lock (no
+    // copy stream, copier thread or staging allocation per call); device 0, as the batch's
+    // default mask
+    int32_t rc = SDSP_OK;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        out->status = SDSP_ERR_PROCESSING;
+        std::snprintf(out->error_message, sizeof out->error_message, "Processing error: no HIP device");
+    } else {
+        try {
+            DeviceCtx& d = device_ctx(0);
+            std::lock_guard<std::mutex> lk(d.mu);
+            SDSP_HIP_CHECK(hipSetDevice(0));
+            DevBuf& in = d.buf("api.track");
+            in.ensure(n_samples * sizeof(float));
+            SDSP_HIP_CHECK(hipMemcpyAsync(in.p, samples, n_samples * sizeof(float), hipMemcpyHostToDevice, d.stream));
+            const uint64_t off = 0;
+            rc = run_locked(d, in.as<float>(), &off, &n_samples, 1, sample_rate, cfg, nullptr, out, SDSP_STAGES_FULL,
+                            nullptr);
+        } catch (const std::exception& e) {
+            std::memset(out, 0, sizeof(*out));
+            out->status = SDSP_ERR_PROCESSING;
+            std::snprintf(out->error_message, sizeof out->error_message, "Processing error: %s", e.what());
+        }
+    }
     if (rc != SDSP_OK && out->status == SDSP_OK) out->status = rc;
     if (out->status != SDSP_OK) {
         if (err && errlen) std::snprintf(err, (size_t)errlen, "%s", out->error_message);

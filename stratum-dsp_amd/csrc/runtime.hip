@@ -1,6 +1,7 @@
 // runtime.hip — device contexts, FFT tables, C ABI housekeeping (config defaults, result
 // ownership, version) and stage probes.  The analyze pipeline itself is in pipeline.hip.
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -12,6 +13,12 @@
 #include "sdsp_runtime.hpp"
 
 namespace sdsp {
+
+static std::atomic<uint64_t> g_alloc_n{0}, g_alloc_bytes{0};
+void note_alloc(size_t bytes) {
+    g_alloc_n++;
+    g_alloc_bytes += bytes;
+}
 
 static std::mutex g_ctx_mu;
 static std::map<int, std::unique_ptr<DeviceCtx>> g_ctx;
@@ -26,35 +33,13 @@ DeviceCtx& device_ctx(int device) {
         // The tempo path (main stream) is the critical path and is made of short, latency-bound
         // kernels; the key path (stream2) is long bandwidth-bound kernels.  The main stream gets
         // the higher priority so its workgroups are dispatched ahead of the key stream's
-        // (SDSP_EQUAL_PRIORITY=1 disables).
-        if (const char* sk = std::getenv("SDSP_ALLOC_SKEW_MB")) {  // placement experiment
-            void* dummy = nullptr;
-            SDSP_HIP_CHECK(hipMalloc(&dummy, (size_t)std::atol(sk) << 20));
-        }
+        // (measured in round 2: the key stream first, equal priorities and CU-masked streams were
+        // all slower end to end).
         int lo = 0, hi = 0;
         SDSP_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-        if (std::getenv("SDSP_EQUAL_PRIORITY")) lo = hi = 0;
-        if (std::getenv("SDSP_KEY_PRIORITY")) std::swap(lo, hi);  // experiment: the key stream first
         SDSP_HIP_CHECK(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi));
-        // SDSP_KEY_CU_FRAC=f (experiment): the key stream runs on a fixed fraction f of the CUs,
-        // spread evenly over CU ids, and the main stream on the rest
-        const char* kf = std::getenv("SDSP_KEY_CU_FRAC");
-        if (kf && std::atof(kf) > 0.0 && std::atof(kf) < 1.0) {
-            SDSP_HIP_CHECK(hipStreamDestroy(c->stream));
-            hipDeviceProp_t prop;
-            SDSP_HIP_CHECK(hipGetDeviceProperties(&prop, device));
-            const int ncu = prop.multiProcessorCount;
-            const double f = std::atof(kf);
-            std::vector<uint32_t> mk((size_t)(ncu + 31) / 32, 0u), mm((size_t)(ncu + 31) / 32, 0u);
-            for (int i = 0; i < ncu; i++) {
-                const bool key = (int)((i + 1) * f) != (int)(i * f);  // even spread
-                (key ? mk : mm)[(size_t)i / 32] |= 1u << (i % 32);
-            }
-            SDSP_HIP_CHECK(hipExtStreamCreateWithCUMask(&c->stream, (uint32_t)mm.size(), mm.data()));
-            SDSP_HIP_CHECK(hipExtStreamCreateWithCUMask(&c->stream2, (uint32_t)mk.size(), mk.data()));
-        } else {
-            SDSP_HIP_CHECK(hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, lo));
-        }
+        SDSP_HIP_CHECK(hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, lo));
+        for (hipStream_t s : {c->stream, c->stream2}) c->own.push_back(s);
     }
     return *c;
 }
@@ -266,6 +251,13 @@ int32_t sdsp_last_stage_times(int32_t device, sdsp_stage_times* out) {
 // device-resident noise tracks of len samples each (one magnitude buffer, the pipeline's row
 // stride), HIP events on the launch stream.  Writes the mean launch time and the algorithmic
 // bytes per launch (4 N_in + 4 F (nfft/2+1) per track).
+// test probe: device allocations the engine has made so far (count, bytes)
+int32_t sdsp_debug_alloc_stats(uint64_t* n_allocs, uint64_t* bytes) {
+    if (n_allocs) *n_allocs = g_alloc_n.load();
+    if (bytes) *bytes = g_alloc_bytes.load();
+    return SDSP_OK;
+}
+
 int32_t sdsp_probe_stft(int32_t device, uint64_t nfft, uint64_t hop, uint64_t n_tracks, uint64_t len, int32_t reps,
                         int32_t stride, double* ms_per_launch, double* bytes_per_launch) {
     try {

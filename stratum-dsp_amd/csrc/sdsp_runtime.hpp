@@ -26,22 +26,32 @@ struct HipError : std::runtime_error {
     using std::runtime_error::runtime_error;
 };
 
+// Device allocations made by the engine (buffers and staging slots): count and bytes, for the
+// tests' "a repeated call allocates nothing" check (sdsp_debug_alloc_stats).
+void note_alloc(size_t bytes);
+
 // Grow-only device allocation.
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
+    // the engine streams that may still read the buffer (DeviceCtx::buf sets them); the caller's
+    // own streams are never waited on here
+    const std::vector<hipStream_t>* readers = nullptr;
     void ensure(size_t n) {
         if (n <= bytes) return;
-        // the old buffer may still be read by work queued on another stream (the key stream's
-        // tail runs under the next sub-batch): drain the device before it is released
         if (p) {
-            SDSP_HIP_CHECK(hipDeviceSynchronize());
+            // work queued on the engine's streams may still read the old buffer
+            if (readers)
+                for (hipStream_t s : *readers) SDSP_HIP_CHECK(hipStreamSynchronize(s));
+            else
+                SDSP_HIP_CHECK(hipDeviceSynchronize());
             SDSP_HIP_CHECK(hipFree(p));
         }
         p = nullptr;
         bytes = 0;
         const size_t want = n + n / 8 + 4096;
         SDSP_HIP_CHECK(hipMalloc(&p, want));
+        note_alloc(want);
         bytes = want;
     }
     template <class T>
@@ -68,13 +78,17 @@ struct DeviceCtx {
     int device = 0;
     hipStream_t stream = nullptr;   // main (tempo / beat) stream
     hipStream_t stream2 = nullptr;  // key-path stream, forked from and joined to `stream`
+    std::vector<hipStream_t> own;   // the streams above
     std::mutex mu;
     std::map<int, std::unique_ptr<FftTables>> fft;  // keyed by real FFT size N
     std::map<std::string, std::unique_ptr<DevBuf>> bufs;
     sdsp_stage_times last{};
     DevBuf& buf(const std::string& name) {
         auto& b = bufs[name];
-        if (!b) b.reset(new DevBuf());
+        if (!b) {
+            b.reset(new DevBuf());
+            b->readers = &own;
+        }
         return *b;
     }
     FftTables& tables(int N, bool with_window);

@@ -125,8 +125,10 @@ def _batch_error(outs, n, what):
     return f"{what}: {msg}" if msg else what
 
 
-def analyze_batch(tracks, sample_rate=44100, config=None, device_mask=0):
-    """Batch form: list of per-track results; failed tracks come back as AnalysisError objects."""
+def analyze_batch(tracks, sample_rate=44100, config=None, device_mask=0, strict=True):
+    """Batch form: list of per-track results; failed tracks come back as AnalysisError objects.
+    strict: raise when the call as a whole reports a failure (a failed chunk); otherwise return
+    the per-track results, the failed chunk's tracks as AnalysisError."""
     arrs = [np.ascontiguousarray(t, dtype=np.float32) for t in tracks]
     n = len(arrs)
     ptrs = (C.POINTER(C.c_float) * n)(*[_fp(a) for a in arrs])
@@ -135,7 +137,7 @@ def analyze_batch(tracks, sample_rate=44100, config=None, device_mask=0):
     cfg = config if config is not None else default_config()
     st = lib().sdsp_analyze_batch(ptrs, lens.ctypes.data_as(C.POINTER(C.c_uint64)), n, sample_rate, C.byref(cfg),
                                   device_mask, outs)
-    if st != 0:
+    if st != 0 and strict:
         raise AnalysisError(st, _batch_error(outs, n, "batch failed"))
     res = []
     for i in range(n):

@@ -44,6 +44,7 @@ int main(int argc, char** argv) {
         devs[d].stage = [&, d](int s, size_t c) {
             if (scen == "copier_dies" && d == 1) throw std::runtime_error("stage failed");
             if (scen == "all_copiers_die") throw std::runtime_error("stage failed");
+            if (scen == "copier_throws_int" && d == 1) throw 42;  // not a std::exception
             thread_local std::mt19937 trng(seed * 7919u + (unsigned)d);
             std::this_thread::sleep_for(std::chrono::microseconds(trng() % 300));
             auto& sl = slots[d][s];
@@ -52,6 +53,7 @@ int main(int argc, char** argv) {
         };
         devs[d].analyze = [&, d](int s, size_t c) {
             if (scen == "analyze_fails" && d == 2 && c % 4 == 1) throw std::runtime_error("analysis failed");
+            if (scen == "analyze_throws_int" && d == 2 && c % 4 == 1) throw 7;  // not a std::exception
             std::this_thread::sleep_for(std::chrono::microseconds(d == 0 ? 900 : 200));
             const auto& sl = slots[d][s];
             if (sl.size() != cb[c + 1] - cb[c]) throw std::logic_error("slot holds another chunk");
@@ -84,13 +86,13 @@ int main(int argc, char** argv) {
         expect_fail += failed_chunk[c];
     }
     if (nf != expect_fail) return 33;
-    if (scen == "basic" || scen == "single" || scen == "copier_dies") {
+    if (scen == "basic" || scen == "single" || scen == "copier_dies" || scen == "copier_throws_int") {
         if (nf != 0) return 34;
     }
-    if (scen == "copier_dies")
+    if (scen == "copier_dies" || scen == "copier_throws_int")
         for (uint64_t i = 0; i < n; i++)
             if (out_dev[i] == 1) return 35;  // device 1 never held a chunk
-    if (scen == "analyze_fails" && nf == 0) return 36;
+    if ((scen == "analyze_fails" || scen == "analyze_throws_int") && nf == 0) return 36;
     if (scen == "all_copiers_die" && nf != n_chunks) return 37;
     int used = 0;
     for (int d = 0; d < ndev; d++)

@@ -64,3 +64,33 @@ def exact_fraction(got, ref):
     else:
         same_b = False
     return (same + same_b) / (len(pairs) + 1)
+
+
+def result_digest(r):
+    """A compact, bit-level fingerprint of an AnalysisResult dict (committed golden files): every
+    float by its f32 bits, the beat lists by a SHA-256 of their f32 bytes."""
+    import hashlib
+
+    def bits(v):
+        return int(np.float32(v).view(np.uint32))
+
+    def lst(v):
+        a = np.asarray(v, np.float32)
+        return [int(a.size), hashlib.sha256(a.tobytes()).hexdigest()[:16]]
+
+    m = r["metadata"]
+    return {
+        "bpm": bits(r["bpm"]), "bpm_confidence": bits(r["bpm_confidence"]), "key": repr(r["key"]),
+        "key_confidence": bits(r["key_confidence"]), "key_clarity": bits(r["key_clarity"]),
+        "grid_stability": bits(r["grid_stability"]), "beats": lst(r["beat_grid"]["beats"]),
+        "downbeats": lst(r["beat_grid"]["downbeats"]), "bars": lst(r["beat_grid"]["bars"]),
+        "duration_seconds": bits(m["duration_seconds"]), "flags": m["flags"],
+        "warnings": len(m["confidence_warnings"]),
+        "mr": [m["tempogram_multi_res_triggered"], m["tempogram_multi_res_used"]],
+    }
+
+
+def samples_digest(x):
+    import hashlib
+
+    return hashlib.sha256(np.ascontiguousarray(x, np.float32).tobytes()).hexdigest()[:32]

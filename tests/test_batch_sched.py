@@ -21,7 +21,8 @@ def harness(tmp_path_factory):
     return str(exe)
 
 
-@pytest.mark.parametrize("scenario", ["basic", "single", "analyze_fails", "copier_dies", "all_copiers_die"])
+@pytest.mark.parametrize("scenario", ["basic", "single", "analyze_fails", "copier_dies", "all_copiers_die",
+                                      "copier_throws_int", "analyze_throws_int"])
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_chunk_queue(harness, scenario, seed):
     out = subprocess.run([harness, scenario, str(seed)], capture_output=True, text=True, timeout=120)

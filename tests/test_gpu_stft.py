@@ -74,3 +74,58 @@ def test_stft_silence_and_subnormal_scale(nfft, hop):
     assert mism == 0, f"{mism} of {ref.size} magnitudes differ"
     p2 = (ref.astype(np.float64) * 2.0 ** 33) ** 2
     assert np.any(ref == 0.0) and np.any((p2 > 0) & (p2 < 2.0 ** -96))  # both special ranges are exercised
+
+
+@pytest.mark.parametrize("frame_parallel", [False, True])
+@pytest.mark.parametrize("nfft,hop", [(8192, 512), (8192, 1024), (2048, 512), (2048, 256)])
+def test_stft_mostly_subnormal_scale_frames(nfft, hop, frame_parallel, monkeypatch):
+    """More than half of the frames (here ~90 %) have magnitudes of subnormal scale, so the sliding
+    kernel lists most of the launch on its redo list: each frame is listed at most once (the 4
+    waves of an 8192-point frame OR one flag), so the list never outgrows its capacity of one
+    entry per frame; bit-exact against the restatement."""
+    if frame_parallel:
+        monkeypatch.setenv("SDSP_STFT_FRAME_PARALLEL", "1")
+    else:
+        monkeypatch.delenv("SDSP_STFT_FRAME_PARALLEL", raising=False)
+    rng = np.random.default_rng(nfft + 11 * hop)
+    n = 44100 * 4
+    x = (rng.standard_normal(n) * 1e-30).astype(np.float32)
+    x[: n // 12] = (rng.standard_normal(n // 12) * 0.3).astype(np.float32)
+    got, fmax = sdsp.debug_stft(x, nfft, hop, np.float32(1.0))
+    ref = oracle.stft(x, nfft, hop)
+    mism = np.count_nonzero(got.view(np.uint32) != ref.view(np.uint32))
+    assert mism == 0, f"{mism} of {ref.size} magnitudes differ"
+    p2 = (ref.astype(np.float64) * 2.0 ** 33) ** 2
+    tiny_frames = np.count_nonzero(np.any((p2 > 0) & (p2 < 2.0 ** -96), axis=1))
+    assert tiny_frames > 0.5 * ref.shape[0], (tiny_frames, ref.shape[0])
+
+
+@pytest.mark.parametrize("frame_parallel", [False, True])
+@pytest.mark.parametrize("nfft,hop", [(8192, 512), (2048, 512), (2048, 300), (4096, 1000), (1024, 256)])
+def test_stft_overflow_rule(nfft, hop, frame_parallel, monkeypatch):
+    """Unnormalised int-scale input (samples ~2^24, e.g. int24 / int32 PCM passed as float with
+    enable_normalization = false): with the window's 2^32 the frame's |Y|^2 = 2^66 |X|^2
+    overflows f32, where the reference's (re*re + im*im) does not (extractor.rs:352).  The spec's
+    overflow rule re-evaluates those frames in the reference's range: bit-exact against the
+    restatement, finite, and within 1e-5 (relative to the frame peak) of numpy's float64 FFT."""
+    if frame_parallel:
+        monkeypatch.setenv("SDSP_STFT_FRAME_PARALLEL", "1")
+    else:
+        monkeypatch.delenv("SDSP_STFT_FRAME_PARALLEL", raising=False)
+    rng = np.random.default_rng(nfft + 13 * hop)
+    n = 44100 * 2
+    t = np.arange(n, dtype=np.float64)
+    x = (np.sin(2 * np.pi * 441.0 * t / 44100) * 2.0 ** 24 + rng.standard_normal(n) * 2.0 ** 18).astype(np.float32)
+    x[n // 2:] *= np.float32(1e-6)  # quiet half: ordinary frames beside the overflowing ones
+    got, fmax = sdsp.debug_stft(x, nfft, hop, np.float32(1.0))
+    ref = oracle.stft(x, nfft, hop)
+    mism = np.count_nonzero(got.view(np.uint32) != ref.view(np.uint32))
+    assert mism == 0, f"{mism} of {ref.size} magnitudes differ"
+    assert np.all(np.isfinite(ref))
+    assert np.any(ref.astype(np.float64) >= 2.0 ** 31)  # the rule is exercised
+    w = np.float32(0.5) * (np.float32(1) - np.cos((np.float32(2 * np.pi) * np.arange(nfft, dtype=np.float32) /
+                                                   np.float32(nfft - 1)).astype(np.float32)))
+    for f in (0, ref.shape[0] // 4, ref.shape[0] - 1):
+        fr = x[f * hop: f * hop + nfft].astype(np.float64) * w.astype(np.float64)
+        m64 = np.abs(np.fft.rfft(fr))
+        assert np.max(np.abs(ref[f] - m64)) <= 1e-5 * max(m64.max(), 1e-30), f
