@@ -163,7 +163,8 @@ def main():
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="config2")
     ap.add_argument("--tracks", type=int, default=0, help="tracks per GPU per step (0 = the workload's)")
     ap.add_argument("--seconds", type=float, default=180.0, help="track length (config2 / bpm-only)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, usable host cores)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = every host core this process may use (its affinity set, capped by the box's CPU share)")
     ap.add_argument("--cpu-tracks", type=int, default=0, help="0 = 2 per thread")
     ap.add_argument("--cpu-1thread-tracks", type=int, default=2, help="tracks timed alone on one thread")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -388,7 +389,14 @@ def host_cpu():
         usable = len(os.sched_getaffinity(0))
     except AttributeError:
         usable = os.cpu_count()
-    return {"nproc": os.cpu_count(), "usable": usable, "model": model}
+    # the CPU share the job is granted: a GPU box hands each GPU a slice of the host and says so in
+    # OMP_NUM_THREADS (its affinity set can still list every core of the machine)
+    share = usable or 1
+    try:
+        share = min(share, int(os.environ.get("OMP_NUM_THREADS", "") or share))
+    except ValueError:
+        pass
+    return {"nproc": os.cpu_count(), "usable": usable, "share": share, "model": model}
 
 
 def cpu_baseline(buf, offs, lens, res, n, sr, args):
@@ -399,8 +407,8 @@ def cpu_baseline(buf, offs, lens, res, n, sr, args):
     import parity
 
     host = host_cpu()
-    threads = args.cpu_threads or min(16, host["usable"] or 1)
-    k = min(n, args.cpu_tracks or 2 * threads)
+    threads = args.cpu_threads or host["share"]
+    k = min(n, args.cpu_tracks or threads)  # one track per thread
     xs = [buf.to_host(int(offs[i]), int(lens[i])) for i in range(k)]
     oracle.lib()
 
@@ -430,6 +438,9 @@ def cpu_baseline(buf, offs, lens, res, n, sr, args):
         # other threads ran): k / the summed per-track seconds
         "value_1thread_loaded": round(k / sum(per_track), 4),
     }
+    # the whole host, if every core ran one track at the loaded one-thread rate (an extrapolation,
+    # stated as such: the job may use only its share of the host's cores)
+    cpu["value_all_host_cores_extrapolated"] = round(cpu["value_1thread_loaded"] * (host["nproc"] or 1), 2)
     # one thread alone, the first tracks again (more than the parallel sample: its own tracks)
     k1 = max(1, args.cpu_1thread_tracks)
     if k1 > k:

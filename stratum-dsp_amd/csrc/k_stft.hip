@@ -764,6 +764,210 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_stft_slide8: the sliding strip for N = 8192 (M = 4096 = 16^3, one 256-thread workgroup per
+// strip), software-pipelined across frames.  The kernel holds its per-strip constants in ~110
+// VGPRs, so it runs 2 waves per SIMD, and one wave alone issues a VALU instruction at most every
+// 4 cycles (MI355X_MICROARCH.md, issue costs): the SIMD reaches its 2-cycle rate only while both
+// of its waves issue VALU.  Every LDS round trip is therefore given independent VALU work of
+// another frame to cover its latency:
+//   region 1 (after the barrier that publishes frame i's pass-1 output in A):
+//       issue frame i's pass-2 reads from A; post-process frame i-1 (held in registers: S, D',
+//       the FMA form, the exact sqrt, 16 buffer stores); pass 2 of frame i; write B;
+//   barrier;
+//   region 2: issue frame i's pass-3 reads from B; window + pass 1 of frame i+1 from the sample
+//       ring, write A (every pass-2 read of A finished before the barrier); pass 3 of frame i; the
+//       (k, M-k) exchange between lanes l and l^32 (ds_bpermute) into the held registers;
+//   barrier (A complete for frame i+1; every pass-3 read of B done before the next B write).
+// Two barriers per frame, as before, and the same arithmetic (bit-identical magnitudes).  Rows
+// are written by buffer stores whose per-lane offsets are fixed for the strip and whose row is a
+// scalar descriptor (no 64-bit address arithmetic per store); the descriptor of the row "before
+// frame 0" has no records, so its stores are dropped by the hardware without a branch.  Frames
+// whose sqrt met an input outside its exact range are collected in a wave-uniform 64-bit mask and
+// listed once per strip after the loop (no per-frame LDS flag).
+template <int S>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_stft_slide8(
+    const float* __restrict__ samples, const uint64_t* __restrict__ frame_pfx, const uint64_t* __restrict__ strip_pfx,
+    int n_tracks, uint64_t n_strips, const uint64_t* __restrict__ src_off, const float* __restrict__ gain, int hop,
+    const float* __restrict__ window, const cx* __restrict__ twp, const cx* __restrict__ rtp, float* __restrict__ mags,
+    const uint64_t* __restrict__ mag_row0, int stride, uint32_t* __restrict__ redo) {
+    constexpr int M = 4096, TPF = 256;
+    constexpr int PADM = M + PADSHIFT * M / 16;
+    static_assert(S >= 1 && S <= 16 && STRIP_T == 64, "hop = S * 512; the miss mask holds 64 frames");
+    __shared__ c2 lds[2 * PADM];
+    __shared__ uint64_t miss_mask[4];
+
+    const int lt = threadIdx.x;
+    const uint64_t strip = (uint64_t)__builtin_amdgcn_readfirstlane((int)xcd_block(blockIdx.x, gridDim.x));
+    if (strip >= n_strips) return;  // the whole workgroup
+    const int trk = find_track(strip_pfx, n_tracks, strip);
+    const uint64_t F = frame_pfx[trk + 1] - frame_pfx[trk];
+    const uint64_t f0 = (strip - strip_pfx[trk]) * (uint64_t)STRIP_T;
+    const int nf = (int)(F - f0 < (uint64_t)STRIP_T ? F - f0 : (uint64_t)STRIP_T);
+    const float gn = gain[trk];
+    c2* const bufA = lds;
+    c2* const bufB = lds + PADM;
+    const int vo = 8 * lt;
+    const uint64_t cstart = f0 * (uint64_t)(hop / 2);
+    const uint64_t clen = (uint64_t)(nf - 1) * (uint64_t)(hop / 2) + (uint64_t)M;
+    const __amdgpu_buffer_rsrc_t rx = rsrc_of(samples + src_off[trk] + 2 * cstart, (uint32_t)(8u * clen));
+    const __amdgpu_buffer_rsrc_t rw = rsrc_of(window, 4u * 8192u);
+    const __amdgpu_buffer_rsrc_t rtw = rsrc_of(twp, 8u * 15u * (TPF + TPF / 16 + 1));
+    const __amdgpu_buffer_rsrc_t rrt = rsrc_of(rtp, 8u * (slide_rt_base<M>() + 8 * TPF + 1));
+    float* const row0 = mags + (mag_row0[trk] + f0) * (uint64_t)stride;
+
+    // per-strip constants (as k_stft_slide)
+    c2 win[16], tw1[15], tw2[15], tw3[15], wk[8], ring[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const c2 x = ld_c2(rx, vo, 8 * TPF * k);
+        ring[k] = {x.x * gn, x.y * gn};
+    }
+#pragma unroll
+    for (int k = 0; k < 16; k++) win[k] = ld_c2(rw, vo, 8 * TPF * k);
+#pragma unroll
+    for (int j = 0; j < 15; j++) tw1[j] = ld_c2(rtw, vo, 8 * TPF * j);
+    const int pp2 = lt / 16, q2 = lt % 16;
+#pragma unroll
+    for (int j = 0; j < 15; j++) tw2[j] = ld_c2(rtw, 8 * pp2, 8 * (15 * TPF + j * (TPF / 16)));
+#pragma unroll
+    for (int j = 0; j < 8; j++) wk[j] = ld_c2(rrt, vo, 8 * (slide_rt_base<M>() + TPF * j));
+#pragma unroll
+    for (int j = 0; j < 15; j++) {
+        const cx t = twp[15 * TPF + 15 * (TPF / 16) + j];
+        tw3[j] = c2{t.re, t.im};
+    }
+    const c2 rtH = ld_c2(rrt, 0, 8 * (slide_rt_base<M>() + 8 * TPF));  // bin M/2
+    const int colA = slide_col8(lt);
+    const bool self0 = lt == 0, self128 = lt == 32;
+    const int src_lane = (self0 || self128) ? (lt & 63) : ((lt & 63) ^ 32);
+    // LDS bases: pass-2 reads x[q + 16 pp + 256 k] (lpad: + 272 k), writes z[q + 256 pp + 16 k] (+ 17 k);
+    // pass-3 reads column colA, Z[colA + 256 m] (+ 272 m)
+    const int rb2 = lpad(q2 + 16 * pp2), wb2 = q2 + P272 * pp2, rb3 = lpad(colA);
+    // byte offsets in a row: own bins colA + 256 j, partner bins M - colA - 256 j
+    const int vown = 4 * colA, vpart = 4 * (M - colA - 256 * 7), vmid = 4 * (M / 2);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the per-strip loads have landed
+
+    // prologue: pass 1 of frame 0 into A, the ring advanced to frame 1
+    c2 v[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) v[k] = {ring[k].x * win[k].x, ring[k].y * win[k].y};
+    radix16<false>(v, tw1);
+#pragma unroll
+    for (int k = 0; k < 16; k++) bufA[P17 * lt + k] = v[k];
+    {
+        c2 nx[S];
+#pragma unroll
+        for (int s2 = 0; s2 < S; s2++) nx[s2] = ld_c2(rx, vo, 8 * ((hop / 2) + TPF * (16 - S + s2)));
+#pragma unroll
+        for (int k = 0; k < 16 - S; k++) ring[k] = ring[k + S];
+#pragma unroll
+        for (int s2 = 0; s2 < S; s2++) ring[16 - S + s2] = {nx[s2].x * gn, nx[s2].y * gn};
+    }
+    __syncthreads();
+
+    // the held frame (i - 1): P[0..7] own Z[colA + 256 j], P[8..15] the partner column's elements
+    // 8..15 (received), Pm = own element 8 (bin M/2 on the column-0 lane)
+    c2 P[16], Pm = {0.0f, 0.0f};
+#pragma unroll
+    for (int k = 0; k < 16; k++) P[k] = {0.0f, 0.0f};
+    uint64_t miss = 0;  // wave-uniform: bit i = frame f0 + i met the sqrt's inexact range
+    for (int i = 0;; i++) {
+        // ---- region 1 ----
+        c2 nx[S];  // the ring's new values for frame i + 2 (zeros past the strip: outside rx)
+#pragma unroll
+        for (int s2 = 0; s2 < S; s2++) nx[s2] = ld_c2(rx, vo, 8 * ((i + 2) * (hop / 2) + TPF * (16 - S + s2)));
+#pragma unroll
+        for (int k = 0; k < 16; k++) v[k] = bufA[rb2 + P272 * k];
+        __builtin_amdgcn_sched_barrier(0);  // the reads first: the post-processing below covers their latency
+        {
+            // post-processing of frame i - 1 (sdsp_fft_spec.h STFT section; see k_stft_slide)
+            const bool live = i > 0;
+            const __amdgpu_buffer_rsrc_t ro = rsrc_of(row0 + (int64_t)(i - 1) * stride, live ? 4u * (M + 1) : 0u);
+            uint32_t lo = 0xFFFFFFFFu, hi = 0u;
+            // |X| = 2^-33 sqrt(e) with the exact fast sqrt; the range test is on v_sqrt's result:
+            // s in [2^-47, inf) implies e > 2^-96 (1-ulp v_sqrt), where the correction is exact
+            auto sq = [&](float yx, float yy) {
+                const float x = __builtin_fmaf(yx, yx, yy * yy);
+                const float s = __builtin_amdgcn_sqrtf(x);
+                const uint32_t si = __float_as_uint(s);
+                lo = min(lo, si - 1u);
+                hi = max(hi, si);
+                const float sm = __uint_as_float(si - 1u), sp = __uint_as_float(si + 1u);
+                const float rm = __builtin_fmaf(-sm, s, x);
+                const float rp = __builtin_fmaf(-sp, s, x);
+                const int dm = (int)(__float_as_uint(rm) - 1u) >> 31;
+                const uint32_t up = (0u - __float_as_uint(rp)) >> 31;
+                return 0x1p-33f * __int_as_float(max((int)(si + (uint32_t)dm + up), 0));
+            };
+            auto st = [&](float mag, int voff, int soff) {
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mag), ro, voff, soff, 0);
+            };
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const c2 Zk = P[j], Zr = P[15 - j], w = wk[j];
+                const float sx = Zk.x + Zr.x, sy = Zk.y - Zr.y, dx = Zk.y + Zr.y, dy = -(Zk.x - Zr.x);
+                st(sq(__builtin_fmaf(w.x, dx, __builtin_fmaf(-w.y, dy, sx)), __builtin_fmaf(w.x, dy, __builtin_fmaf(w.y, dx, sy))),
+                   vown, 1024 * j);
+                st(sq(__builtin_fmaf(-w.x, dx, __builtin_fmaf(w.y, dy, sx)), __builtin_fmaf(w.x, dy, __builtin_fmaf(w.y, dx, -sy))),
+                   vpart, 1024 * (7 - j));
+            }
+            if (self0) {  // bin M/2, self-paired
+                const c2 Z = Pm, w = rtH;
+                const float sx = Z.x + Z.x, sy = Z.y - Z.y, dx = Z.y + Z.y, dy = -(Z.x - Z.x);
+                st(sq(__builtin_fmaf(w.x, dx, __builtin_fmaf(-w.y, dy, sx)), __builtin_fmaf(w.x, dy, __builtin_fmaf(w.y, dx, sy))),
+                   vmid, 0);
+            }
+            const bool missed = __builtin_amdgcn_ballot_w64(lo < 0x27FFFFFFu || hi >= 0x7F800000u) != 0;
+            miss |= (uint64_t)(missed && live) << ((i - 1) & 63);
+        }
+        if (i == nf) break;
+        radix16<false>(v, tw2);
+#pragma unroll
+        for (int k = 0; k < 16; k++) bufB[wb2 + P17 * k] = v[k];
+        __syncthreads();
+        __builtin_amdgcn_sched_barrier(0);  // keep region 2's VALU below the barrier (it covers the pass-3 reads)
+        // ---- region 2 ----
+        c2 u[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) u[k] = bufB[rb3 + P272 * k];
+        __builtin_amdgcn_sched_barrier(0);  // the reads first: pass 1 below covers their latency
+        // pass 1 of frame i + 1 (past the strip's end: unused values into A, nothing reads them)
+#pragma unroll
+        for (int k = 0; k < 16; k++) v[k] = {ring[k].x * win[k].x, ring[k].y * win[k].y};
+        radix16<false>(v, tw1);
+#pragma unroll
+        for (int k = 0; k < 16; k++) bufA[P17 * lt + k] = v[k];
+#pragma unroll
+        for (int k = 0; k < 16 - S; k++) ring[k] = ring[k + S];
+#pragma unroll
+        for (int s2 = 0; s2 < S; s2++) ring[16 - S + s2] = {nx[s2].x * gn, nx[s2].y * gn};
+        // pass 3 of frame i (n = 16, s = 256, p' = 0) on column colA, then the exchange: every lane
+        // sends its elements 8..15 to the partner lane; the column-0 lane sends itself 9..15, 0
+        radix16<true>(u, tw3);
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const c2 snd = self0 ? u[(9 + k) & 15] : u[8 + k];
+            P[8 + k] = {__shfl(snd.x, src_lane, 64), __shfl(snd.y, src_lane, 64)};
+            P[k] = u[k];
+        }
+        Pm = u[8];
+        __syncthreads();
+        __builtin_amdgcn_sched_barrier(0);  // keep the post-processing below the barrier (it covers the pass-2 reads)
+    }
+    // list the strip's missed frames once (k_stft_mag recomputes them right after this kernel)
+    if ((lt & 63) == 0) miss_mask[lt >> 6] = miss;
+    __syncthreads();
+    if (lt == 0) {
+        uint64_t m = miss_mask[0] | miss_mask[1] | miss_mask[2] | miss_mask[3];
+        while (m) {
+            const int b = __builtin_ctzll(m);
+            m &= m - 1;
+            redo[1 + atomicAdd(redo, 1u)] = (uint32_t)(frame_pfx[trk] + f0 + (uint64_t)b);
+        }
+    }
+}
+
 // strips of STRIP_T frames per track: strip_pfx[t] = sum over tracks < t of ceil(F / STRIP_T)
 std::vector<uint64_t> stft_strips(const std::vector<uint64_t>& frame_pfx) {
     std::vector<uint64_t> sp(frame_pfx.size(), 0);
@@ -880,10 +1084,13 @@ void launch_stft(int nfft, bool frame_max, const float* samples, const uint64_t*
                        block, 0, st, samples, frame_pfx, strip_pfx, n_tracks, n_strips, src_off, gain, hop, window, twp, \
                        rtp, mags, mag_row0, stride, fmax, redo)
         if (nfft == 8192) {
+            const dim3 g8((unsigned)n_strips);
             if (hop == 512)
-                SDSP_SLIDE(8192, 1, false);
+                hipLaunchKernelGGL(k_stft_slide8<1>, g8, block, 0, st, samples, frame_pfx, strip_pfx, n_tracks, n_strips,
+                                   src_off, gain, hop, window, twp, rtp, mags, mag_row0, stride, redo);
             else
-                SDSP_SLIDE(8192, 2, false);
+                hipLaunchKernelGGL(k_stft_slide8<2>, g8, block, 0, st, samples, frame_pfx, strip_pfx, n_tracks, n_strips,
+                                   src_off, gain, hop, window, twp, rtp, mags, mag_row0, stride, redo);
         } else if (frame_max) {
             if (hop == 256)
                 SDSP_SLIDE(2048, 2, true);

@@ -173,7 +173,9 @@ def fft_tempogram(nov, sr, hop, lo, hi):
     w = 0.5 * (1.0 - np.cos(2.0 * np.pi * np.arange(n) / (n - 1))) if n > 1 else np.ones(1)
     X = np.fft.rfft((nov - nov.mean()) * w, P)
     power = X.real ** 2 + X.imag ** 2
-    bpm = np.arange(P // 2 + 1) * ((sr / hop) / P) * 60.0
+    # bin BPMs are discrete values the reference computes in f32 (:111, 163-173): the same here
+    fres = f32(f32(f32(sr) / f32(hop)) / f32(P))
+    bpm = ((np.arange(P // 2 + 1).astype(np.float32) * fres) * f32(60.0)).astype(np.float64)
     keep = (bpm >= lo) & (bpm <= hi)
     b, p = bpm[keep], power[keep]
     order = np.argsort(-p, kind="stable")
@@ -289,8 +291,10 @@ def estimate_bpm_tempogram(M, sr, hop, lo, hi, res, band=BAND_DEFAULT):
         seed_bpms.append(fft_best[0])
     if ac_best and ac_best[0] > 0:
         seed_bpms.append(ac_best[0])
-    cands = sorted(x for b in seed_bpms for f in (1.0, 0.5, 2.0, 1 / 3, 3.0, 2 / 3, 1.5)
-                   for x in [b * f] if np.isfinite(x) and lo <= x <= hi)
+    # candidate BPMs: f32 products with the f32 folding factors (tempogram.rs:551-558)
+    facs = [f32(1.0), f32(0.5), f32(2.0), f32(1.0) / f32(3.0), f32(3.0), f32(2.0) / f32(3.0), f32(3.0) / f32(2.0)]
+    cands = sorted(x for b in seed_bpms for f in facs
+                   for x in [float(f32(f32(b) * f))] if np.isfinite(x) and lo <= x <= hi)
     uniq = []
     for b in cands:
         if uniq and abs(b - uniq[-1]) < 0.75:
@@ -503,3 +507,267 @@ def generate_beat_grid(bpm, conf, onsets_s):
     if len(times) >= 2 and iv.size and iv.mean() > 1e-10:
         stab = 1.0 / (1.0 + iv.std() / iv.mean())
     return beats, downs, stab, diag
+
+
+# ---- multi-resolution escalation (a17, a18) ----
+# AnalysisConfig::default() (config.rs:610-618, 653, 665)
+MR_DEFAULT = dict(top_k=25, w512=0.45, w256=0.35, w1024=0.20, dt512=0.92, margin=0.08, human_prior=False,
+                  base_top_n=25)
+SCORE_TIE = 1e-5  # score / ratio comparisons closer than this may be decided by the reference's f32 rounding
+#                   (f32 and float64 candidate scores differ by < 4e-6: tests/test_ref64_multires.py)
+
+
+def _near(a, b, eps):
+    """a and b differ, by less than eps: the reference's f32 values may order them either way.  Equal
+    float64 values are not near ties: they come from exactly representable operands (integer BPM
+    grids, halves, zero scores), which f32 holds exactly too."""
+    return 0.0 < abs(a - b) < eps
+
+
+class Ties(list):
+    """Comparisons whose outcome f32 rounding decides, as (tag, a, b)."""
+
+    def ge(self, tag, a, b, eps=SCORE_TIE):
+        if _near(a, b, eps):
+            self.append((tag, a, b))
+        return a >= b
+
+    def gt(self, tag, a, b, eps=SCORE_TIE):
+        if _near(a, b, eps):
+            self.append((tag, a, b))
+        return a > b
+
+
+def cand_lookup(cands, bpm, tol, ties=None, tag="lookup"):
+    """lookup_nearest over a candidate list (multi_resolution.rs:282-293): the score of the first
+    strictly nearest candidate within tol, else 0.  Candidate BPMs are the reference's f32 values
+    (discrete), and the distance is the reference's f32 |c - bpm|, so the pick is the reference's
+    own; only an exactly equal distance to two candidates whose list order (by score) is itself a
+    near tie is left to f32 rounding."""
+    best_d, best_s, best_i, eq = math.inf, 0.0, -1, []
+    for i, c in enumerate(cands):
+        d = float(abs(f32(c[0]) - f32(bpm)))
+        if d <= tol:
+            if d < best_d:
+                best_d, best_s, best_i, eq = d, c[1], i, []
+            elif d == best_d:
+                eq.append(i)
+    if ties is not None:
+        for i in eq:
+            if cands[i][1] != best_s and _near(cands[i][1], best_s, SCORE_TIE):
+                ties.append((tag + "-order", best_s, cands[i][1]))
+    return best_s
+
+
+def escalation_gate(bpm, conf, agree, cands, res=1.0, ties=None):
+    """The ambiguity gate of src/lib.rs:412-457 on the base hop-512 estimate and its candidate list
+    (top base_top_n).  Returns (ambiguous, trap_low, trap_high)."""
+    ties = Ties() if ties is None else ties
+    trap_low = 55.0 <= bpm <= 80.0
+    trap_high = 170.0 <= bpm <= 200.0
+    tol = max(2.0, res)
+
+    def support(b):  # cand_support (:420-432): the maximum score within tol (f32 distances)
+        best = 0.0
+        for c in cands:
+            if float(abs(f32(c[0]) - f32(b))) <= tol:
+                best = max(best, c[1])
+        return best
+
+    s_base, s_2x, s_half = support(bpm), support(bpm * 2.0), support(bpm * 0.5)  # x2, x0.5: exact in f32
+    family = (s_2x > 0.0 and ties.ge("gate-2x", s_2x, s_base * 0.90)) or \
+             (s_half > 0.0 and ties.ge("gate-half", s_half, s_base * 0.90))
+    fold_into_trap = 170.0 <= bpm * 2.0 <= 200.0
+    weak = agree == 0 or conf < 0.06
+    if _near(conf, 0.06, SCORE_TIE):
+        ties.append(("gate-weak", conf, 0.06))
+    return bool(trap_low or trap_high or family or (weak and fold_into_trap)), trap_low, trap_high
+
+
+def beat_contrast(nov, sr, hop, bpm, ties=None):
+    """beat_contrast_score (multi_resolution.rs:580-678), float64."""
+    n = nov.size
+    if n < 16 or not (math.isfinite(bpm) and bpm > 0):
+        return 0.0
+    fpb = 60.0 * sr / (bpm * hop)
+    if not math.isfinite(fpb) or fpb < 3.0:
+        return 0.0
+    if ties is not None and _near(fpb - math.floor(fpb), 0.5, 1e-5):
+        ties.append(("mr-period-round", fpb, 0.5))  # f32 frames-per-beat rounds either way
+    period = _round_half_away(fpb)
+    if not 3 <= period <= 512:
+        return 0.0
+    w = 2
+    pad = np.concatenate([np.zeros(w), nov, np.zeros(w)])  # every value is >= 0: 0-padding is exact
+    wmax = np.max(np.stack([pad[j:j + n] for j in range(2 * w + 1)]), axis=0)
+    total = max(float(nov.sum()), 1e-6)
+    best = -1e9
+    for ph in range(period):
+        idx = np.arange(ph, n, period)
+        bm = float(wmax[idx].mean()) if idx.size else 0.0
+        hm = tm = 0.0
+        if period >= 6:
+            j = idx + period // 2
+            j = j[j < n]
+            hm = float(wmax[j].mean()) if j.size else 0.0
+        if period >= 9:
+            j1, j2 = idx + period // 3, idx + (2 * period) // 3
+            # the reference interleaves the 1/3 and 2/3 windows per beat; a mean does not care
+            jj = np.concatenate([j1[j1 < n], j2[j2 < n]])
+            tm = float(wmax[jj].mean()) if jj.size else 0.0
+        contrast = bm - 0.60 * hm - 0.40 * tm
+        best = max(best, min(max(contrast / max(total / n, 1e-6), -10.0), 10.0))
+    return best
+
+
+def multi_resolution(x, sr, stft, frame_size=2048, lo=40.0, hi=240.0, res=1.0, mr=MR_DEFAULT, band=BAND_DEFAULT,
+                     ties=None):
+    """multi_resolution_tempogram_from_samples (multi_resolution.rs:205-901) on the trimmed,
+    normalised samples x.  stft(x, nfft, hop) supplies the magnitudes (the spec-pinned STFT).
+    Returns (bpm, confidence, agreement)."""
+    ties = Ties() if ties is None else ties
+    if x.size < frame_size:
+        raise ValueError("Audio too short for STFT")
+    top_k = max(mr["top_k"], 1)
+    aux_k = min(max(top_k * 4, 25), 200)
+    tol = max(2.0, res)
+    spec = {h: stft(x, frame_size, h).astype(np.float64) for h in (256, 512, 1024)}
+    c256 = estimate_bpm_tempogram(spec[256], sr, 256, lo, hi, res, band)[3][:aux_k]
+    c512 = estimate_bpm_tempogram(spec[512], sr, 512, lo, hi, res, band)[3][:top_k]
+    c1024 = estimate_bpm_tempogram(spec[1024], sr, 1024, lo, hi, res, band)[3][:aux_k]
+    w512, w256, w1024, dt = mr["w512"], mr["w256"], mr["w1024"], mr["dt512"]
+
+    def lk(c, b):
+        return cand_lookup(c, b, tol, ties)
+
+    hyps = []
+    for t in [c[0] for c in c512[:top_k]]:
+        if not (math.isfinite(t) and t > 0):
+            continue
+        st = (lk(c512, t), lk(c256, t), lk(c1024, t))
+        s2 = (lk(c512, 2 * t), lk(c256, 2 * t), lk(c1024, 2 * t))
+        sh = (lk(c512, 0.5 * t), lk(c256, 0.5 * t), lk(c1024, 0.5 * t))
+        h_t = w512 * st[0] + w256 * st[1] + w1024 * st[2]
+        h_2t = w512 * (dt * st[0] + (1 - dt) * s2[0]) + w256 * s2[1] + w1024 * s2[2]
+        h_h = w512 * (dt * st[0] + (1 - dt) * sh[0]) + w256 * sh[1] + w1024 * sh[2]
+        if ties.gt("mr-1024-half", st[2], sh[2] * 1.02):
+            h_h *= 0.90
+        if ties.gt("mr-1024-2t", st[2], s2[2] * 1.02):
+            h_2t *= 0.90
+        eps = 1e-6
+        r2 = (s2[1] + eps) / (st[1] + eps)
+        if not ties.ge("mr-r2-110", r2, 1.10):
+            h_2t *= 0.75
+        if not ties.ge("mr-r2-100", r2, 1.00):
+            h_2t *= 0.75
+        rh = (sh[2] + eps) / (st[2] + eps)
+        if not ties.ge("mr-rh-110", rh, 1.10):
+            h_h *= 0.75
+        if not ties.ge("mr-rh-100", rh, 1.00):
+            h_h *= 0.75
+        local = [(b, s) for b, s in ((t, h_t), (2 * t, h_2t), (0.5 * t, h_h)) if lo <= b <= hi]
+        local = [(b, s * (0.80 if b > 210.0 else 0.90 if b > 180.0 else 0.92 if b < 60.0 else 1.0)) for b, s in local]
+        if not local:
+            continue
+        # (a near tie in this order never matters: the two near-equal leaders have a margin below
+        # margin_threshold, and either order then keeps T with h_t)
+        local.sort(key=lambda h: -h[1])  # stable, as the reference's sort_by
+        bb, bs = local[0]
+        margin = bs - (local[1][1] if len(local) > 1 else 0.0)
+        cb, cs = bb, bs
+        below = not ties.ge("mr-margin", margin, mr["margin"])
+        if abs(cb - t) > 1e-3 and below:
+            cb, cs = t, h_t
+        if below and mr["human_prior"] and 70.0 <= cb <= 180.0 and margin < 0.05:
+            cs += 0.05
+        hyps.append((cb, cs))
+    if not hyps:
+        raise ValueError("Multi-resolution fusion produced no hypotheses")
+    order = sorted(range(len(hyps)), key=lambda i: -hyps[i][1])  # stable, as sort_by
+    nov = novelty_full(spec[512], band)
+
+    def finish(order, ties):
+        """dedup (:531-546), folds (:697-751), triplet family (:764-867), confidence and agreement
+        (:869-886) for one order of the hypotheses"""
+        uniq = []
+        for i in order:
+            h = hyps[i]
+            if any(abs(u[0] - h[0]) < 0.75 for u in uniq):
+                continue
+            uniq.append(h)
+            if len(uniq) >= 8:
+                break
+        best = uniq[0]
+
+        def total_support(b):
+            s3 = (cand_lookup(c256, b, tol, ties), cand_lookup(c512, b, tol, ties), cand_lookup(c1024, b, tol, ties))
+            return sum(s3), sum(v > 0 for v in s3)
+
+        if best[0] >= 170.0:  # fold-down
+            half = best[0] * 0.5
+            if 70.0 <= half <= 120.0:
+                sb, _ = total_support(best[0])
+                sh_, ah = total_support(half)
+                ratio = sh_ / sb if sb > 0 else 0.0
+                if ah >= 3 and sh_ > 0 and sb > 0 and ties.ge("mr-fold-down", ratio, 0.45):
+                    best = (half, sh_)
+        if best[0] <= 80.0:  # fold-up
+            dbl = best[0] * 2.0
+            if 70.0 <= dbl <= 180.0:
+                sb, _ = total_support(best[0])
+                sd, ad = total_support(dbl)
+                ratio = sd / sb if sb > 0 else 0.0
+                if ad >= 2 and sd > 0 and sb > 0 and ties.ge("mr-fold-up", ratio, 0.55):
+                    best = (dbl, sd)
+        if 70.0 <= best[0] <= 180.0 and nov.size:  # triplet / compound family
+            fams = []
+            for f in (f32(1.0), f32(3.0) / f32(2.0), f32(2.0) / f32(3.0), f32(4.0) / f32(3.0), f32(3.0) / f32(4.0)):
+                b = float(f32(f32(best[0]) * f))  # f32 BPM products (:786), discrete like the candidates
+                if not (math.isfinite(b) and lo <= b <= hi and 70.0 <= b <= 180.0):
+                    continue
+                sup, ag = total_support(b)
+                if ag < 2 or sup <= 0:
+                    continue
+                fams.append((b, sup, beat_contrast(nov, sr, 512, b, ties)))
+            if len(fams) >= 2:
+                bsup = max(max(f[1] for f in fams), 1e-6)
+                alt = max([f[1] / bsup for f in fams if abs(f[0] - best[0]) > 0.75] + [0.0])
+                if ties.ge("mr-family-alt", alt, 0.45):
+                    chosen, cscore = fams[0], -1e9
+                    for f in fams:
+                        sc = f[2] + 0.35 * min(max(f[1] / bsup, 0.0), 1.0)
+                        if ties.gt("mr-family-pick", sc, cscore, 1e-4):
+                            chosen, cscore = f, sc
+                    cur = beat_contrast(nov, sr, 512, best[0], ties)
+                    if abs(chosen[0] - best[0]) > 0.75 and ties.ge("mr-family-align", chosen[2], cur + 0.40, 1e-4):
+                        best = (chosen[0], chosen[1])
+        second = uniq[1][1] if len(uniq) > 1 else 0.0
+        conf = min(max(max(best[1] - second, 0.0) / best[1], 0.0), 1.0) if best[1] > 1e-6 else 0.0
+        agree = sum(cand_lookup(c, best[0], tol, ties) > 0 for c in (c256, c512, c1024))
+        return best[0], conf, int(agree)
+
+    out = finish(order, ties)
+    # hypotheses whose scores differ by less than f32 can resolve may sort either way: the order
+    # matters only if the other order changes the result (BPM, agreement, confidence beyond 1e-4)
+    for k in range(len(order) - 1):
+        a, b = hyps[order[k]], hyps[order[k + 1]]
+        if _near(a[1], b[1], SCORE_TIE):
+            alt = order[:k] + [order[k + 1], order[k]] + order[k + 2:]
+            o2 = finish(alt, Ties())
+            if abs(o2[0] - out[0]) > 1e-4 or o2[2] != out[2] or abs(o2[1] - out[1]) > 1e-4:
+                ties.append(("mr-hyp-order", a, b))
+    return out
+
+
+def accept_multi_resolution(base, mr_est, trap_low, trap_high, ties=None):
+    """The acceptance rule of src/lib.rs:511-545: (bpm, conf, agree) tuples -> used_mr."""
+    ties = Ties() if ties is None else ties
+    bb, bc, ba = base
+    mb, mc, ma = mr_est
+    rel = max(mb / bb, bb / mb) if bb > 1e-6 else 1.0
+    family = abs(rel - 2.0) < 0.05 or abs(rel - 1.5) < 0.05 or abs(rel - 4.0 / 3.0) < 0.05
+    forbid = bb <= 180.0 and mb > 180.0
+    return (not forbid) and (ties.ge("acc-conf", mc, bc + 0.05)
+                             or (ma > ba and ties.ge("acc-agree", mc, bc * 0.90))
+                             or ((trap_low or trap_high) and family and ties.ge("acc-family", mc, bc * 0.88)
+                                 and (70.0 <= mb <= 180.0 or bb > 180.0)))
