@@ -771,3 +771,130 @@ def accept_multi_resolution(base, mr_est, trap_low, trap_high, ties=None):
                              or (ma > ba and ties.ge("acc-agree", mc, bc * 0.90))
                              or ((trap_low or trap_high) and family and ties.ge("acc-family", mc, bc * 0.88)
                                  and (70.0 <= mb <= 180.0 or bb > 180.0)))
+
+
+# ---- onset detection (a4, a6, a7, a8) ----
+ONSET_DEFAULT = dict(percentile=0.80, tol_ms=50, weights=(0.25, 0.25, 0.25, 0.25), energy_db=-20.0)  # config.rs:601-604
+
+
+def _peaks(flux, thr, ties, tag):
+    """Peak picking shared by the three detectors: interior i (1 <= i < n-1) with flux > thr,
+    > prev, >= next; the first value with > thr and >= its successor; the last with > thr and >
+    its predecessor.  Returns flux indices, sorted, unique."""
+    n = flux.size
+    scale = max(float(flux.max()), 1e-30) if n else 1.0
+
+    def gt(a, b):
+        if ties is not None and _near(a, b, 1e-6 * scale):
+            ties.append((tag, a, b))
+        return a > b
+
+    def ge(a, b):
+        if ties is not None and _near(a, b, 1e-6 * scale):
+            ties.append((tag, a, b))
+        return a >= b
+
+    out = [i for i in range(1, n - 1) if gt(flux[i], thr) and gt(flux[i], flux[i - 1]) and ge(flux[i], flux[i + 1])]
+    if n > 1 and gt(flux[0], thr) and ge(flux[0], flux[1]):
+        out.append(0)
+    if n > 1 and gt(flux[n - 1], thr) and gt(flux[n - 1], flux[n - 2]):
+        out.append(n - 1)
+    return sorted(set(out))
+
+
+def energy_flux_onsets(x, frame, hop, threshold_db=-20.0, ties=None):
+    """detect_energy_flux_onsets (energy_flux.rs:67-243) on samples x: onset sample positions."""
+    n = x.size
+    if n == 0 or frame > n:
+        return []
+    nf = (n - frame) // hop + 1
+    if nf < 2:
+        return []
+    x = x.astype(np.float64)
+    c = np.concatenate([[0.0], np.cumsum(x * x)])
+    s = np.arange(nf) * hop
+    rms = np.sqrt((c[s + frame] - c[s]) / frame)
+    flux = np.maximum(np.diff(rms), 0.0)
+    mx = float(flux.max())
+    if mx <= EPS:
+        return []
+    thr = mx * 10.0 ** (threshold_db / 20.0)
+    on = [(i + 1) * hop for i in _peaks(flux, thr, ties, "energy-peak") if (i + 1) * hop < n]
+    out = []
+    for o in on:  # dedup: at least hop / 2 after the last kept onset
+        if not out or o >= out[-1] + hop // 2:
+            out.append(o)
+    return out
+
+
+def _percentile_threshold(flux, pct):
+    srt = np.sort(flux)
+    idx = min(int(f32(f32(srt.size) * f32(pct))), srt.size - 1)  # f32 index arithmetic, truncated
+    return float(srt[idx])
+
+
+def spectral_flux_onsets(M, pct, ties=None):
+    """detect_spectral_flux_onsets (spectral_flux.rs:69-221): onset frame indices."""
+    if M.shape[0] < 2:
+        return []
+    mx = M.max(axis=1, initial=0.0)
+    N = np.where((mx > EPS)[:, None], M / np.where(mx > EPS, mx, 1.0)[:, None], 0.0)
+    d = np.maximum(N[1:] - N[:-1], 0.0)
+    flux = np.sqrt((d * d).sum(axis=1))
+    return [i + 1 for i in _peaks(flux, _percentile_threshold(flux, pct), ties, "spectral-peak")]
+
+
+def hfc_onsets(M, pct, ties=None):
+    """detect_hfc_onsets (hfc.rs:76-214): onset frame indices."""
+    if M.shape[0] < 2:
+        return []
+    h = (M * M * np.arange(M.shape[1], dtype=np.float64)).sum(axis=1)
+    flux = np.maximum(np.diff(h), 0.0)
+    return [i + 1 for i in _peaks(flux, _percentile_threshold(flux, pct), ties, "hfc-peak")]
+
+
+def vote_onsets(lists, weights, tol_ms, sr):
+    """vote_onsets (consensus.rs:111-287): clusters in arrival order (an onset joins the first
+    cluster holding a member within the tolerance), centre = integer mean, confidence = weight
+    share; candidates sorted by confidence, descending, stable."""
+    tol = int(f32(f32(f32(tol_ms) / f32(1000.0)) * f32(sr)))  # discrete: the reference's f32 arithmetic
+    allo = sorted(((s, m) for m, l in enumerate(lists) for s in l), key=lambda o: o[0])  # stable by sample
+    clusters = []
+    for s, m in allo:
+        for cl in clusters:
+            if any(abs(s - e) <= tol for e, _ in cl):
+                cl.append((s, m))
+                break
+        else:
+            clusters.append([(s, m)])
+    wmax = float(sum(weights))
+    cands = []
+    for cl in clusters:
+        centre = sum(s for s, _ in cl) // len(cl)
+        tw = sum(weights[m] for _, m in cl)
+        cands.append((centre, min(max(tw / wmax, 0.0), 1.0) if wmax > 0 else 0.0, len({m for _, m in cl})))
+    cands.sort(key=lambda c: -c[1])
+    return cands
+
+
+def consensus_onsets(x, sr, M, frame=2048, hop=512, cfg=ONSET_DEFAULT, ties=None):
+    """The onset stage of src/lib.rs:152-289 (default config: energy flux on the trimmed samples,
+    spectral flux and HFC on the hop spectrogram, consensus vote, >= 2 methods else all).
+    Returns (energy, spectral, hfc, chosen) as sample positions."""
+    n = x.size
+    energy = energy_flux_onsets(x, frame, hop, cfg["energy_db"], ties)
+
+    def to_samples(frames):
+        return sorted({f * hop for f in frames if f * hop < n})
+
+    spectral = to_samples(spectral_flux_onsets(M, cfg["percentile"], ties))
+    hfc = to_samples(hfc_onsets(M, cfg["percentile"], ties))
+    chosen = energy
+    if M.shape[0] > 0:
+        cands = vote_onsets([energy, spectral, hfc, []], cfg["weights"], cfg["tol_ms"], sr)
+        strong = sorted({c[0] for c in cands if c[2] >= 2})
+        anyc = sorted({c[0] for c in cands})
+        pick = strong if strong else anyc
+        if pick:
+            chosen = pick
+    return energy, spectral, hfc, chosen
