@@ -225,8 +225,11 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
                 continue;
             }
         }
-        for (int j = 0; j < CW; j++) {  // not unrolled: the early exit keeps it a loop
-            if (j >= nb) break;
+        // unrolled (Wm / Rw are register windows indexed by j); the chunk's valid bins are a guard,
+        // not an early exit, so the unroll is complete
+#pragma unroll
+        for (int j = 0; j < CW; j++) {
+            if (j >= nb) continue;
             const int b = c0 + j;
             const int s = b & (W - 1);
             const float m = Mt[ro][s];

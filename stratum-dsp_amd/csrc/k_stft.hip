@@ -119,23 +119,20 @@ __device__ __forceinline__ float sqrt_cr(float x) {
 }
 
 // Correctly rounded f32 sqrt without compare masks or branches, for x = +0 and x in [2^-96, inf):
-// the same v_sqrt_f32 + +-1 ulp FMA-residual correction as sqrt_cr, with the two decisions taken
-// from the residuals' sign bits (rm <= 0 -> s - 1 ulp, rp > 0 -> s + 1 ulp; an exact zero residual
-// is +0, never -0).  x = +0 gives sm = NaN, whose residual's sign is unspecified: the final
-// signed max with 0 maps the possible -1 back to +0.  Inputs outside that set (subnormal-scale x,
-// inf, NaN) are recorded in lo / hi (min of bits - 1, max of bits) for the caller's fix-up pass.
+// Markstein's step from the hardware reciprocal square root, y ~ 1/sqrt(x): s0 = x y, h = y / 2,
+// r = x - s0^2 (exact by FMA), s = s0 + r h.  x = +0 takes y from max(x, 2^-126), which is finite,
+// so s0 = +0 and s = +0.  tools/check_sqrt2.hip checks it against the correctly rounded sqrtf on
+// every such f32 on gfx950 (the only mismatch is x = +inf).  5 VALU + 1 transcendental, against 11
+// + 1 for the +-1 ulp residual correction of v_sqrt's result it replaces.  Inputs outside that set
+// (subnormal-scale x, inf, NaN) are recorded in lo / hi (min of bits - 1, max of bits) for the
+// caller's fix-up pass.
 __device__ __forceinline__ float sqrt_fast(float x, uint32_t& lo, uint32_t& hi) {
     const uint32_t u = __float_as_uint(x);
     lo = min(lo, u - 1u);
     hi = max(hi, u);
-    const float s = __builtin_amdgcn_sqrtf(x);
-    const uint32_t si = __float_as_uint(s);
-    const float sm = __uint_as_float(si - 1u), sp = __uint_as_float(si + 1u);
-    const float rm = __builtin_fmaf(-sm, s, x);
-    const float rp = __builtin_fmaf(-sp, s, x);
-    const int dm = (int)(__float_as_uint(rm) - 1u) >> 31;  // -1 iff rm <= 0
-    const uint32_t up = (0u - __float_as_uint(rp)) >> 31;  // 1 iff rp > 0
-    return __int_as_float(max((int)(si + (uint32_t)dm + up), 0));
+    const float y = __builtin_amdgcn_rsqf(__builtin_fmaxf(x, 0x1p-126f));
+    const float s0 = x * y, h = 0.5f * y;
+    return __builtin_fmaf(__builtin_fmaf(-s0, s0, x), h, s0);
 }
 // true when some input of sqrt_fast was outside its exact range
 __device__ __forceinline__ bool sqrt_fast_missed(uint32_t lo, uint32_t hi) {
@@ -885,21 +882,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             const bool live = i > 0;
             const __amdgpu_buffer_rsrc_t ro = rsrc_of(row0 + (int64_t)(i - 1) * stride, live ? 4u * (M + 1) : 0u);
             uint32_t lo = 0xFFFFFFFFu, hi = 0u;
-            // |X| = 2^-33 sqrt(e) with the exact fast sqrt; the range test is on v_sqrt's result:
-            // s in [2^-47, inf) implies e > 2^-96 (1-ulp v_sqrt), where the correction is exact
-            auto sq = [&](float yx, float yy) {
-                const float x = __builtin_fmaf(yx, yx, yy * yy);
-                const float s = __builtin_amdgcn_sqrtf(x);
-                const uint32_t si = __float_as_uint(s);
-                lo = min(lo, si - 1u);
-                hi = max(hi, si);
-                const float sm = __uint_as_float(si - 1u), sp = __uint_as_float(si + 1u);
-                const float rm = __builtin_fmaf(-sm, s, x);
-                const float rp = __builtin_fmaf(-sp, s, x);
-                const int dm = (int)(__float_as_uint(rm) - 1u) >> 31;
-                const uint32_t up = (0u - __float_as_uint(rp)) >> 31;
-                return 0x1p-33f * __int_as_float(max((int)(si + (uint32_t)dm + up), 0));
-            };
+            // |X| = 2^-33 sqrt(e) with the exact fast sqrt
+            auto sq = [&](float yx, float yy) { return 0x1p-33f * sqrt_fast(__builtin_fmaf(yx, yx, yy * yy), lo, hi); };
             auto st = [&](float mag, int voff, int soff) {
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mag), ro, voff, soff, 0);
             };
@@ -918,7 +902,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                 st(sq(__builtin_fmaf(w.x, dx, __builtin_fmaf(-w.y, dy, sx)), __builtin_fmaf(w.x, dy, __builtin_fmaf(w.y, dx, sy))),
                    vmid, 0);
             }
-            const bool missed = __builtin_amdgcn_ballot_w64(lo < 0x27FFFFFFu || hi >= 0x7F800000u) != 0;
+            const bool missed = __builtin_amdgcn_ballot_w64(sqrt_fast_missed(lo, hi)) != 0;
             miss |= (uint64_t)(missed && live) << ((i - 1) & 63);
         }
         if (i == nf) break;
