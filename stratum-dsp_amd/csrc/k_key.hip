@@ -149,14 +149,14 @@ __global__ __launch_bounds__(MASK_T) void k_mask_r(float* __restrict__ mags, int
     for (int j = 0; j < RX; j++) X[j] = 0.0f;
     float prev = 0.0f;
     auto emit = [&](float a, int64_t den, float xr, int64_t t) {
-        col[t * stride] = mask_elem<M, PW>(a, den, xr, p, inv_w);
+        __builtin_nontemporal_store(mask_elem<M, PW>(a, den, xr, p, inv_w), &col[t * stride]);
     };
     for (int64_t base = 0; base < F + M; base += R) {
         float xv[R];
         if (base >= 2 * M && base + R <= F) {
             // interior block: every step has a full window; no edge conditions
 #pragma unroll
-            for (int u = 0; u < R; u++) xv[u] = col[(base + u) * stride];
+            for (int u = 0; u < R; u++) xv[u] = __builtin_nontemporal_load(&col[(base + u) * stride]);
 #pragma unroll
             for (int u = 0; u < R; u++) {
                 prev = prev + xv[u];
@@ -167,7 +167,7 @@ __global__ __launch_bounds__(MASK_T) void k_mask_r(float* __restrict__ mags, int
             continue;
         }
 #pragma unroll
-        for (int u = 0; u < R; u++) xv[u] = base + u < F ? col[(base + u) * stride] : 0.0f;
+        for (int u = 0; u < R; u++) xv[u] = base + u < F ? __builtin_nontemporal_load(&col[(base + u) * stride]) : 0.0f;
 #pragma unroll
         for (int u = 0; u < R; u++) {
             const int64_t tin = base + u;

@@ -9,6 +9,7 @@ O=$R/gpurun_out/prof_$tag
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 python3 $R/bench.py > $O/bench.json 2> $O/bench.err &&
+timeout -k 10 600 python3 $R/bench.py > $O/bench2.json 2> $O/bench2.err &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/conc -o $tag -- python3 $R/bench.py --tracks 1024 --steps 2 --warmup 1 --no-cpu-baseline > $O/conc.json 2> $O/conc.err &&
 SDSP_SERIAL_STREAMS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/serial -o $tag -- python3 $R/bench.py --tracks 1024 --steps 2 --warmup 1 --no-cpu-baseline > $O/serial.json 2> $O/serial.err &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/probe -o $tag -- python3 $R/tools/stft_probe.py > $O/probe.jsonl 2> $O/probe.err &&
@@ -20,4 +21,5 @@ python3 $R/tools/timeline.py $O/conc/${tag}_kernel_trace.csv 3000 > $O/conc_time
 python3 $R/tools/streams.py $O/conc/${tag}_kernel_trace.csv 3000 >> $O/conc_timeline.txt &&
 python3 $R/tools/pmc_stft.py 8192 $O/fetch/${tag}_counter_collection.csv $O/write/${tag}_counter_collection.csv $O/fetch.log > $O/pmc_stft8192.json &&
 timeout -k 10 300 python3 $R/bench.py --tracks 64 --steps 1 --warmup 0 --cpu-tracks 32 --cpu-1thread-tracks 32 > $O/cpu1.json 2> $O/cpu1.err &&
+timeout -k 10 500 bash $R/tools/pmc_stft_sq.sh $tag > $O/sq_isolated.txt 2>&1 &&
 echo "profiles done"
