@@ -155,3 +155,23 @@ def test_unnormalised_int_scale_input():
         assert np.isfinite(got["bpm"]) and np.isfinite(got["key_confidence"])
         assert not parity.diff_results(got, ref), parity.diff_results(got, ref)
         assert parity.exact_fraction(got, ref) == 1.0
+
+
+def test_unnormalised_overflowing_magnitudes():
+    """Samples at 2^60 with enable_normalization = false: a tone bin's |X|^2 overflows f32 in the
+    reference's own formula (extractor.rs:352), so those magnitudes are +inf.  k_features then
+    meets quotients X / max outside its FMA-corrected range (an inf operand) and redoes those
+    chunks with the IEEE division; the whole analysis (NaN / inf propagation included) equals the
+    oracle's."""
+    cfg = sdsp.default_config()
+    cfg.enable_normalization = 0
+    x, *_ = synth.make_track(5600, seconds=12.0)
+    x = (x * np.float32(2.0 ** 60)).astype(np.float32)
+    st, ref = oracle.analyze(x, 44100, config=cfg)
+    if st != 0:  # the reference fails this input: the engine fails it with the same error
+        with pytest.raises(sdsp.AnalysisError) as ei:
+            sdsp.analyze_audio(x, 44100, config=cfg)
+        assert str(ei.value) == ref, (str(ei.value), ref)
+        return
+    got = sdsp.analyze_audio(x, 44100, config=cfg)
+    assert not parity.diff_results(got, ref), parity.diff_results(got, ref)
