@@ -150,9 +150,25 @@ def spawn_ranks(n):
     for r in range(n):
         e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=e))
-    rcs = [p.wait() for p in procs]
-    bad = [rc for rc in rcs if rc != 0]
-    return bad[0] if bad else 0
+    # poll: a rank that dies before the barrier would leave its siblings blocked in gloo, so the
+    # first non-zero exit ends the others and is returned
+    while True:
+        rcs = [p.poll() for p in procs]
+        bad = [rc for rc in rcs if rc not in (None, 0)]
+        if bad:
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            return bad[0]
+        if all(rc == 0 for rc in rcs):
+            return 0
+        time.sleep(0.2)
 
 
 def main():
@@ -183,6 +199,8 @@ def main():
     bpm_mode = mix_default if args.bpm_mode < 0 else args.bpm_mode
     eng = (DryEngine if args.dry_run else Engine)(local)
     tdist = None
+    if args.dry_run and os.environ.get("SDSP_BENCH_FAIL_RANK") == str(rank):
+        raise SystemExit(3)  # test hook (dry runs only): this rank dies before the process group
     if world > 1:
         import torch.distributed as tdist
 

@@ -5,6 +5,7 @@
 // paths, key scoring options, chroma front-ends).  Only degenerate sizes raise NotImplemented.
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <sstream>
@@ -729,8 +730,18 @@ void set_trace(const Trace& t) {
     for (float v : t.energies) es += v;
     for (float v : t.weights) ws += v;
     s.precision(17);
-    s << "\"chroma_sum\":" << cs << ",\"chroma_sq\":" << cq << ",\"energy_sum\":" << es << ",\"weights_sum\":" << ws
-      << ",";
+    // non-finite sums (non-finite input) as the tokens Python's json accepts
+    auto num = [](double v) -> std::string {
+        if (v != v) return "NaN";
+        if (v == INFINITY) return "Infinity";
+        if (v == -INFINITY) return "-Infinity";
+        std::ostringstream o;
+        o.precision(17);
+        o << v;
+        return o.str();
+    };
+    s << "\"chroma_sum\":" << num(cs) << ",\"chroma_sq\":" << num(cq) << ",\"energy_sum\":" << num(es)
+      << ",\"weights_sum\":" << num(ws) << ",";
     s << "\"n_key_frames\":" << t.energies.size();
     s << "}";
     g_trace_json = s.str();

@@ -174,6 +174,11 @@ static void hpcp_frame_band(const float* m, size_t bins, uint32_t sr, size_t fft
         if (f > fmax) break;
         const float mv = sc[bin], mp = sc[bin - 1], mn = sc[bin + 1];
         if (mv <= mp || mv < mn) continue;
+        // A NaN score (a NaN magnitude: non-finite input) passes the reference's local-maximum
+        // test, and its rank is then implementation-defined (select_nth_unstable_by with
+        // partial_cmp -> Equal: parity unpinned).  The restatement, like the kernels, ranks NaN
+        // below every peak, i.e. never selects it (its weight powf(max(NaN, 0), p) would be 0).
+        if (mv != mv) continue;
         peaks.push_back({bin, mv});
     }
     if (peaks.empty()) return;

@@ -104,6 +104,41 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
     };
     const float mx_c = own_ok ? fmax_of(f) : 0.0f;
     const bool cn = mx_c > EPS;
+    // X / max by one correctly rounded reciprocal per frame and an FMA correction per bin:
+    // q0 = m yr, q = q0 + (m - max q0) yr is the correctly rounded m / max for normal operands whose
+    // quotient and residual stay normal (tools/check_div_fast.hip: all 2^46 mantissa pairs, and
+    // v_rcp-free here: yr is an IEEE division).  That holds for m = 0 and m in [max 2^-120, inf)
+    // with m >= 2^-100 and max <= 2^100; cn = false gives yr = 0, so q = 0 as the reference's
+    // zeroed frame.  A chunk where some lane of the wave saw another m redoes its flux terms with
+    // the IEEE division (rare: needs magnitudes 2^-100 below the frame maximum, or inf / NaN).
+    const float yr = cn ? 1.0f / mx_c : 0.0f;
+    const bool q_frame_ok = !cn || mx_c <= 0x1p100f;
+    const uint32_t q_lim = __float_as_uint(sd_maxf(0x1p-100f, mx_c * 0x1p-120f)) - 1u;
+    uint32_t q_lo = 0xFFFFFFFFu, q_hi = 0u;  // min of bits(m) - 1, max of bits(m) over the chunk
+    auto quot = [&](float m) {
+        const uint32_t u = __float_as_uint(m);
+        q_lo = min(q_lo, u - 1u);
+        q_hi = max(q_hi, u);
+        const float q0 = m * yr;
+        return __builtin_fmaf(__builtin_fmaf(-mx_c, q0, m), yr, q0);
+    };
+    // the chunk's flux terms again with the IEEE division, from the fold's value at the chunk
+    // start, when some lane's quotient left the exact range
+    auto quot_redo = [&](int c0, int nb, float so_start) {
+        const bool miss = !q_frame_ok || q_lo < q_lim || q_hi >= 0x7F800000u;
+        q_lo = 0xFFFFFFFFu;
+        q_hi = 0u;
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(miss) == 0, 1)) return;
+        so = so_start;
+        for (int j = 0; j < nb; j++) {
+            const float m = Mt[ro][(c0 + j) & (W - 1)];
+            const float cv = cn ? m / mx_c : 0.0f;
+            const float pv = __builtin_bit_cast(
+                float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, cv), 0x138, 0xf, 0xf, false));
+            const float d = max_bnn(cv - pv, 0.0f);
+            so += d * d;
+        }
+    };
 
     // rows f0-1 .. f0+FT_STEP-1 of the track; row r <-> frame f0-1+r
     const int64_t r_lo = f0 >= 1 ? 0 : 1;
@@ -198,6 +233,7 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
                     flush();
                     cur = vbc;
                 }
+                const float so_start = so;
 #pragma unroll
                 for (int j = 0; j < CW; j++) {
                     const int b = c0 + j;
@@ -208,7 +244,7 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
                     e[0] += ee;
                     h[0] += hh;
                     const float lc = Lt[ro][s];
-                    const float cv = cn ? m / mx_c : 0.0f;
+                    const float cv = quot(m);
                     const float pv = __builtin_bit_cast(
                         float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, cv), 0x138, 0xf, 0xf, false));
                     const float d = max_bnn(cv - pv, 0.0f);
@@ -222,11 +258,13 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
                         sb += df2;
                     }
                 }
+                quot_redo(c0, CW, so_start);
                 continue;
             }
         }
         // unrolled (Wm / Rw are register windows indexed by j); the chunk's valid bins are a guard,
         // not an early exit, so the unroll is complete
+        const float so_start = so;
 #pragma unroll
         for (int j = 0; j < CW; j++) {
             if (j >= nb) continue;
@@ -249,7 +287,7 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
             const float lc = Lt[ro][s];
             // X/max of this lane's frame, and of the previous frame from lane - 1 (its frame is
             // f - 1 for every lane that reads it: lanes 1-63; the helper's value is unused)
-            const float cv = cn ? m / mx_c : 0.0f;
+            const float cv = quot(m);
             const float pv = __builtin_bit_cast(
                 float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, cv), 0x138 /* wave_shr:1 */, 0xf, 0xf, false));
             if (P.n_mels > 0) {
@@ -316,6 +354,7 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
                 }
             }
         }
+        quot_redo(c0, nb, so_start);
     }
     flush();
     if (!valid) return;

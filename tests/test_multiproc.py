@@ -6,6 +6,7 @@ import json
 import os
 import socket
 import subprocess
+import time
 import sys
 
 import pytest
@@ -83,6 +84,18 @@ def test_bench_spawns_ranks_without_torchrun():
     assert d["config"]["baseline_config"] == 3
     assert abs(d["value"] - 3 * 2 * 2 / (d["ms_per_step"] * 2 / 1000.0)) / d["value"] < 1e-2
     assert len(d["step_ms"]["all"]) == 2
+
+
+def test_bench_spawned_rank_failure_ends_the_job():
+    """A rank that dies before the barrier ends its siblings (which would otherwise wait in gloo)
+    and the parent exits with its status instead of hanging."""
+    env = dict(os.environ, SDSP_BENCH_FAIL_RANK="1")
+    t0 = time.time()
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0",
+                          "--tracks", "2", "--seconds", "1", "--dry-run"], capture_output=True, text=True, timeout=200,
+                         cwd=ROOT, env=env)
+    assert out.returncode == 3, (out.returncode, out.stderr[-1000:])
+    assert time.time() - t0 < 150
 
 
 @pytest.mark.parametrize("workload,cfg", [("mixed", 4), ("bpm-only", 5)])
