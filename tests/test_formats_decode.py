@@ -1,0 +1,452 @@
+"""The decode front-end's other containers and codecs (stratum-dsp_amd/csrc/host_formats.hip and
+the ADPCM paths of host_decode.hip) through the C ABI (sdsp_decode_audio_file), on the CPU.
+
+The reference decodes with symphonia 0.5 built with every feature (Cargo.toml:15) and converts its
+buffers as examples/analyze_file.rs:25-180 shows.  Neither symphonia nor any encoder for these
+formats is in this image and the reference ships no such fixture, so each file is written here
+from its format specification and the expected samples follow the examples' conversion; parity
+against symphonia itself is unpinned.  The PCM containers are lossless, so their expected values
+are exact; the ADPCM expectations come from a restatement of the decoding algorithm below and are
+also checked to track the encoded signal.
+
+Covered: AIFF and AIFF-C (big-endian 16/24/32-bit PCM, 'sowt', 'fl32', 'fl64', G.711, the
+80-bit extended sample rate, odd chunk padding, the 8-bit S8 case the examples reject), CAF
+('lpcm' integer and float in both byte orders, G.711, a data chunk of unknown size), Ogg FLAC
+(metadata and audio packets, packets across pages, a page with a bad CRC), IMA and Microsoft
+ADPCM in WAV (mono and stereo, a final partial block), and the named errors for MP3, AAC, MP4,
+Vorbis, Opus and ALAC.
+"""
+import struct
+
+import numpy as np
+import pytest
+
+import flac_enc as fe
+import sdsp
+
+F32 = np.float32
+
+
+def _decode(tmp_path, data, name):
+    p = tmp_path / name
+    p.write_bytes(data)
+    return sdsp.decode_audio_file(str(p))
+
+
+def _mono(chans):
+    """The examples' mix: f32 channel values summed from -0.0 in channel order, / channels."""
+    if len(chans) == 1:
+        return np.asarray(chans[0], F32)
+    acc = np.full(len(chans[0]), F32(-0.0), F32)
+    for c in chans:
+        acc = (acc + np.asarray(c, F32)).astype(F32)
+    return (acc / F32(len(chans))).astype(F32)
+
+
+def _ints(n, bits, seed, nch):
+    rng = np.random.default_rng(seed)
+    amp = (1 << (bits - 1)) - 1
+    t = np.arange(n)
+    out = []
+    for c in range(nch):
+        x = 0.7 * np.sin(2 * np.pi * t * (330 + 40 * c) / 44100) + 0.1 * rng.standard_normal(n)
+        v = np.clip(np.round(x * amp), -amp - 1, amp).astype(np.int64)
+        v[:2] = [amp, -amp - 1]
+        out.append(v)
+    return out
+
+
+def _int_bytes(chans, bits, big):
+    n = len(chans[0])
+    width = bits // 8
+    buf = bytearray()
+    for i in range(n):
+        for c in chans:
+            buf += int(c[i]).to_bytes(width, "big" if big else "little", signed=True)
+    return bytes(buf)
+
+
+def _int_f32(chans, bits):
+    return [np.asarray(c, np.int64).astype(F32) / F32(2.0 ** (bits - 1)) for c in chans]
+
+
+def _alaw_s16(a):
+    a ^= 0x55
+    t = (a & 0x0F) << 4
+    seg = (a & 0x70) >> 4
+    if seg == 0:
+        t += 8
+    elif seg == 1:
+        t += 0x108
+    else:
+        t = (t + 0x108) << (seg - 1)
+    return t if a & 0x80 else -t
+
+
+def _ulaw_s16(u):
+    u = ~u & 0xFF
+    t = ((u & 0x0F) << 3) + 0x84
+    t <<= (u & 0x70) >> 4
+    return (0x84 - t) if u & 0x80 else (t - 0x84)
+
+
+# ---- AIFF / AIFF-C ----
+def _ext80(rate):
+    """IEEE 754 80-bit extended big-endian of a positive integer."""
+    e = rate.bit_length() - 1
+    m = rate << (63 - e)
+    return struct.pack(">HQ", 16383 + e, m)
+
+
+def _chunk_be(cid, body):
+    return cid + struct.pack(">I", len(body)) + body + (b"\0" if len(body) & 1 else b"")
+
+
+def _aiff(nch, bits, rate, frames, data, comp=None, extra=b""):
+    comm = struct.pack(">hIh", nch, frames, bits) + _ext80(rate)
+    if comp is not None:
+        comm += comp + bytes([4]) + b"name" + b"\0"  # pascal string, padded to even length
+    ssnd = struct.pack(">II", 0, 0) + data
+    form = (b"AIFC" if comp is not None else b"AIFF") + extra + _chunk_be(b"COMM", comm) + _chunk_be(b"SSND", ssnd)
+    return b"FORM" + struct.pack(">I", len(form)) + form
+
+
+@pytest.mark.parametrize("bits", [16, 24, 32])
+@pytest.mark.parametrize("nch", [1, 2, 3])
+def test_aiff_pcm(tmp_path, bits, nch):
+    chans = _ints(3001, bits, bits + nch, nch)
+    data = _aiff(nch, bits, 48000, 3001, _int_bytes(chans, bits, True),
+                 extra=_chunk_be(b"NAME", b"odd"))  # an odd-sized chunk before COMM (pad byte)
+    x, sr = _decode(tmp_path, data, "t.aiff")
+    assert sr == 48000
+    assert x.tobytes() == _mono(_int_f32(chans, bits)).tobytes()
+
+
+@pytest.mark.parametrize("comp,bits,big", [(b"NONE", 16, True), (b"twos", 24, True), (b"sowt", 16, False),
+                                            (b"sowt", 32, False)])
+def test_aifc_integer(tmp_path, comp, bits, big):
+    chans = _ints(2000, bits, 7, 2)
+    data = _aiff(2, bits, 22050, 2000, _int_bytes(chans, bits, big), comp=comp)
+    x, sr = _decode(tmp_path, data, "t.aifc")
+    assert sr == 22050
+    assert x.tobytes() == _mono(_int_f32(chans, bits)).tobytes()
+
+
+@pytest.mark.parametrize("comp", [b"fl32", b"FL32", b"fl64"])
+def test_aifc_float(tmp_path, comp):
+    rng = np.random.default_rng(3)
+    a = rng.uniform(-1, 1, 1500)
+    b = rng.uniform(-1, 1, 1500)
+    a[0], b[0] = 1e-42, -0.0  # a subnormal, a negative zero
+    wide = comp == b"fl64"
+    fmt = ">d" if wide else ">f"
+    data = b"".join(struct.pack(fmt, v) for pair in zip(a, b) for v in pair)
+    x, _ = _decode(tmp_path, _aiff(2, 64 if wide else 32, 44100, 1500, data, comp=comp), "t.aifc")
+    want = _mono([a.astype(F32), b.astype(F32)])  # f64 -> f32 `as f32` (round to nearest)
+    assert x.tobytes() == want.tobytes()
+
+
+@pytest.mark.parametrize("comp", [b"ulaw", b"alaw"])
+def test_aifc_g711(tmp_path, comp):
+    codes = np.arange(256, dtype=np.uint8)
+    f = _ulaw_s16 if comp == b"ulaw" else _alaw_s16
+    x, _ = _decode(tmp_path, _aiff(1, 16, 8000, 256, codes.tobytes(), comp=comp), "t.aifc")
+    want = np.array([f(int(c)) for c in codes], np.int64).astype(F32) / F32(32768.0)
+    assert x.tobytes() == want.tobytes()
+
+
+def test_aiff_errors(tmp_path):
+    # 8-bit AIFF is signed PCM: symphonia's S8 buffer, which the examples' conversion rejects
+    with pytest.raises(sdsp.AnalysisError) as e:
+        _decode(tmp_path, _aiff(1, 8, 44100, 4, bytes(4)), "t.aiff")
+    assert "Unsupported audio format" in str(e.value)
+    with pytest.raises(sdsp.AnalysisError) as e:
+        _decode(tmp_path, _aiff(1, 16, 44100, 4, bytes(8), comp=b"ima4"), "t.aifc")
+    assert "ima4" in str(e.value)
+
+
+# ---- CAF ----
+def _caf(rate, fmt_id, flags, bpp, fpp, nch, bits, data, unknown_size=False):
+    desc = struct.pack(">d", float(rate)) + fmt_id + struct.pack(">IIIII", flags, bpp, fpp, nch, bits)
+    body = struct.pack(">I", 0) + data
+    out = b"caff" + struct.pack(">HH", 1, 0)
+    out += b"desc" + struct.pack(">q", len(desc)) + desc
+    out += b"free" + struct.pack(">q", 3) + b"abc"
+    out += b"data" + struct.pack(">q", -1 if unknown_size else len(body)) + body
+    return out
+
+
+@pytest.mark.parametrize("bits", [16, 24, 32])
+@pytest.mark.parametrize("little", [False, True])
+def test_caf_lpcm_int(tmp_path, bits, little):
+    chans = _ints(1777, bits, bits, 2)
+    w = bits // 8
+    data = _caf(96000, b"lpcm", 2 if little else 0, 2 * w, 1, 2, bits, _int_bytes(chans, bits, not little),
+                unknown_size=little)
+    x, sr = _decode(tmp_path, data, "t.caf")
+    assert sr == 96000
+    assert x.tobytes() == _mono(_int_f32(chans, bits)).tobytes()
+
+
+@pytest.mark.parametrize("bits", [32, 64])
+@pytest.mark.parametrize("little", [False, True])
+def test_caf_lpcm_float(tmp_path, bits, little):
+    rng = np.random.default_rng(bits)
+    v = rng.uniform(-1.5, 1.5, 999)
+    fmt = ("<" if little else ">") + ("d" if bits == 64 else "f")
+    data = b"".join(struct.pack(fmt, s) for s in v)
+    x, _ = _decode(tmp_path, _caf(44100, b"lpcm", 1 | (2 if little else 0), bits // 8, 1, 1, bits, data), "t.caf")
+    assert x.tobytes() == v.astype(F32).tobytes()
+
+
+def test_caf_ulaw_and_errors(tmp_path):
+    codes = np.arange(256, dtype=np.uint8)
+    x, _ = _decode(tmp_path, _caf(8000, b"ulaw", 0, 1, 1, 1, 8, codes.tobytes()), "t.caf")
+    assert x.tobytes() == (np.array([_ulaw_s16(int(c)) for c in codes], np.int64).astype(F32) / F32(32768.0)).tobytes()
+    with pytest.raises(sdsp.AnalysisError) as e:
+        _decode(tmp_path, _caf(44100, b"alac", 0, 0, 4096, 2, 16, bytes(16)), "t.caf")
+    assert "ALAC" in str(e.value)
+    with pytest.raises(sdsp.AnalysisError) as e:
+        _decode(tmp_path, _caf(44100, b"lpcm", 0, 1, 1, 1, 8, bytes(16)), "t.caf")
+    assert "Unsupported audio format" in str(e.value)
+
+
+# ---- Ogg FLAC ----
+def _ogg_crc(page):
+    crc = 0
+    for b in page:
+        crc ^= b << 24
+        for _ in range(8):
+            crc = ((crc << 1) ^ 0x04C11DB7) if crc & 0x80000000 else (crc << 1)
+            crc &= 0xFFFFFFFF
+    return crc
+
+
+def _ogg_pages(packets, serial=0x1234, max_seg=255, corrupt=(), per_packet=False):
+    """Pages of at most max_seg lacing values (a packet may span pages: continued flag), or with
+    per_packet one page per packet."""
+    segs = []  # (bytes, ends_packet)
+    for p in packets:
+        n = len(p)
+        i = 0
+        while n - i >= 255:
+            segs.append((p[i:i + 255], False))
+            i += 255
+        segs.append((p[i:], True))
+    out = b""
+    seq = 0
+    k = 0
+    continued = False
+    while k < len(segs):
+        if per_packet:
+            e = k
+            while not segs[e][1]:
+                e += 1
+            chunk = segs[k:e + 1]
+        else:
+            chunk = segs[k:k + max_seg]
+        k += len(chunk)
+        flags = (1 if continued else 0) | (2 if seq == 0 else 0) | (4 if k >= len(segs) else 0)
+        lacing = bytes(len(s) for s, _ in chunk)
+        hdr = b"OggS" + bytes([0, flags]) + struct.pack("<qIII", 0, serial, seq, 0) + bytes([len(chunk)]) + lacing
+        page = bytearray(hdr + b"".join(s for s, _ in chunk))
+        struct.pack_into("<I", page, 22, _ogg_crc(page))
+        if seq in corrupt:
+            page[-1] ^= 0x40
+        out += bytes(page)
+        continued = not chunk[-1][1]
+        seq += 1
+    return out
+
+
+def _flac_ogg_packets(chans_per_frame, bps, rate, nch):
+    frames = [fe.frame(ch, bps, k) for k, ch in enumerate(chans_per_frame)]
+    native = fe.stream(frames, rate, nch, bps)
+    streaminfo = native[4:4 + 38]
+    first = bytes([0x7F]) + b"FLAC" + bytes([1, 0]) + struct.pack(">H", 1) + b"fLaC" + streaminfo
+    vendor = b"test"
+    comment = bytes([0x84, 0, 0, 8 + len(vendor)]) + struct.pack("<I", len(vendor)) + vendor + struct.pack("<I", 0)
+    return [first, comment] + frames
+
+
+@pytest.mark.parametrize("max_seg", [255, 3])
+def test_ogg_flac(tmp_path, max_seg):
+    bps, nch = 16, 2
+    chans = [[fe_s for fe_s in _ints(1152, bps, 50 + k, nch)] for k in range(4)]
+    data = _ogg_pages(_flac_ogg_packets(chans, bps, 44100, nch), max_seg=max_seg)
+    x, sr = _decode(tmp_path, data, "t.ogg")
+    assert sr == 44100
+    assert x.tobytes() == fe.expected_mono(chans, bps).tobytes()
+
+
+def test_ogg_bad_crc_page_is_dropped(tmp_path):
+    bps = 16
+    chans = [_ints(1152, bps, 70 + k, 1) for k in range(4)]
+    # one packet per page: pages 0-1 headers, page 3 = audio frame 1
+    data = _ogg_pages(_flac_ogg_packets(chans, bps, 44100, 1), per_packet=True, corrupt=(3,))
+    x, _ = _decode(tmp_path, data, "t.ogg")
+    kept = [chans[0], chans[2], chans[3]]
+    assert x.tobytes() == fe.expected_mono(kept, bps).tobytes()
+
+
+def test_ogg_other_codecs(tmp_path):
+    vorbis = bytes([1]) + b"vorbis" + bytes(23)
+    opus = b"OpusHead" + bytes(11)
+    for head, name in [(vorbis, "Vorbis"), (opus, "Opus")]:
+        with pytest.raises(sdsp.AnalysisError) as e:
+            _decode(tmp_path, _ogg_pages([head, b"x"]), "t.ogg")
+        assert name in str(e.value)
+
+
+# ---- ADPCM in WAV ----
+IMA_STEP = [7, 8, 9, 10, 11, 12, 13, 14, 16, 17, 19, 21, 23, 25, 28, 31, 34, 37, 41, 45, 50, 55, 60, 66, 73, 80, 88,
+            97, 107, 118, 130, 143, 157, 173, 190, 209, 230, 253, 279, 307, 337, 371, 408, 449, 494, 544, 598, 658,
+            724, 796, 876, 963, 1060, 1166, 1282, 1411, 1552, 1707, 1878, 2066, 2272, 2499, 2749, 3024, 3327, 3660,
+            4026, 4428, 4871, 5358, 5894, 6484, 7132, 7845, 8630, 9493, 10442, 11487, 12635, 13899, 15289, 16818,
+            18500, 20350, 22385, 24623, 27086, 29794, 32767]
+IMA_INDEX = [-1, -1, -1, -1, 2, 4, 6, 8] * 2
+
+
+def _ima_step(pred, idx, n):
+    diff = ((2 * (n & 7) + 1) * IMA_STEP[idx]) >> 3
+    pred = pred - diff if n & 8 else pred + diff
+    return max(-32768, min(32767, pred)), max(0, min(88, idx + IMA_INDEX[n]))
+
+
+def _ima_encode_channel(x, nblk):
+    """Nibbles for len(x) samples after the block header's (greedy: the nibble whose decoded value
+    is nearest), and the decoded values a standard decoder produces."""
+    pred, idx = int(x[0]), 20
+    head = (pred, idx)
+    nibs, dec = [], []
+    for v in x[1:1 + nblk]:
+        best = min(range(16), key=lambda n: abs(_ima_step(pred, idx, n)[0] - int(v)))
+        pred, idx = _ima_step(pred, idx, best)
+        nibs.append(best)
+        dec.append(pred)
+    return head, nibs, [head[0]] + dec
+
+
+def _wav(tag, nch, rate, block_align, bits, data, ext=b""):
+    fmt = struct.pack("<HHIIHH", tag, nch, rate, rate * block_align, block_align, bits)
+    if ext:
+        fmt += struct.pack("<H", len(ext)) + ext
+    body = b"WAVE" + b"fmt " + struct.pack("<I", len(fmt)) + fmt + b"data" + struct.pack("<I", len(data)) + data
+    return b"RIFF" + struct.pack("<I", len(body)) + body
+
+
+@pytest.mark.parametrize("nch", [1, 2])
+def test_ima_adpcm(tmp_path, nch):
+    words = 31  # 4-byte words per channel per block: 248 + 1 samples per block
+    ba = 4 * nch + 4 * nch * words
+    per = 1 + 8 * words
+    chans = [np.round(np.asarray(c, np.float64) * 0.5).astype(np.int64) for c in _ints(per * 3, 16, 9, nch)]
+    for c in chans:
+        c[:2] = c[2]  # no full-scale step at the start: the tracking check below is about the signal
+    data = bytearray()
+    dec = [[] for _ in range(nch)]
+    for b in range(3):
+        heads, nibs = [], []
+        for c in range(nch):
+            h, n, d = _ima_encode_channel(chans[c][b * per:(b + 1) * per], per - 1)
+            heads.append(h)
+            nibs.append(n)
+            dec[c] += d
+        for (p, i) in heads:
+            data += struct.pack("<hBB", p, i, 0)
+        for w in range(words):
+            for c in range(nch):
+                q = nibs[c][8 * w:8 * w + 8]
+                data += bytes(q[2 * j] | (q[2 * j + 1] << 4) for j in range(4))
+    data += bytes(ba // 2)  # a final partial block: header + whole words only
+    part_words = (ba // 2 - 4 * nch) // (4 * nch)
+    for c in range(nch):
+        dec[c] += [0] + [_ima_part for _ima_part in _ima_zero_run(part_words * 8)]
+    x, sr = _decode(tmp_path, _wav(0x11, nch, 22050, ba, 4, bytes(data), ext=struct.pack("<H", per)), "t.wav")
+    want = _mono([np.asarray(d, np.int64).astype(F32) / F32(32768.0) for d in dec])
+    assert sr == 22050
+    assert x.tobytes() == want.tobytes()
+    # the stream tracks its signal (a check that the algorithm is the standard one)
+    ref = _mono([c[:3 * per].astype(F32) / F32(32768.0) for c in chans])
+    err = x[:3 * per] - ref
+    assert np.sqrt(np.mean(err ** 2)) < 0.1 * np.sqrt(np.mean(ref ** 2))
+
+
+def _ima_zero_run(n):
+    """Decoded values of n zero nibbles from predictor 0, step index 0."""
+    pred, idx, out = 0, 0, []
+    for _ in range(n):
+        pred, idx = _ima_step(pred, idx, 0)
+        out.append(pred)
+    return out
+
+
+MS_ADAPT = [230, 230, 230, 230, 307, 409, 512, 614, 768, 614, 512, 409, 307, 230, 230, 230]
+MS_COEF = [(256, 0), (512, -256), (0, 0), (192, 64), (240, 0), (460, -208), (392, -232)]
+
+
+def _c_div(a, b):
+    q = abs(a) // abs(b)
+    return q if (a >= 0) == (b > 0) else -q
+
+
+def _ms_step(s1, s2, delta, c1, c2, nib):
+    sn = nib - 16 if nib >= 8 else nib
+    pred = _c_div(s1 * c1 + s2 * c2, 256) + sn * delta
+    pred = max(-32768, min(32767, pred))
+    return pred, s1, max(16, (MS_ADAPT[nib] * delta) >> 8)
+
+
+@pytest.mark.parametrize("nch", [1, 2])
+def test_ms_adpcm(tmp_path, nch):
+    nbytes = 64 * nch  # nibble bytes per block
+    ba = 7 * nch + nbytes
+    per = 2 + 2 * nbytes // nch
+    chans = [np.round(np.asarray(c, np.float64) * 0.5).astype(np.int64) for c in _ints(per * 2, 16, 11, nch)]
+    for c in chans:
+        c[:2] = c[2]
+    data = bytearray()
+    dec = [[] for _ in range(nch)]
+    for b in range(2):
+        seg = [c[b * per:(b + 1) * per] for c in chans]
+        pidx = [3 if c == 0 else 1 for c in range(nch)]
+        st = []
+        for c in range(nch):
+            st.append([int(seg[c][1]), int(seg[c][0]), 64])  # s1, s2, delta
+        data += bytes(pidx)
+        data += b"".join(struct.pack("<h", s[2]) for s in st)
+        data += b"".join(struct.pack("<h", s[0]) for s in st)
+        data += b"".join(struct.pack("<h", s[1]) for s in st)
+        for c in range(nch):
+            dec[c] += [st[c][1], st[c][0]]
+        nibs = []
+        for k in range(2, per):
+            for c in range(nch):
+                c1, c2 = MS_COEF[pidx[c]]
+                s1, s2, d = st[c]
+                best = min(range(16), key=lambda n: abs(_ms_step(s1, s2, d, c1, c2, n)[0] - int(seg[c][k])))
+                st[c] = list(_ms_step(s1, s2, d, c1, c2, best))
+                dec[c].append(st[c][0])
+                nibs.append(best)
+        data += bytes((nibs[2 * j] << 4) | nibs[2 * j + 1] for j in range(len(nibs) // 2))
+    ext = struct.pack("<HH", per, len(MS_COEF)) + b"".join(struct.pack("<hh", a, b) for a, b in MS_COEF)
+    x, sr = _decode(tmp_path, _wav(2, nch, 44100, ba, 4, bytes(data), ext=ext), "t.wav")
+    want = _mono([np.asarray(d, np.int64).astype(F32) / F32(32768.0) for d in dec])
+    assert sr == 44100
+    assert x.tobytes() == want.tobytes()
+    ref = _mono([c[:2 * per].astype(F32) / F32(32768.0) for c in chans])
+    err = x - ref
+    assert np.sqrt(np.mean(err ** 2)) < 0.2 * np.sqrt(np.mean(ref ** 2))
+
+
+# ---- named codec errors ----
+@pytest.mark.parametrize("head,name", [
+    (b"ID3\x04\x00\x00\x00\x00\x00\x00" + b"\xff\xfb\x90\x00" + bytes(64), "MPEG audio"),
+    (b"\xff\xfb\x90\x00" + bytes(64), "MPEG audio"),
+    (b"\xff\xf1\x50\x80" + bytes(64), "AAC"),
+    (b"\x00\x00\x00\x20ftypM4A " + bytes(64), "MP4"),
+])
+def test_named_codec_errors(tmp_path, head, name):
+    with pytest.raises(sdsp.AnalysisError) as e:
+        _decode(tmp_path, head, "t.bin")
+    assert name in str(e.value) and e.value.kind == "DecodingError"
