@@ -9,9 +9,9 @@
 // This front-end reads RIFF/WAVE (PCM, IEEE float, A-law, mu-law, IMA and Microsoft ADPCM, and
 // WAVE_FORMAT_EXTENSIBLE with those sub-formats), which symphonia decodes into exactly those buffer
 // types (A-law / mu-law / ADPCM to S16), FLAC (host_flac.hip; symphonia's S32 buffers), and AIFF /
-// AIFF-C, CAF and Ogg FLAC (host_formats.hip).  A frame's mono value depends only on that frame,
-// so packet boundaries do not matter.  Other codecs (MP3, AAC, Vorbis, Opus, ALAC) are a decoding
-// error that names the codec.
+// AIFF-C, CAF and Ogg FLAC (host_formats.hip), and ALAC in CAF or MP4 (host_alac.hip).  A frame's
+// mono value depends only on that frame, so packet boundaries do not matter.  Other codecs (MP3,
+// AAC, Vorbis, Opus) are a decoding error that names the codec.
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -25,6 +25,7 @@ bool sdsp_decode_flac(const std::vector<uint8_t>& f, std::vector<float>* out, ui
 bool sdsp_decode_aiff(const std::vector<uint8_t>& f, std::vector<float>* out, uint32_t* sr, std::string* err);
 bool sdsp_decode_caf(const std::vector<uint8_t>& f, std::vector<float>* out, uint32_t* sr, std::string* err);
 bool sdsp_decode_ogg(const std::vector<uint8_t>& f, std::vector<float>* out, uint32_t* sr, std::string* err);
+bool sdsp_decode_mp4(const std::vector<uint8_t>& f, std::vector<float>* out, uint32_t* sr, std::string* err);
 
 namespace {
 
@@ -339,7 +340,7 @@ extern "C" int32_t sdsp_decode_audio_file(const char* path, float** samples, uin
     } else if (magic(0, "OggS")) {
         ok = sdsp_decode_ogg(buf, &mono, &sr, &why);
     } else if (magic(4, "ftyp")) {
-        ok = false, why = "unsupported codec: ISO MP4 audio (AAC / ALAC)";
+        ok = sdsp_decode_mp4(buf, &mono, &sr, &why);
     } else if (id3 || (buf.size() >= 2 && buf[0] == 0xFF && (buf[1] & 0xE0) == 0xE0)) {
         ok = false, why = (buf.size() >= 2 && !id3 && (buf[1] & 0xF6) == 0xF0) ? "unsupported codec: AAC (ADTS)"
                                                                              : "unsupported codec: MPEG audio (MP1/MP2/MP3)";

@@ -11,11 +11,11 @@
 //                   signed -> S8, unsupported), 'sowt' little-endian PCM, 'fl32' / 'fl64' floats,
 //                   G.711 'alaw' / 'ulaw' (-> S16); the sample rate from the 80-bit extended float;
 //   CAF             'lpcm' (integer: signed, big- or little-endian by the format flags; floats),
-//                   'alaw' / 'ulaw';
+//                   'alaw' / 'ulaw', 'alac' (host_alac.hip);
 //   Ogg             the FLAC mapping (first packet 0x7F "FLAC" + STREAMINFO): the packets are
 //                   reassembled into a native FLAC stream for host_flac.hip; pages whose CRC
 //                   fails are dropped.  Vorbis / Opus streams are a decoding error.
-// MP3, AAC (MP4 / ADTS), ALAC, Vorbis and Opus are decoding errors that name the codec.  Parity
+// MP3, AAC (MP4 / ADTS), Vorbis and Opus are decoding errors that name the codec.  Parity
 // with symphonia itself is unpinned (this image has no symphonia); tests/test_formats_decode.py
 // writes each container from its specification and checks the reference's conversion bit for bit.
 #include <cmath>
@@ -24,6 +24,7 @@
 #include <vector>
 
 bool sdsp_decode_flac(const std::vector<uint8_t>& f, std::vector<float>* out, uint32_t* sr, std::string* err);
+bool sdsp_decode_caf_alac(const std::vector<uint8_t>& f, std::vector<float>* out, uint32_t* sr, std::string* err);
 
 namespace {
 
@@ -253,7 +254,7 @@ bool sdsp_decode_caf(const std::vector<uint8_t>& f, std::vector<float>* out, uin
         pcm.kind = fs == "alaw" ? Pcm::ALAW : Pcm::ULAW;
         pcm.width = 1;
     } else if (fs == "alac") {
-        return fail(err, "unsupported codec: ALAC");
+        return sdsp_decode_caf_alac(f, out, sr, err);
     } else {
         return fail(err, "unsupported CAF format '" + fs + "'");
     }
