@@ -461,7 +461,7 @@ bool sdsp_decode_mp4(const std::vector<uint8_t>& f, std::vector<float>* out, uin
         if (std::memcmp(t, "moov", 4) == 0) moov = b, moov_n = n;
         return true;
     });
-    if (!moov) return fail(err, "missing moov box");
+    if (!moov) return fail(err, "malformed ISO MP4 file: missing moov box");
     std::string codec;
     bool found = false;
     AlacConfig c;
@@ -526,7 +526,7 @@ bool sdsp_decode_mp4(const std::vector<uint8_t>& f, std::vector<float>* out, uin
         });
         return true;
     });
-    if (!found) return fail(err, "no audio track");
+    if (!found) return fail(err, "ISO MP4 file without an audio track");
     if (codec == "bad") return fail(err, why);
     if (codec == "mp4a") return fail(err, "unsupported codec: AAC (ISO MP4)");
     if (codec != "alac") return fail(err, "unsupported codec: ISO MP4 '" + codec + "'");
