@@ -13,9 +13,10 @@
 //   CAF             'lpcm' (integer: signed, big- or little-endian by the format flags; floats),
 //                   'alaw' / 'ulaw', 'alac' (host_alac.hip);
 //   Ogg             the FLAC mapping (first packet 0x7F "FLAC" + STREAMINFO): the packets are
-//                   reassembled into a native FLAC stream for host_flac.hip; pages whose CRC
-//                   fails are dropped.  Vorbis / Opus streams are a decoding error.
-// MP3, AAC (MP4 / ADTS), Vorbis and Opus are decoding errors that name the codec.  Parity
+//                   reassembled into a native FLAC stream for host_flac.hip; Vorbis
+//                   (host_vorbis.hip); pages whose CRC fails are dropped.  Opus is a decoding
+//                   error.
+// MP3, AAC (MP4 / ADTS) and Opus are decoding errors that name the codec.  Parity
 // with symphonia itself is unpinned (this image has no symphonia); tests/test_formats_decode.py
 // writes each container from its specification and checks the reference's conversion bit for bit.
 #include <cmath>
@@ -25,6 +26,8 @@
 
 bool sdsp_decode_flac(const std::vector<uint8_t>& f, std::vector<float>* out, uint32_t* sr, std::string* err);
 bool sdsp_decode_caf_alac(const std::vector<uint8_t>& f, std::vector<float>* out, uint32_t* sr, std::string* err);
+bool sdsp_decode_vorbis(const std::vector<std::vector<uint8_t>>& packets, int64_t last_granule, std::vector<float>* out,
+                        uint32_t* sr, std::string* err);
 
 namespace {
 
@@ -291,6 +294,7 @@ bool sdsp_decode_ogg(const std::vector<uint8_t>& f, std::vector<float>* out, uin
     std::vector<uint8_t> cur;
     bool have_serial = false;
     uint32_t serial = 0;
+    int64_t last_granule = -1;  // of the last page of the stream that completes a packet
     size_t pos = 0;
     while (pos + 27 <= f.size()) {
         const uint8_t* p = f.data() + pos;
@@ -315,6 +319,8 @@ bool sdsp_decode_ogg(const std::vector<uint8_t>& f, std::vector<float>* out, uin
             have_serial = true;
         }
         if (s == serial) {
+            const int64_t g = (int64_t)le64(p + 6);
+            if (g != -1) last_granule = g;
             if (!(p[5] & 1)) cur.clear();  // not a continuation: no packet carries over
             const uint8_t* d = p + 27 + nseg;
             for (int i = 0; i < nseg; i++) {
@@ -331,7 +337,7 @@ bool sdsp_decode_ogg(const std::vector<uint8_t>& f, std::vector<float>* out, uin
     if (packets.empty()) return fail(err, "no Ogg packets");
     const std::vector<uint8_t>& h = packets[0];
     if (h.size() >= 7 && h[0] == 0x01 && std::memcmp(h.data() + 1, "vorbis", 6) == 0)
-        return fail(err, "unsupported codec: Vorbis");
+        return sdsp_decode_vorbis(packets, last_granule, out, sr, err);
     if (h.size() >= 8 && std::memcmp(h.data(), "OpusHead", 8) == 0) return fail(err, "unsupported codec: Opus");
     if (!(h.size() >= 13 + 38 && h[0] == 0x7F && std::memcmp(h.data() + 1, "FLAC", 4) == 0 &&
           std::memcmp(h.data() + 9, "fLaC", 4) == 0))
