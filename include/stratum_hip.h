@@ -330,15 +330,17 @@ int32_t sdsp_compute_confidence(const sdsp_result* result, sdsp_confidence* out)
 int32_t sdsp_key_name(int32_t key_mode, uint32_t key_tonic, char* buf, uint64_t buflen);
 
 /*
- * Audio decode front-end (examples/analyze_file.rs:25-180, analyze_batch.rs:30-177): RIFF/WAVE
- * files -- PCM u8 / s16 / s24 / s32, IEEE float f32 / f64, G.711, WAVE_FORMAT_EXTENSIBLE with
- * those sub-formats -- and FLAC streams (8-32 bits, 1-8 channels; symphonia's S32 buffers,
- * sample << (32 - bps)), decoded to mono f32 exactly as the reference's symphonia path converts
- * them (s16 / 32768, s24 / 8388608, s32 / 2147483648, (u8 - 128) / 128, f64 -> f32; channels
- * summed in order and divided by the channel count).  A FLAC frame that fails its CRC is skipped,
- * as the examples skip a packet that fails to decode.  *samples is malloc'ed (free with
- * sdsp_free_samples).  Returns 0, or SDSP_ERR_DECODING with the reason in err for anything else
- * (other containers and codecs -- MP3, AAC, Ogg, ALAC -- are outside this front-end).
+ * Audio decode front-end (examples/analyze_file.rs:25-180, analyze_batch.rs:30-177), by magic
+ * number: RIFF/WAVE (PCM u8 / s16 / s24 / s32, IEEE float f32 / f64, G.711, IMA and Microsoft
+ * ADPCM, WAVE_FORMAT_EXTENSIBLE with those sub-formats), AIFF / AIFF-C, CAF (lpcm, G.711, ALAC),
+ * FLAC (native or in Ogg; 8-32 bits, 1-8 channels; symphonia's S32 buffers, sample << (32 -
+ * bps)), ALAC in ISO MP4 / M4A, and Ogg Vorbis -- decoded to mono f32 as the reference's
+ * symphonia path converts its buffers (s16 / 32768, s24 / 8388608, s32 / 2147483648, (u8 - 128) /
+ * 128, f64 -> f32, f32 as is; channels summed in order and divided by the channel count).  A
+ * packet that fails to decode (a FLAC frame failing its CRC, a damaged ALAC packet, an Ogg page
+ * failing its CRC) is skipped, as the examples skip such a packet.  *samples is malloc'ed (free
+ * with sdsp_free_samples).  Returns 0, or SDSP_ERR_DECODING with the reason in err (MP3 / MP2 /
+ * MP1, AAC and Opus are named as unsupported codecs).
  */
 int32_t sdsp_decode_audio_file(const char* path, float** samples, uint64_t* n_samples, uint32_t* sample_rate,
                                char* err, uint64_t errlen);
