@@ -334,7 +334,8 @@ int32_t sdsp_key_name(int32_t key_mode, uint32_t key_tonic, char* buf, uint64_t 
  * number: RIFF/WAVE (PCM u8 / s16 / s24 / s32, IEEE float f32 / f64, G.711, IMA and Microsoft
  * ADPCM, WAVE_FORMAT_EXTENSIBLE with those sub-formats), AIFF / AIFF-C, CAF (lpcm, G.711, ALAC),
  * FLAC (native or in Ogg; 8-32 bits, 1-8 channels; symphonia's S32 buffers, sample << (32 -
- * bps)), ALAC in ISO MP4 / M4A, and Ogg Vorbis -- decoded to mono f32 as the reference's
+ * bps)), ALAC in ISO MP4 / M4A, Ogg Vorbis, and Matroska / WebM carrying PCM, FLAC, ALAC or
+ * Vorbis -- decoded to mono f32 as the reference's
  * symphonia path converts its buffers (s16 / 32768, s24 / 8388608, s32 / 2147483648, (u8 - 128) /
  * 128, f64 -> f32, f32 as is; channels summed in order and divided by the channel count).  A
  * packet that fails to decode (a FLAC frame failing its CRC, a damaged ALAC packet, an Ogg page

@@ -549,3 +549,17 @@ bool sdsp_decode_mp4(const std::vector<uint8_t>& f, std::vector<float>* out, uin
     }
     return decode_packets(c, f.data(), f.size(), pk, out, sr, err);
 }
+
+// ALAC from a magic cookie and a list of packets (the Matroska A_ALAC track, host_mkv.hip)
+bool sdsp_decode_alac_packets(const std::vector<uint8_t>& cookie, const std::vector<std::vector<uint8_t>>& packets,
+                              std::vector<float>* out, uint32_t* sr, std::string* err) {
+    AlacConfig c;
+    if (!parse_cookie(cookie.data(), cookie.size(), &c, err)) return false;
+    std::vector<uint8_t> flat;
+    std::vector<std::pair<uint64_t, uint64_t>> pk;
+    for (const auto& p : packets) {
+        pk.push_back({flat.size(), p.size()});
+        flat.insert(flat.end(), p.begin(), p.end());
+    }
+    return decode_packets(c, flat.data(), flat.size(), pk, out, sr, err);
+}

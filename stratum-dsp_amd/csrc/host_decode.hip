@@ -9,7 +9,8 @@
 // This front-end reads RIFF/WAVE (PCM, IEEE float, A-law, mu-law, IMA and Microsoft ADPCM, and
 // WAVE_FORMAT_EXTENSIBLE with those sub-formats), which symphonia decodes into exactly those buffer
 // types (A-law / mu-law / ADPCM to S16), FLAC (host_flac.hip; symphonia's S32 buffers), and AIFF /
-// AIFF-C, CAF and Ogg FLAC (host_formats.hip), and ALAC in CAF or MP4 (host_alac.hip).  A frame's
+// AIFF-C, CAF and Ogg FLAC (host_formats.hip), ALAC in CAF or MP4 (host_alac.hip), Ogg Vorbis
+// (host_vorbis.hip) and Matroska / WebM with those codecs (host_mkv.hip).  A frame's
 // mono value depends only on that frame, so packet boundaries do not matter.  Other codecs (MP3,
 // AAC, Vorbis, Opus) are a decoding error that names the codec.
 #include <algorithm>
@@ -26,6 +27,7 @@ bool sdsp_decode_aiff(const std::vector<uint8_t>& f, std::vector<float>* out, ui
 bool sdsp_decode_caf(const std::vector<uint8_t>& f, std::vector<float>* out, uint32_t* sr, std::string* err);
 bool sdsp_decode_ogg(const std::vector<uint8_t>& f, std::vector<float>* out, uint32_t* sr, std::string* err);
 bool sdsp_decode_mp4(const std::vector<uint8_t>& f, std::vector<float>* out, uint32_t* sr, std::string* err);
+bool sdsp_decode_mkv(const std::vector<uint8_t>& f, std::vector<float>* out, uint32_t* sr, std::string* err);
 
 namespace {
 
@@ -339,6 +341,8 @@ extern "C" int32_t sdsp_decode_audio_file(const char* path, float** samples, uin
         ok = sdsp_decode_caf(buf, &mono, &sr, &why);
     } else if (magic(0, "OggS")) {
         ok = sdsp_decode_ogg(buf, &mono, &sr, &why);
+    } else if (buf.size() >= 4 && buf[0] == 0x1A && buf[1] == 0x45 && buf[2] == 0xDF && buf[3] == 0xA3) {
+        ok = sdsp_decode_mkv(buf, &mono, &sr, &why);
     } else if (magic(4, "ftyp")) {
         ok = sdsp_decode_mp4(buf, &mono, &sr, &why);
     } else if (id3 || (buf.size() >= 2 && buf[0] == 0xFF && (buf[1] & 0xE0) == 0xE0)) {
