@@ -255,6 +255,7 @@ bool decode_frame(const uint8_t* d, size_t len, const AlacConfig& c, std::vector
             if (ech == 2) {
                 mix_bits = (int)b.read(8);
                 mix_res = (int8_t)b.read(8);
+                if (mix_bits > 31) return fail(err, "malformed ALAC element");
             }
             int mode[2], den[2], pbf[2], na[2];
             int16_t coefs[2][32];
