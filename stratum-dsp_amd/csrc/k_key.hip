@@ -184,172 +184,6 @@ __global__ __launch_bounds__(MASK_T) void k_mask_r(float* __restrict__ mags, int
     }
 }
 
-// k_mask_re: k_mask_r that also folds HPCP's frame energy, so HPCP reads only its peak bins.
-// HPCP's energy of frame t is sum_b m[t][b]^2 folded in bin order from 0 (extractor.rs:1097-1150,
-// the energy of the frame's masked magnitudes).  Workgroup g of a track holds bins 64 g .. 64 g
-// + 63, so that fold runs across the track's workgroups: every 32 frames, group g stages its
-// m^2 values in LDS (rows t & 31; a block of the unrolled frame loop, 26 frames, keeps them in
-// registers and stores them around its fold, at most one 32-frame boundary per block), takes
-// group g-1's partial sums of those 32 frames, continues the fold over its 64 columns in order
-// (lane l = frame t0 + l), and hands the result to group g+1; the last group writes the energy.
-// Bins past B fold +0.0, which leaves every sum unchanged.  The hand-off goes through uncached
-// device memory: per frame a 64-bit word {partial sum, tag}, the tag naming the launch (epoch)
-// and the producing group, in two slots by group parity (group g+2 overwrites group g's slot only
-// after group g+1 has taken it).  One atomic 64-bit load checks and fetches a word, so the words
-// of a block's fold are loaded at the block's start and their latency hides under its mask
-// work; it needs no cache maintenance (a hop costs ~1.2 us on MI355X, tools/micro/uc_chain.hip).  A group only waits
-// on the group before it, whose block index is lower: in-order dispatch keeps the lowest
-// unfinished group resident, so the chain always progresses, and every wait is bounded (a
-// timeout sets err, the host raises an error).  Only bins [wlo, whi] (HPCP's candidates and
-// their neighbours) are written back.
-constexpr int MFOLD_ROWS = 32, MFOLD_LD = 65;  // 32-frame folds; LDS row stride 65: conflict-free columns
-
-template <int M, int PW>
-__global__ __launch_bounds__(MASK_T) __attribute__((amdgpu_waves_per_eu(4))) void k_mask_re(
-    float* __restrict__ mags, int stride, int B, const uint64_t* __restrict__ frame_pfx, const int* __restrict__ tracks,
-    int blocks_per_track, float power, int wlo, int whi, uint64_t total, float* __restrict__ energy, uint64_t* part,
-    uint32_t epoch, unsigned* __restrict__ err) {
-    constexpr int R = 2 * M + 2, RX = M + 1;
-    static_assert(R <= MFOLD_ROWS, "one fold per unrolled block");
-    __shared__ float et[MFOLD_ROWS * MFOLD_LD];
-    const int it = blockIdx.x / blocks_per_track;
-    const int grp = blockIdx.x % blocks_per_track;
-    const int trk = tracks[it];
-    const int lane = threadIdx.x;
-    const int b = grp * MASK_T + lane;
-    const bool active = b < B;
-    const int64_t F = (int64_t)(frame_pfx[trk + 1] - frame_pfx[trk]);
-    if (F <= 0) return;  // the whole workgroup
-    const uint64_t g0 = frame_pfx[trk];
-    // lanes past B read bin 0's column (unconditional loads keep the waits per load, not per
-    // block) and fold +0.0
-    float* col = mags + g0 * (uint64_t)stride + (active ? b : 0);
-    const bool wr = active && b >= wlo && b <= whi;
-    const float p = sd_maxf(power, 1.0f);
-    const float inv_w = 1.0f / (float)(2 * M + 1);
-    float P[R], X[RX];
-#pragma unroll
-    for (int j = 0; j < R; j++) P[j] = 0.0f;
-#pragma unroll
-    for (int j = 0; j < RX; j++) X[j] = 0.0f;
-    float prev = 0.0f;
-    float sq[R];  // m^2 of this block's frames, staged into LDS around the block's fold
-    auto emit = [&](float a, int64_t den, float xr, int64_t t, int u) {
-        const float m = mask_elem<M, PW>(a, den, xr, p, inv_w);
-        if (wr) __builtin_nontemporal_store(m, &col[t * stride]);
-        sq[u] = active ? m * m : 0.0f;
-    };
-    // partial sums travel as 64-bit words {sum, tag}: the tag (epoch, producer group + 1) says the
-    // word is this launch's and complete, so one atomic load both checks and fetches it; slots by
-    // the producer's parity
-    const bool last = grp == blocks_per_track - 1;
-    const uint64_t in_off = (uint64_t)((grp - 1) & 1) * total + g0, out_off = (uint64_t)(grp & 1) * total + g0;
-    const uint32_t want = (epoch << 8) | (uint32_t)grp, mine_tag = (epoch << 8) | (uint32_t)(grp + 1);
-    auto load_in = [&](int64_t t0) -> uint64_t {
-        return __hip_atomic_load(part + in_off + (uint64_t)(t0 + lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    };
-    // the fold of frames t0 .. t0+n-1 (t0 a multiple of 32), rows t & 31 of et; w = the input
-    // word loaded earlier (its latency covered by the block's mask work)
-    auto fold = [&](int64_t t0, int n, uint64_t w) {
-        __syncthreads();  // one wave: orders its LDS row writes before the column reads
-        const bool mine = lane < n;
-        float e = 0.0f;
-        if (grp > 0) {
-            uint32_t spins = 0;
-#ifdef SDSP_FOLD_NOWAIT  // experiment: the hand-off's cost without its waits (wrong sums)
-            while (false) {
-#else
-            while (__builtin_amdgcn_ballot_w64(mine && (uint32_t)(w >> 32) != want) != 0) {
-#endif
-                if (++spins > (1u << 24)) {
-                    if (lane == 0) atomicOr(err, 1u);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
-                if (mine) w = load_in(t0);
-            }
-            e = __uint_as_float((uint32_t)w);
-#ifdef SDSP_FOLD_LAG  // experiment: trail the predecessor by more than a block after the first hand-off
-            if (t0 == 0)
-                for (int z = 0; z < SDSP_FOLD_LAG; z++) __builtin_amdgcn_s_sleep(127);
-#endif
-        }
-        const float* row = et + (lane & (MFOLD_ROWS - 1)) * MFOLD_LD;
-#pragma unroll 16
-        for (int j = 0; j < MASK_T; j++) e = e + row[j];
-        if (mine) {
-            if (last)
-                energy[g0 + (uint64_t)(t0 + lane)] = e;
-            else
-                __hip_atomic_store(part + out_off + (uint64_t)(t0 + lane),
-                                   ((uint64_t)mine_tag << 32) | (uint64_t)__float_as_uint(e), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        }
-        __syncthreads();  // the folded rows may be refilled
-    };
-    int64_t folded = 0;  // frames folded so far (a multiple of 32)
-    for (int64_t base = 0; base < F + M; base += R) {
-        const int64_t t_lo = base - M;                        // this block's frames: t_lo + u
-        const int64_t t_hi = t_lo + R < F ? t_lo + R : F;  // the valid ones end before t_hi
-        const int64_t split = folded + MFOLD_ROWS;
-        // this block completes a fold: fetch its input words now
-        uint64_t w = 0;
-        if (grp > 0 && split <= t_hi && lane < MFOLD_ROWS) w = load_in(folded);
-        float xv[R];
-        if (base >= 2 * M && base + R <= F) {
-#pragma unroll
-            for (int u = 0; u < R; u++) xv[u] = __builtin_nontemporal_load(&col[(base + u) * stride]);
-#pragma unroll
-            for (int u = 0; u < R; u++) {
-                prev = prev + xv[u];
-                P[(u + 1) % R] = prev;
-                X[u % RX] = xv[u];
-                emit(P[(u + 1) % R] - P[(u + R - 2 * M) % R], 2 * M + 1, X[(u + 1) % RX], t_lo + u, u);
-            }
-        } else {
-#pragma unroll
-            for (int u = 0; u < R; u++)
-                xv[u] = base + u < F ? __builtin_nontemporal_load(&col[(base + u) * stride]) : 0.0f;
-#pragma unroll
-            for (int u = 0; u < R; u++) {
-                const int64_t tin = base + u;
-                prev = prev + xv[u];
-                P[(u + 1) % R] = prev;
-                X[u % RX] = xv[u];
-                const int64_t t = tin - M;
-                sq[u] = 0.0f;
-                if (t >= 0 && t < F) {
-                    const int64_t st = t >= M ? t - M : 0;
-                    const int64_t en = t + M + 1 < F ? t + M + 1 : F;
-                    emit(P[(u + 1) % R] - P[(u + R - 2 * M) % R], en - st, X[(u + 1) % RX], t, u);
-                }
-            }
-        }
-        // rows of the frames before the 32-frame boundary (if this block reaches it), the fold,
-        // then the rest: at most one boundary per block (R <= 32)
-#pragma unroll
-        for (int u = 0; u < R; u++) {
-            const int64_t t = t_lo + u;
-            if (t >= 0 && t < t_hi && t < split) et[(int)(t & (MFOLD_ROWS - 1)) * MFOLD_LD + lane] = sq[u];
-        }
-        if (split <= t_hi) {
-            fold(folded, MFOLD_ROWS, w);
-            folded = split;
-#pragma unroll
-            for (int u = 0; u < R; u++) {
-                const int64_t t = t_lo + u;
-                if (t >= split && t < t_hi) et[(int)(t & (MFOLD_ROWS - 1)) * MFOLD_LD + lane] = sq[u];
-            }
-        }
-    }
-    if (folded < F) {  // the last partial fold
-        const int n = (int)(F - folded);
-        uint64_t w = 0;
-        if (grp > 0 && lane < n) w = load_in(folded);
-        fold(folded, n, w);
-    }
-}
-
 // ----------------------------------------------------------------------------------------
 constexpr int HP_CW = 16;  // bins per staged chunk (LDS row stride 17: conflict-free)
 
@@ -433,7 +267,7 @@ struct HpcpFrame {
             if (norm > EPS) v /= norm;
             chroma[g * 12 + q] = v;
         }
-        if (!P.e_given) energy[g] = e;
+        energy[g] = e;
     }
 };
 
@@ -478,19 +312,15 @@ __global__ __launch_bounds__(HP_FRAMES) SDSP_HPCP_ATTR void k_hpcp(const float* 
         for (int u = 0; u < NLD; u++)
             nx[u] = (sub + u * RSTEP < rows && col_ok) ? rowp[(uint64_t)u * rstride + c0] : 0.0f;
     };
-    // bins c_lo .. c_hi, from the chunk holding c_lo (bins below c_lo feed only candidates below
-    // pk_lo, which are never taken)
-    const int cend = (P.c_hi >= 0 && P.c_hi < P.B ? P.c_hi : P.B - 1) + 1;
-    const int cbeg = (P.c_lo > 0 ? P.c_lo : 0) / HP_CW * HP_CW;
-    load_chunk(cbeg);
-    for (int c0 = cbeg; c0 < cend; c0 += HP_CW) {
+    load_chunk(0);
+    for (int c0 = 0; c0 < P.B; c0 += HP_CW) {
         __syncthreads();
 #pragma unroll
         for (int u = 0; u < NLD; u++) tile[sub + u * RSTEP][jj] = nx[u];
         __syncthreads();
-        if (c0 + HP_CW < cend) load_chunk(c0 + HP_CW);
+        if (c0 + HP_CW < P.B) load_chunk(c0 + HP_CW);
         if (!valid) continue;
-        hf.walk(tile[i], c0, cend - c0 < HP_CW ? cend - c0 : HP_CW, P);
+        hf.walk(tile[i], c0, P.B - c0 < HP_CW ? P.B - c0 : HP_CW, P);
     }
     // pitch-class accumulators reuse the staging tile (every read of it is done)
     __syncthreads();
@@ -1085,15 +915,6 @@ void launch_mask(float* mags, int stride, int B, const uint64_t* frame_pfx, cons
     else
         hipLaunchKernelGGL(k_mask<0>, dim3(n_items * bpt), dim3(MASK_T), lds, st, mags, stride, B, frame_pfx, tracks,
                            bpt, margin, power, 0);
-}
-void launch_mask_fold(float* mags, int stride, int B, const uint64_t* frame_pfx, const int* tracks, int n_items,
-                      float power, int wlo, int whi, uint64_t total, float* energy, uint64_t* part, uint32_t epoch,
-                      unsigned* err, hipStream_t st) {
-    if (n_items == 0) return;
-    const int bpt = (B + MASK_T - 1) / MASK_T;
-    if (bpt > 255) throw std::runtime_error("k_mask_re: more than 255 groups per track");  // 8-bit tag field
-    hipLaunchKernelGGL((k_mask_re<12, 2>), dim3(n_items * bpt), dim3(MASK_T), 0, st, mags, stride, B, frame_pfx, tracks,
-                       bpt, power, wlo, whi, total, energy, part, epoch, err);
 }
 void launch_hpcp(const float* mags, const uint64_t* frame_pfx, const uint64_t* tile_pfx, const int* tracks,
                  int n_items, uint64_t n_tiles, const HpcpParams& P, const HarmEntry* harm, float* chroma,

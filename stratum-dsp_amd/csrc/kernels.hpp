@@ -138,9 +138,6 @@ struct HpcpParams {
     int K;
     int hmax;
     float p;
-    // bins walked: [c_lo, c_hi] (0, B-1 for all); e_given: the frame energies are already in
-    // `energy` (k_mask_re folded them), so the walk covers only the candidates' bins
-    int c_lo = 0, c_hi = -1, e_given = 0;
 };
 struct KeyParams {
     int weighting;
@@ -314,13 +311,6 @@ void launch_hpss_rows(const float* p, const uint64_t* row0, const uint64_t* fpfx
 void launch_beat_sync(const int* tracks, int n_items, const uint64_t* frame_pfx, const float* fchroma,
                       const float* fenergy, const float* beats, const uint64_t* beat_off, const uint64_t* row_pfx,
                       float fd, float* chroma, float* energy, hipStream_t st);
-// k_mask_re (margin 12, power 2): the mask of k_mask_r, written back only on bins [wlo, whi], with
-// HPCP's frame energies folded into `energy`; part (2 x total 64-bit words) is uncached device
-// memory, zeroed when allocated; epoch (24 bits) differs from every earlier launch's on it; err
-// != 0 after a hand-off timeout
-void launch_mask_fold(float* mags, int stride, int B, const uint64_t* frame_pfx, const int* tracks, int n_items,
-                      float power, int wlo, int whi, uint64_t total, float* energy, uint64_t* part, uint32_t epoch,
-                      unsigned* err, hipStream_t st);
 void launch_hpcp(const float* mags, const uint64_t* frame_pfx, const uint64_t* tile_pfx, const int* tracks,
                  int n_items, uint64_t n_tiles, const HpcpParams& P, const HarmEntry* harm, float* chroma,
                  float* energy, hipStream_t st);

@@ -41,11 +41,6 @@ namespace {
 // Spectrogram row strides (floats; multiples of 4 for 16-B rows).  The key spectrogram's rows
 // are 16 KiB + 256 B apart: at 16 KiB + 16 B the mask's column streams (one 256-B row segment
 // per wave per frame) run 1.5x slower (profiles/README.md, stride sweep of round 2).
-// the default key chain folds HPCP's frame energies inside the mask kernel (k_mask_re); 0 builds
-// the unfused chain (k_mask_r, then the full HPCP walk) for A/B runs (tools/build_exp.sh)
-#ifndef SDSP_KEY_FOLD
-#define SDSP_KEY_FOLD 1
-#endif
 constexpr int STRIDE2 = 1028;  // 1025 bins
 constexpr int STRIDE8 = 4160;  // 4097 bins
 // row stride of the tempo path's spectrogram for AnalysisConfig::frame_size (nb = fs/2 + 1 bins)
@@ -482,14 +477,6 @@ struct Ctx {
     template <class T>
     T* dev(const std::string& name, size_t n) {
         DevBuf& b = d.buf(name);
-        b.ensure(std::max<size_t>(n * sizeof(T), 16));
-        return b.as<T>();
-    }
-    // uncached device memory (cross-workgroup hand-offs inside one kernel, k_mask_re)
-    template <class T>
-    T* dev_uc(const std::string& name, size_t n) {
-        DevBuf& b = d.buf(name);
-        b.uncached = true;
         b.ensure(std::max<size_t>(n * sizeof(T), 16));
         return b.as<T>();
     }
@@ -1523,9 +1510,6 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     const int NK = (int)K.size();
     std::vector<KeyOut> kout;
     KeyOut* d_kout = nullptr;
-    float* d_energy_f = nullptr;
-    uint64_t* d_fold_part = nullptr;
-    unsigned* d_fold_err = nullptr;
     KeyDbg* d_kdbg = nullptr;
     std::unique_ptr<Timers> ktp(new Timers());
     Timers& kt = *ktp;
@@ -1572,18 +1556,6 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         const bool use_log = cfg_.enable_key_log_frequency;  // :1062-1095
         const bool tuned = cfg_.enable_key_tuning_compensation && !use_log;
         const bool whiten = cfg_.enable_key_hpcp_whitening && cfg_.key_hpcp_whitening_smooth_bins >= 3;
-        // HPCP's peak band (extractor.rs:529-680: 100 Hz .. min(5 kHz, Nyquist))
-        int pk_lo = 1, pk_hi = 0;
-        band_bins(B8, fres8, sd_maxf(100.0f, 20.0f), sd_minf(5000.0f, (float)sr_ / 2.0f), &pk_lo, &pk_hi);
-        // the fused mask + energy fold serves only the default chain: the margin-12 / power-2 mask
-        // read by nothing but HPCP (no key HPSS, log-frequency chroma, tuning, whitening, bass
-        // blend or beat-synchronous chroma)
-        const bool beat_sync_key = cfg_.enable_key_beat_synchronous && !use_log;
-        const bool key_fold = SDSP_KEY_FOLD && !cfg_.enable_key_hpss_harmonic && cfg_.enable_key_harmonic_mask &&
-                              cfg_.key_spectrogram_smooth_margin == 12 && sd_maxf(cfg_.key_harmonic_mask_power, 1.0f) == 2.0f &&
-                              !use_log && !tuned && cfg_.enable_key_hpcp && !whiten && !cfg_.enable_key_hpcp_bass_blend &&
-                              !beat_sync_key && pk_lo <= pk_hi;
-        const int fold_lo = std::max(pk_lo - 1, 0), fold_hi = std::min(pk_hi + 1, B8 - 1);
         if (cfg_.enable_key_hpss_harmonic) {
             const KeyHpssParams kh = key_hpss_params(cfg_, sr_, B8, fres8, ks_);
             if (kh.nb > 0) {  // an empty band returns the spectrogram unchanged (extractor.rs:1408-1410)
@@ -1605,24 +1577,6 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
                 SDSP_HIP_CHECK(hipStreamWaitEvent(st2, kt.ev[9], 0));
                 launch_key_hpss(mags8, d_kpfx, d_mt, mt.back(), d_at, at.back(), d_moff, d_kid, NK, kh, d_kmask, st2);
             }
-        } else if (key_fold) {
-            // the default key path: the mask folds HPCP's frame energies (k_mask_re) and writes back
-            // only the bins HPCP's peak walk reads
-            // the hand-off words: uncached, zeroed when (re)allocated; each launch tags its own
-            DevBuf& pb = d_.buf("E.fold_part");
-            const size_t before = pb.bytes;
-            d_fold_part = c_.dev_uc<uint64_t>("E.fold_part", 2 * total8);
-            if (pb.bytes != before) SDSP_HIP_CHECK(hipMemsetAsync(d_fold_part, 0, pb.bytes, st2));
-            d_fold_err = c_.dev<unsigned>("E.fold_err", 1);
-            d_energy_f = c_.dev<float>("E.energy", total8);
-            SDSP_HIP_CHECK(hipMemsetAsync(d_fold_err, 0, sizeof(unsigned), st2));
-            d_.fold_epoch = (d_.fold_epoch + 1) & 0xFFFFFF;
-            if (d_.fold_epoch == 0) {  // wrapped: clear the old tags
-                d_.fold_epoch = 1;
-                SDSP_HIP_CHECK(hipMemsetAsync(d_fold_part, 0, pb.bytes, st2));
-            }
-            launch_mask_fold(mags8, ks_, B8, d_kpfx, d_kid, NK, cfg_.key_harmonic_mask_power, fold_lo, fold_hi, total8,
-                             d_energy_f, d_fold_part, d_.fold_epoch, d_fold_err, st2);
         } else if (cfg_.enable_key_harmonic_mask)
             launch_mask(mags8, ks_, B8, d_kpfx, d_kid, NK, (int)cfg_.key_spectrogram_smooth_margin,
                         cfg_.key_harmonic_mask_power, st2);
@@ -1648,13 +1602,9 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
             HpcpParams hp{};
             hp.B = B8;
             hp.stride = ks_;
-            hp.pk_lo = pk_lo;
-            hp.pk_hi = pk_hi;
-            if (key_fold) {  // the energies are folded; walk only the candidates' bins
-                hp.c_lo = fold_lo;
-                hp.c_hi = fold_hi;
-                hp.e_given = 1;
-            }
+            hp.pk_lo = 1;
+            hp.pk_hi = 0;
+            band_bins(B8, fres8, sd_maxf(100.0f, 20.0f), sd_minf(5000.0f, (float)sr_ / 2.0f), &hp.pk_lo, &hp.pk_hi);
             hp.K = (int)std::max<uint64_t>(cfg_.key_hpcp_peaks_per_frame, 1);
             hp.hmax = (int)std::max<uint64_t>(cfg_.key_hpcp_num_harmonics, 1);
             hp.p = sd_clampf(cfg_.key_hpcp_mag_power, 0.05f, 1.0f);
@@ -2140,8 +2090,6 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     if (NK > 0) {  // join the key stream
         SDSP_HIP_CHECK(hipStreamWaitEvent(st, kt.ev[2], 0));
         kout = c_.down(d_kout, (size_t)NK);
-        if (d_fold_err && c_.down(d_fold_err, 1)[0] != 0)
-            throw HipError("key mask: the energy fold's hand-off between workgroups timed out");
         htr("E join");
         times_.stft8192_ms += kt.ms(0, 1);
         times_.key_ms += kt.ms(1, 2);

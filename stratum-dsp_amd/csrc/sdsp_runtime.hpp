@@ -1,7 +1,6 @@
 // sdsp_runtime.hpp — host-side runtime internals (device contexts, buffers, launchers).
 #pragma once
 
-#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <map>
@@ -38,7 +37,6 @@ struct DevBuf {
     // the engine streams that may still read the buffer (DeviceCtx::buf sets them); the caller's
     // own streams are never waited on here
     const std::vector<hipStream_t>* readers = nullptr;
-    bool uncached = false;  // device memory that bypasses the caches (cross-workgroup hand-offs)
     void ensure(size_t n) {
         if (n <= bytes) return;
         if (p) {
@@ -52,10 +50,7 @@ struct DevBuf {
         p = nullptr;
         bytes = 0;
         const size_t want = n + n / 8 + 4096;
-        if (uncached)
-            SDSP_HIP_CHECK(hipExtMallocWithFlags(&p, want, hipDeviceMallocUncached));
-        else
-            SDSP_HIP_CHECK(hipMalloc(&p, want));
+        SDSP_HIP_CHECK(hipMalloc(&p, want));
         note_alloc(want);
         bytes = want;
     }
@@ -88,7 +83,6 @@ struct DeviceCtx {
     std::map<int, std::unique_ptr<FftTables>> fft;  // keyed by real FFT size N
     std::map<std::string, std::unique_ptr<DevBuf>> bufs;
     sdsp_stage_times last{};
-    uint32_t fold_epoch = 0;  // k_mask_re launches on this device (tags of its hand-off words)
     DevBuf& buf(const std::string& name) {
         auto& b = bufs[name];
         if (!b) {
