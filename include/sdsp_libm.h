@@ -248,6 +248,43 @@ SD_HD float sd_logf_ge1(float x, const sd_logtab_t* tab) {
     return sd_logf_core(b & 0x7fffffu, (int)(b >> 23) - 127, tab);
 }
 
+/* sd_logf_ge1 with a two-column table {s, ln c}, s = (1/c) 2^-23 (i < 53) or (1/c) 2^-24
+ * (i >= 53), built from the {c, 1/c, ln c} table (sd_logtab2_from).  m - c is an integer k times
+ * 2^-23 (m/2 - c: times 2^-24), so r = k s is the same double product as (m - c) (1/c) without
+ * forming m or c: bit-identical to sd_logf_ge1 (tools/check_logf_ge1.c, every f32 >= 1). */
+typedef struct {
+    double s, lg;
+} sd_logtab2_t;
+SD_HD sd_logtab2_t sd_logtab2_from(const sd_logtab_t* tab, int i) {
+    sd_logtab2_t t;
+    t.s = tab[i].inv * (i < 53 ? 0x1p-23 : 0x1p-24);
+    t.lg = tab[i].lg;
+    return t;
+}
+SD_HD float sd_logf_ge1_t2(float x, const sd_logtab2_t* tab) {
+    if (!(x < SD_INF_F)) return x; /* +inf -> +inf, NaN -> NaN, as sd_logf */
+    const uint32_t b = sd_bits_f(x);
+    const uint32_t mant = b & 0x7fffffu;
+    const int i = (int)(mant >> 16);
+    int e = (int)(b >> 23) - 127;
+    int k = (int)(mant & 0xffffu);
+    if (i >= 53) {
+        k = (int)mant - ((i + 1) << 16);
+        e = e + 1;
+    }
+    const sd_logtab2_t t = tab[i];
+    const double r = (double)k * t.s;
+    double p = -1.0 / 6.0;
+    p = __builtin_fma(p, r, 0.2);
+    p = __builtin_fma(p, r, -0.25);
+    p = __builtin_fma(p, r, 1.0 / 3.0);
+    p = __builtin_fma(p, r, -0.5);
+    p = __builtin_fma(p, r, 1.0);
+    p = p * r;
+    const double ed = (double)e;
+    return (float)__builtin_fma(ed, SD_LN2_HI, __builtin_fma(ed, SD_LN2_LO, t.lg + p));
+}
+
 /* f32::log10 */
 SD_HD float sd_log10f(float x) {
     if (x != x) return x;

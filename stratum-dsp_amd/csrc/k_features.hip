@@ -44,13 +44,13 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
                                                         float* __restrict__ SFO, float* __restrict__ MEL,
                                                         uint64_t total) {
     static_assert((W & (W - 1)) == 0, "W must be a power of two");
-    constexpr int ROWS = FT_STEP + 1;
+    constexpr int ROWS = FT_FRAMES;  // row i: lane i's frame (each wave stages its own 64 rows)
     constexpr int LS = W + 1;
     __shared__ float Mt[ROWS][LS];
     __shared__ float Lt[ROWS][LS];
-    __shared__ sd_logtab_t ltab[128];  // sd_logf's table, read per element by the staging
+    __shared__ sd_logtab2_t ltab[128];  // sd_logf's table {s, ln c}, read per element by the staging
     static_assert(KK == 0 || CW + 2 * KK <= W, "window halo must fit the ring");
-    for (int q = threadIdx.x; q < 128; q += FT_FRAMES) ltab[q] = SD_LOGTAB_D[q];
+    for (int q = threadIdx.x; q < 128; q += FT_FRAMES) ltab[q] = sd_logtab2_from(SD_LOGTAB_D, q);
 
     const uint64_t gb = blockIdx.x;
     const int trk = find_track(tile_pfx, T, gb);
@@ -59,8 +59,8 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
     const uint64_t g0 = frame_pfx[trk];
     const int i = threadIdx.x;
     const bool helper = (i & 63) == 0;
-    const int ro = 63 * (i >> 6) + (i & 63);  // this lane's row; row r <-> frame f0 - 1 + r
-    const int64_t f = f0 - 1 + ro;
+    const int ro = i;  // this lane's LDS row
+    const int64_t f = f0 - 1 + 63 * (i >> 6) + (i & 63);
     const bool own_ok = f >= 0 && f < F;
     const bool valid = !helper && f < F;  // ro >= 1 here, so f >= 0
     const bool has_prev = valid && f >= 1;
@@ -140,57 +140,74 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
         }
     };
 
-    // rows f0-1 .. f0+FT_STEP-1 of the track; row r <-> frame f0-1+r
-    const int64_t r_lo = f0 >= 1 ? 0 : 1;
-    const int64_t r_hi = F - f0 + 1 < ROWS ? F - f0 + 1 : ROWS;  // rows [r_lo, r_hi) exist
-    const int sub = i / CW, jj = i % CW;
+    // Each wave stages the rows of its own 64 lanes (frames f0 - 1 + 63 w + l), so the waves
+    // share no LDS row and run without workgroup barriers: a wave's LDS operations execute in
+    // issue order, and a compiler barrier keeps the staging writes and the walk's reads in
+    // program order.  (The helper row duplicates the previous wave's last row: 1/64 extra loads.)
+    const int lane = i & 63, wrow = i & ~63;
+    const int sub = lane / CW, jj = lane % CW;
+    const int64_t fw = f0 - 1 + 63 * (i >> 6);  // frame of the wave's row 0
 
-    // stage bins [b0, b0+CW) (columns beyond B or rows outside the track read as 0), in two
-    // halves so the loads of the next step are in flight while the current step is walked
-    constexpr int RSTEP = FT_FRAMES / CW;
-    constexpr int NLD = (ROWS + RSTEP - 1) / RSTEP;
+    // stage bins [b0, b0+CW) (columns beyond B or rows outside the track read as 0); the loads
+    // of the next step are in flight while the current step is walked
+    constexpr int RSTEP = 64 / CW;
+    constexpr int NLD = CW;
     const float* rowp[NLD];  // this thread's staged rows
 #pragma unroll
     for (int u = 0; u < NLD; u++) {
-        const int r = sub + u * RSTEP;
-        rowp[u] = nullptr;
-        if (r >= r_lo && r < r_hi) {
+        const int64_t fr = fw + sub + u * RSTEP;
+        rowp[u] = rm.magsA;  // rows outside the track: a valid address, the value is replaced by 0
+        if (fr >= 0 && fr < F) {
             bool odd;
-            const uint64_t row = row_of(f0 - 1 + r, &odd);
+            const uint64_t row = row_of(fr, &odd);
             rowp[u] = (odd ? rm.magsB : rm.magsA) + row * (uint64_t)P.stride;
         }
     }
     float nx[NLD];
+    // unconditional loads (the zeros are selected afterwards): no branch per load, so the
+    // compiler's wait counts stay per load (1.5 % faster than guarded loads; a second chunk in
+    // flight measured no faster, so load latency is not what bounds the kernel)
+    uint32_t row_ok = 0;
+#pragma unroll
+    for (int u = 0; u < NLD; u++) {
+        const int64_t fr = fw + sub + u * RSTEP;
+        row_ok |= (uint32_t)(fr >= 0 && fr < F) << u;
+    }
     auto load = [&](int b0) {
         const int b = b0 + jj;
-        const bool col_ok = b < B;
+        const int bc = b < B ? b : B - 1;
 #pragma unroll
-        for (int u = 0; u < NLD; u++) nx[u] = (col_ok && rowp[u]) ? rowp[u][b] : 0.0f;
+        for (int u = 0; u < NLD; u++) nx[u] = rowp[u][bc];
+    };
+    auto fix = [&](int b0) {  // zeros for columns past B and rows outside the track
+        const bool col_ok = b0 + jj < B;
+#pragma unroll
+        for (int u = 0; u < NLD; u++) nx[u] = (col_ok && ((row_ok >> u) & 1)) ? nx[u] : 0.0f;
     };
     auto commit = [&](int b0) {
+        fix(b0);
         const int slot = (b0 + jj) & (W - 1);
 #pragma unroll
         for (int u = 0; u < NLD; u++) {
-            const int r = sub + u * RSTEP;
-            if (r < ROWS) {
-                Mt[r][slot] = nx[u];
-                Lt[r][slot] = sd_logf_ge1(1.0f + sd_maxf(nx[u], 0.0f), ltab);
-            }
+            const int r = wrow + sub + u * RSTEP;
+            Mt[r][slot] = nx[u];
+            Lt[r][slot] = sd_logf_ge1_t2(1.0f + sd_maxf(nx[u], 0.0f), ltab);
         }
     };
-    __syncthreads();  // ltab
+    __syncthreads();  // ltab; from here on each wave works on its own rows
     // prologue: bins [0, K) (K <= CW); the ring slots of bins [-K, 0) read as L = 0
     if (jj < K) {
         load(0);
         commit(0);
     }
     if (KK > 0)
-        for (int q = threadIdx.x; q < ROWS * KK; q += FT_FRAMES) Lt[q / KK][W - KK + q % KK] = 0.0f;
+        for (int q = 0; q < KK; q++) Lt[ro][W - KK + q] = 0.0f;
     load(K);
     for (int c0 = 0; c0 < B; c0 += CW) {
-        __syncthreads();  // previous step's readers are done with the slots overwritten here
+        // the wave's walk of the previous step has issued its reads of the slots overwritten here
+        asm volatile("" ::: "memory");
         commit(c0 + K);
-        __syncthreads();
+        asm volatile("" ::: "memory");
         if (c0 + CW < B) load(c0 + CW + K);
         const int nb = B - c0 < CW ? B - c0 : CW;
         // a wave with no valid frame skips the walk; lanes of invalid frames in a partly valid
@@ -206,7 +223,7 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
         float Wm[VHK ? CW : 1];
         // every lane walks the flux terms (no divergent branch per bin); lanes without a previous
         // frame read row max(ro - 1, 0) and their sums are never stored
-        const int rp = ro > 0 ? ro - 1 : 0;
+        const int rp = lane > 0 ? ro - 1 : ro;
         if (KK > 0) {
 #pragma unroll
             for (int q = 0; q < (KK > 0 ? CW + 2 * KK : 1); q++) Rw[q] = Lt[rp][(c0 - KK + q) & (W - 1)];

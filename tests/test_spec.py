@@ -109,3 +109,21 @@ def test_stft_silence_and_tiny_frames():
 
 def test_stft_short_input():
     assert oracle.stft(np.ones(100, np.float32), 2048, 512).shape == (0, 1025)
+
+
+def test_logf_ge1_two_column_table_exhaustive(tmp_path):
+    """k_features' ln(1 + max(X, 0)) (sd_logf_ge1_t2: the reduction k * (1/c) 2^-k without
+    forming m or c) is bit-identical to sd_logf_ge1 on every f32 >= 1, +inf and NaN
+    (tools/check_logf_ge1.c: ~1.1e9 inputs, a second or two on 8 threads)."""
+    import shutil
+    import subprocess
+    from pathlib import Path
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    root = Path(__file__).resolve().parents[1]
+    exe = tmp_path / "check_logf_ge1"
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-march=x86-64-v3", "-fopenmp",
+                    str(root / "tools" / "check_logf_ge1.c"), "-o", str(exe), "-lm"], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert " 0 differ" in out.stdout, out.stdout
