@@ -12,6 +12,12 @@ namespace sdsp {
 constexpr int NVAR = 5;  // novelty variants: full, low, mid, high, mel
 
 // ---- k_features ----
+// the mel plans of one 8-bin chunk: per bin j, bits 4j..4j+1 = nflush (<= 3), bit 4j+2 = s0,
+// bit 4j+3 = s1; w0 / w1 as MelPlan (0: no contribution)
+struct MelChunk {
+    uint32_t bits;
+    float w0[8], w1[8];
+};
 struct FeatParams {
     int B;             // bins per frame (nfft/2+1)
     int stride;        // row stride of mags
@@ -23,8 +29,11 @@ struct FeatParams {
     // of every bin of the chunk, bit 2 = FT_CHUNK_FAST (one band, no band-edge clipping of the
     // SuperFlux window, no mel work, full chunk)
     const int* chunk_flags;
+    // FT_CHUNK_MEL chunks (bit 3: as FT_CHUNK_FAST, but with mel work): the chunk's 8 mel plans
+    // packed (MelChunk), indexed by chunk
+    const MelChunk* mel_chunks;
 };
-constexpr int FT_CHUNK_FAST = 4;
+constexpr int FT_CHUNK_FAST = 4, FT_CHUNK_MEL = 8;
 // per-bin mel accumulation plan (k_features): flush `nflush` finished mels before the bin,
 // then, in the reference's contribution order, add L*w0 to accumulator s0 and L*w1 to s1
 // (accumulator 0 = mel mA, 1 = mel mA+1; w = 0 means no contribution)

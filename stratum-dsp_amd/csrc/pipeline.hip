@@ -1161,9 +1161,11 @@ void Pipeline::tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPa
             return v;
         };
         std::vector<int> cf((size_t)(B + 7) / 8 + 1, 0);
+        std::vector<MelChunk> mc((size_t)(B + 7) / 8 + 1, MelChunk{});
         for (int c0 = 0; c0 < B; c0 += 8) {
             const int v0 = band_of(c0);
-            bool fast = fp.K == 4 && c0 + 8 <= B;
+            bool fast = fp.K == 4 && c0 + 8 <= B, mel = false, mel_ok = true;
+            MelChunk& m = mc[(size_t)c0 / 8];
             for (int b = c0; fast && b < c0 + 8; b++) {
                 const int v = band_of(b);
                 if (v != v0) fast = false;
@@ -1173,12 +1175,19 @@ void Pipeline::tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPa
                 }
                 if (fp.n_mels > 0) {
                     const MelPlan& q = mplan[(size_t)b];
-                    if (q.nflush != 0 || q.w0 != 0.0f || q.w1 != 0.0f) fast = false;
+                    if (q.nflush != 0 || q.w0 != 0.0f || q.w1 != 0.0f) mel = true;
+                    if (q.nflush < 0 || q.nflush > 3 || (q.s0 & ~1) || (q.s1 & ~1)) mel_ok = false;
+                    const int j = b - c0;
+                    m.bits |= (uint32_t)(q.nflush & 3) << (4 * j) | (uint32_t)(q.s0 & 1) << (4 * j + 2) |
+                              (uint32_t)(q.s1 & 1) << (4 * j + 3);
+                    m.w0[j] = q.w0;
+                    m.w1[j] = q.w1;
                 }
             }
-            cf[(size_t)c0 / 8] = v0 | (fast ? FT_CHUNK_FAST : 0);
+            cf[(size_t)c0 / 8] = v0 | (fast && !mel ? FT_CHUNK_FAST : 0) | (fast && mel && mel_ok ? FT_CHUNK_MEL : 0);
         }
         fp.chunk_flags = c_.up(tag + "ftchunk", cf);
+        fp.mel_chunks = c_.up(tag + "ftmelchunk", mc);
     }
     o.E = c_.dev<float>(tag + "E", 4 * total);
     o.H = c_.dev<float>(tag + "H", 4 * total);
