@@ -76,6 +76,7 @@ __global__ void k_gain(const unsigned int* __restrict__ peak_bits, int T, float 
 // min_frames long or starting at 0; its start becomes the trim end).  Both follow from the
 // first and the last non-silent frame, found by an order-free min/max reduction.
 __global__ __launch_bounds__(256) void k_trim(const float* __restrict__ rms, const uint64_t* __restrict__ frame_pfx,
+                                              const uint64_t* __restrict__ base_pfx, int stride,
                                               int T, const uint64_t* __restrict__ n_raw, int hop, float thr,
                                               uint64_t min_frames, int enable, uint64_t* __restrict__ trim_start,
                                               uint64_t* __restrict__ trim_end) {
@@ -91,10 +92,10 @@ __global__ __launch_bounds__(256) void k_trim(const float* __restrict__ rms, con
         return;
     }
     const int64_t nf = (int64_t)(frame_pfx[t + 1] - frame_pfx[t]);
-    const float* r = rms + frame_pfx[t];
+    const float* r = rms + base_pfx[t];  // frame f at r[f * stride]
     long long lo = nf, hi = -1;  // first / last non-silent frame
     for (int64_t f = threadIdx.x; f < nf; f += blockDim.x)
-        if (!(r[f] <= thr)) {
+        if (!(r[f * stride] <= thr)) {
             lo = lo < f ? lo : f;
             hi = hi > f ? hi : f;
         }
@@ -607,7 +608,8 @@ __global__ __launch_bounds__(256) void k_frame_rms(const float* __restrict__ x,
                                                           const float* __restrict__ gain,
                                                           const uint64_t* __restrict__ n_len,
                                                           const uint64_t* __restrict__ frame_pfx, int T,
-                                                          uint64_t total, int fs, int hop, float* __restrict__ rms) {
+                                                          uint64_t total, int fs, int hop, float* __restrict__ rms,
+                                                          int only_partial) {
     typedef float f4 __attribute__((ext_vector_type(4)));
     const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (g >= total) return;
@@ -617,6 +619,7 @@ __global__ __launch_bounds__(256) void k_frame_rms(const float* __restrict__ x,
     const uint64_t s = f * (uint64_t)hop;
     const uint64_t e = s + (uint64_t)fs < n ? s + (uint64_t)fs : n;
     const int64_t len = e > s ? (int64_t)(e - s) : 0;
+    if (only_partial && len == fs) return;  // k_rms_gather took this frame from the raw pass
     const uint64_t a = src_off[trk] + s;  // float index of the frame's first sample
     const int d = (int)(a & 3u);
     const f4* q = reinterpret_cast<const f4*>(x + (a - (uint64_t)d));
@@ -775,13 +778,39 @@ void launch_frame_rms(const float* x, const uint64_t* src_off, const float* gain
         return;
     }
     hipLaunchKernelGGL(k_frame_rms, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, x, src_off, gain, n_len,
-                       frame_pfx, T, total, fs, hop, rms);
+                       frame_pfx, T, total, fs, hop, rms, 0);
+}
+
+// The energy pass's frame RMS from the trim pass's (one read of the samples for both): with the
+// trim pass run on the raw signal at the energy hop, and every trim start a multiple of that hop
+// (trim frames start at multiples of fs / 2, a multiple of hop), trimmed frame j of track i is
+// raw frame raw_base[i] + j whenever it is whole (j hop + fs <= n_trim): the same samples, gain
+// and fold order, so the same value.  Frames cut short by the trimmed end are folded again by
+// k_frame_rms (only_partial).
+__global__ __launch_bounds__(256) void k_rms_gather(const float* __restrict__ raw, const uint64_t* __restrict__ raw_base,
+                                                    const uint64_t* __restrict__ frame_pfx, int T, uint64_t total,
+                                                    const uint64_t* __restrict__ n_trim, int fs, int hop,
+                                                    float* __restrict__ rms) {
+    const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (g >= total) return;
+    const int i = find_track(frame_pfx, T, g);
+    const uint64_t j = g - frame_pfx[i];
+    if (j * (uint64_t)hop + (uint64_t)fs <= n_trim[i]) rms[g] = raw[raw_base[i] + j];
+}
+void launch_frame_rms_from_raw(const float* raw, const uint64_t* raw_base, const float* x, const uint64_t* src_off,
+                               const float* gain, const uint64_t* n_trim, const uint64_t* frame_pfx, int T, uint64_t total,
+                               int fs, int hop, float* rms, hipStream_t st) {
+    if (total == 0) return;
+    const dim3 grid((unsigned)((total + 255) / 256));
+    hipLaunchKernelGGL(k_rms_gather, grid, dim3(256), 0, st, raw, raw_base, frame_pfx, T, total, n_trim, fs, hop, rms);
+    hipLaunchKernelGGL(k_frame_rms, grid, dim3(256), 0, st, x, src_off, gain, n_trim, frame_pfx, T, total, fs, hop, rms, 1);
 }
 void launch_trim(const float* rms, const uint64_t* frame_pfx, int T, const uint64_t* n_raw, int hop, float thr,
-                 uint64_t min_frames, int enable, uint64_t* trim_start, uint64_t* trim_end, hipStream_t st) {
+                 uint64_t min_frames, int enable, uint64_t* trim_start, uint64_t* trim_end, hipStream_t st,
+                 const uint64_t* base_pfx, int stride) {
     if (T == 0) return;
-    hipLaunchKernelGGL(k_trim, dim3(T), dim3(256), 0, st, rms, frame_pfx, T, n_raw, hop, thr, min_frames,
-                       enable, trim_start, trim_end);
+    hipLaunchKernelGGL(k_trim, dim3(T), dim3(256), 0, st, rms, frame_pfx, base_pfx ? base_pfx : frame_pfx,
+                       base_pfx ? stride : 1, T, n_raw, hop, thr, min_frames, enable, trim_start, trim_end);
 }
 void launch_energy_onsets(const float* rms, const uint64_t* frame_pfx, const uint64_t* n_trim, int hop, float factor,
                           uint32_t* out, const uint64_t* out_off, int* out_n, int T, hipStream_t st) {

@@ -262,8 +262,16 @@ void launch_loudness_gain(const float* x, const uint64_t* in_off, const uint64_t
                           int* status, hipStream_t st);
 void launch_frame_rms(const float* x, const uint64_t* src_off, const float* gain, const uint64_t* n_len,
                       const uint64_t* frame_pfx, int T, uint64_t total, int fs, int hop, float* rms, hipStream_t st, bool per_frame_kernel = false);
+// base_pfx / stride: trim frame f of track t at rms[base_pfx[t] + f * stride] (default: frame_pfx, 1)
 void launch_trim(const float* rms, const uint64_t* frame_pfx, int T, const uint64_t* n_raw, int hop, float thr,
-                 uint64_t min_frames, int enable, uint64_t* trim_start, uint64_t* trim_end, hipStream_t st);
+                 uint64_t min_frames, int enable, uint64_t* trim_start, uint64_t* trim_end, hipStream_t st,
+                 const uint64_t* base_pfx = nullptr, int stride = 1);
+// the energy pass's frame RMS (fs, hop) of the trimmed tracks from `raw`, the same framing of the
+// raw tracks (k_rms_gather), frame j of track i at raw[raw_base[i] + j]; frames the trimmed end
+// cuts short are computed from the samples
+void launch_frame_rms_from_raw(const float* raw, const uint64_t* raw_base, const float* x, const uint64_t* src_off,
+                               const float* gain, const uint64_t* n_trim, const uint64_t* frame_pfx, int T, uint64_t total,
+                               int fs, int hop, float* rms, hipStream_t st);
 void launch_energy_onsets(const float* rms, const uint64_t* frame_pfx, const uint64_t* n_trim, int hop, float factor,
                           uint32_t* out, const uint64_t* out_off, int* out_n, int T, hipStream_t st);
 void launch_flux_onsets(const float* sfo, const float* hfc, const float* hpe, float* scratch, const uint64_t* frame_pfx,

@@ -1419,14 +1419,33 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         launch_peak_gain(d_samples, d_off, d_nr, d_cpfx, T, cpfx[(size_t)T], d_peak, target, cfg_.enable_normalization,
                          d_gain, st);
     }
-    float* d_srms = c_.dev<float>("A.srms", spfx[(size_t)T]);
-    launch_frame_rms(d_samples, d_off, d_gain, d_nr, d_spfx, T, spfx[(size_t)T], FS, FS / 2, d_srms, st);
+    // One read of the samples for both frame-RMS passes: with trimming on and the trim hop (fs / 2)
+    // a multiple of the energy hop, the trim pass runs on the raw signal at the energy hop (trim
+    // frame f = raw frame f * (fs / 2) / hop), and the energy pass takes its whole frames from it
+    // (launch_frame_rms_from_raw)
+    const int G_e = HOP > 0 && FS % HOP == 0 ? FS / HOP : 0;
+    const bool rms_shared = cfg_.enable_silence_trimming && HOP > 0 && HOP % 32 == 0 && (FS / 2) % HOP == 0 &&
+                            (G_e == 1 || G_e == 2 || G_e == 4 || G_e == 8);
+    std::vector<uint64_t> rpfx((size_t)T + 1, 0);
+    for (int t = 0; t < T; t++)
+        rpfx[(size_t)t + 1] = rpfx[(size_t)t] + (rms_shared ? (nr[(size_t)t] >= (uint64_t)FS ? (nr[(size_t)t] - FS) / HOP + 1 : 1) : 0);
+    float* d_srms = nullptr;
+    uint64_t* d_rpfx = nullptr;
+    if (rms_shared) {
+        d_rpfx = c_.up("A.rpfx", rpfx);
+        d_srms = c_.dev<float>("A.rrms", std::max<uint64_t>(rpfx[(size_t)T], 1));
+        launch_frame_rms(d_samples, d_off, d_gain, d_nr, d_rpfx, T, rpfx[(size_t)T], FS, HOP, d_srms, st);
+    } else {
+        d_srms = c_.dev<float>("A.srms", spfx[(size_t)T]);
+        launch_frame_rms(d_samples, d_off, d_gain, d_nr, d_spfx, T, spfx[(size_t)T], FS, FS / 2, d_srms, st);
+    }
     const float thr = sd_powf(10.0f, cfg_.min_amplitude_db / 20.0f);
     const uint64_t min_samples = sd_f2u64((float)500u / 1000.0f * (float)sr_);
     const uint64_t min_frames = (min_samples + (FS / 2) - 1) / (FS / 2);
     uint64_t* d_ts = c_.dev<uint64_t>("A.ts", (size_t)T);
     uint64_t* d_te = c_.dev<uint64_t>("A.te", (size_t)T);
-    launch_trim(d_srms, d_spfx, T, d_nr, FS / 2, thr, min_frames, cfg_.enable_silence_trimming, d_ts, d_te, st);
+    launch_trim(d_srms, d_spfx, T, d_nr, FS / 2, thr, min_frames, cfg_.enable_silence_trimming, d_ts, d_te, st,
+                rms_shared ? d_rpfx : nullptr, rms_shared ? (FS / 2) / HOP : 1);
     SDSP_HIP_CHECK(hipGetLastError());
     std::vector<float> gain_h = c_.down(d_gain, (size_t)T);
     std::vector<uint64_t> ts = c_.down(d_ts, (size_t)T), te = c_.down(d_te, (size_t)T);
@@ -1744,7 +1763,17 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     float* d_g = c_.up("B.gain2", bin.gain_h);
     uint64_t* d_nt = c_.up("B.ntrim", bin.n_trim);
     float* d_erms = c_.dev<float>("B.erms", std::max<uint64_t>(bo.total, 1));
-    launch_frame_rms(d_samples, d_src, d_g, d_nt, bo.d_fpfx, NR, bo.total, FS, HOP, d_erms, st);
+    bool from_raw = rms_shared;
+    std::vector<uint64_t> rbase;
+    for (int t : R) {
+        from_raw = from_raw && ts[(size_t)t] % (uint64_t)HOP == 0;
+        rbase.push_back(rpfx[(size_t)t] + ts[(size_t)t] / (uint64_t)HOP);
+    }
+    if (from_raw)
+        launch_frame_rms_from_raw(d_srms, c_.up("B.rbase", rbase), d_samples, d_src, d_g, d_nt, bo.d_fpfx, NR, bo.total,
+                                  FS, HOP, d_erms, st);
+    else
+        launch_frame_rms(d_samples, d_src, d_g, d_nt, bo.d_fpfx, NR, bo.total, FS, HOP, d_erms, st);
     uint32_t* d_eon = c_.dev<uint32_t>("B.eon", std::max<uint64_t>(bo.total, 1));
     int* d_en = c_.dev<int>("B.en", (size_t)NR);
     launch_energy_onsets(d_erms, bo.d_fpfx, d_nt, HOP, sd_powf(10.0f, -20.0f / 20.0f), d_eon, bo.d_fpfx, d_en, NR, st);

@@ -89,3 +89,55 @@ def test_edge_batch_equals_single_calls():
             assert isinstance(o, sdsp.AnalysisError) and o.code == st, (o, st, ref)
         else:
             assert isinstance(o, dict) and not parity.diff_results(o, ref), parity.diff_results(o, ref)
+
+
+# Leading / trailing silence of assorted lengths: the trim start moves the energy pass's frames
+# onto the raw signal's hop grid (launch_frame_rms_from_raw takes them from the trim pass), and
+# the trimmed end cuts the last frames short (those are folded from the samples).
+@pytest.mark.parametrize("lead,tail", [(0.0, 0.0), (0.37, 0.0), (1.3, 0.71), (2.9, 1.93), (0.0, 2.5)])
+def test_leading_trailing_silence(lead, tail):
+    sr = 44100
+    x, *_ = synth.make_track(7400 + int(lead * 100) + int(tail * 10), seconds=14.0, sr=sr)
+    y = np.concatenate([np.zeros(int(lead * sr), np.float32), x,
+                        np.zeros(int(tail * sr) + 123, np.float32)]).astype(np.float32)
+    assert _same(y, sr) is not None
+
+
+def test_short_island_after_trimming():
+    # ~1.5 frames of tone between long silences: the trimmed track is shorter than two frames
+    sr = 44100
+    y = np.zeros(sr * 6, np.float32)
+    t = np.arange(3100, dtype=np.float64) / sr
+    y[sr * 3 + 17: sr * 3 + 17 + 3100] = (0.5 * np.sin(2 * np.pi * 440.0 * t)).astype(np.float32)
+    _same(y, sr)
+
+
+@pytest.mark.parametrize("hop", [256, 384, 1024])
+def test_trim_with_other_hops(hop):
+    # hop 256 / 1024: the shared raw pass (G = 8 / 2); 384 does not divide the trim hop: two passes
+    sr = 44100
+    x, *_ = synth.make_track(7500 + hop, seconds=12.0, sr=sr)
+    y = np.concatenate([np.zeros(int(1.7 * sr), np.float32), x, np.zeros(sr, np.float32)]).astype(np.float32)
+    ocfg, cfg = oracle.default_config(), sdsp.default_config()
+    ocfg.hop_size = cfg.hop_size = hop
+    st, ref = oracle.analyze(y, sr, ocfg)
+    assert st == 0
+    got = sdsp.analyze_audio(y, sr, config=cfg)
+    assert not parity.diff_results(got, ref)
+    assert parity.exact_fraction(got, ref) == 1.0
+
+
+def test_batch_mixed_trims():
+    sr = 44100
+    tracks, refs = [], []
+    for k, lead in enumerate([0.0, 0.5, 1.25, 2.0]):
+        x, *_ = synth.make_track(7600 + k, seconds=10.0 + k, sr=sr)
+        y = np.concatenate([np.zeros(int(lead * sr), np.float32), x, np.zeros(int(0.3 * k * sr), np.float32)])
+        tracks.append(y.astype(np.float32))
+        st, ref = oracle.analyze(tracks[-1], sr)
+        assert st == 0
+        refs.append(ref)
+    got = sdsp.analyze_batch(tracks, sr)
+    for g, r in zip(got, refs):
+        assert not parity.diff_results(g, r)
+        assert parity.exact_fraction(g, r) == 1.0
