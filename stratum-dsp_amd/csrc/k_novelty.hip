@@ -107,6 +107,23 @@ __global__ __launch_bounds__(1024) void k_novelty(const float* __restrict__ E, c
 // k_mel_norm, one workgroup per track: normalise, then the curve's sequential sum.
 __device__ inline float mel_flux_frame(const float* mtile, int RW, int i, int n_mels, int K) {
     float sum = 0.0f;
+    if (K == 2) {
+        // the default: the previous frame's mels in a 5-register window (one LDS read per mel
+        // instead of five).  Mel sums are >= +0 and never NaN, so the window's +0 padding past
+        // either end leaves every maximum (from +0, over the clipped range) unchanged.
+        float w0 = 0.0f, w1 = 0.0f, w2 = mtile[i], w3 = n_mels > 1 ? mtile[RW + i] : 0.0f;
+        for (int b = 0; b < n_mels; b++) {
+            const float w4 = b + 2 < n_mels ? mtile[(b + 2) * RW + i] : 0.0f;
+            const float pm = sd_maxf(sd_maxf(sd_maxf(sd_maxf(sd_maxf(0.0f, w0), w1), w2), w3), w4);
+            const float d = sd_maxf(mtile[b * RW + i + 1] - pm, 0.0f);
+            sum += d * d;
+            w0 = w1;
+            w1 = w2;
+            w2 = w3;
+            w3 = w4;
+        }
+        return __builtin_sqrtf(sum);
+    }
     for (int b = 0; b < n_mels; b++) {
         const int lo = b - K < 0 ? 0 : b - K;
         const int hi = b + K + 1 < n_mels ? b + K + 1 : n_mels;
@@ -125,9 +142,17 @@ __global__ __launch_bounds__(256) void k_mel_flux(const float* __restrict__ MEL,
     extern __shared__ float mtile[];  // [n_mels][257]: frames gb .. gb+256
     constexpr int RW = 257;
     const uint64_t gb = (uint64_t)blockIdx.x * 256;
-    for (int m = 0; m < n_mels; m++)
-        for (int r = threadIdx.x; r < RW; r += 256)
-            mtile[m * RW + r] = gb + r < total ? MEL[(uint64_t)m * total + gb + r] : 0.0f;
+    // 8 mel rows in flight per thread (the loads of a batch before its LDS stores)
+    for (int m0 = 0; m0 < n_mels; m0 += 8)
+        for (int r = threadIdx.x; r < RW; r += 256) {
+            float v[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                v[k] = (m0 + k < n_mels && gb + r < total) ? MEL[(uint64_t)(m0 + k) * total + gb + r] : 0.0f;
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                if (m0 + k < n_mels) mtile[(m0 + k) * RW + r] = v[k];
+        }
     __syncthreads();
     const int i = threadIdx.x;
     const uint64_t g = gb + i;
