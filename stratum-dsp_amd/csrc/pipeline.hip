@@ -836,6 +836,19 @@ class Pipeline {
 
     void sub_batch(const float* d_samples, const std::vector<uint64_t>& in_off, const std::vector<uint64_t>& n_raw,
                    const std::vector<int>& idx, std::vector<TrackRes>& res);
+    // Late key join: a sub-batch's key results are read after the next sub-batch's tempo path is
+    // queued, so the key stream's tail (mask, HPCP, vote) runs beside that tempo path instead of
+    // holding the main stream back.  Uploads read by the key stream and the key output live in
+    // per-parity buffers (E0.*, E1.*); the key stream itself is in order, so its big buffers are
+    // shared.
+    struct KeyPending {
+        std::unique_ptr<Timers> kt;
+        KeyOut* d_kout = nullptr;
+        std::vector<size_t> at;  // result slot of each key track
+    };
+    std::unique_ptr<KeyPending> key_pending_;
+    int sb_parity_ = 0;
+    void finish_key(std::vector<TrackRes>& res);
     void tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPassOut& out);
     void legacy_select(const TempoPassIn& bin, const uint32_t* d_onsets, const uint64_t* d_on_off, const int* d_on_n,
                        const std::vector<int>& R, const std::vector<int>& idx, std::vector<TrackRes>& res,
@@ -915,6 +928,7 @@ void Pipeline::run(const float* d_samples, const std::vector<uint64_t>& in_off, 
         cum += need[i];
     }
     flush();
+    finish_key(res);
     times_.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     d_.last = times_;
 }
@@ -1367,6 +1381,24 @@ void Pipeline::tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPa
 namespace sdsp {
 
 // SDSP_HOST_TRACE=1: host wall time between the sub-batch's synchronisation points (stderr)
+void Pipeline::finish_key(std::vector<TrackRes>& res) {
+    if (!key_pending_) return;
+    std::unique_ptr<KeyPending> kp = std::move(key_pending_);
+    SDSP_HIP_CHECK(hipStreamWaitEvent(d_.stream, kp->kt->ev[2], 0));
+    const std::vector<KeyOut> kout = c_.down(kp->d_kout, kp->at.size());
+    for (size_t k = 0; k < kp->at.size(); k++) {
+        TrackRes& r = res[kp->at[k]];
+        const KeyOut& ko = kout[k];
+        if (!ko.ok) continue;
+        r.key_mode = ko.mode;
+        r.key_tonic = ko.tonic;
+        r.key_conf = ko.conf;
+        r.key_clarity = ko.clarity;
+    }
+    times_.stft8192_ms += kp->kt->ms(0, 1);
+    times_.key_ms += kp->kt->ms(1, 2);
+}
+
 struct HostTrace {
     bool on = std::getenv("SDSP_HOST_TRACE") != nullptr;
     std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now(), tp = t0;
@@ -1543,7 +1575,8 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     Timers& kt = *ktp;
     kt.init(d_);
     // what the main stream uploads for the key stream (read by it before the sub-batch's join)
-    const std::string EP = "E.";
+    sb_parity_ ^= 1;
+    const std::string EP = sb_parity_ ? "E1." : "E0.";
     // SDSP_SERIAL_STREAMS=1 keeps the key path on the main stream (per-kernel profiling)
     static const bool serial_streams = std::getenv("SDSP_SERIAL_STREAMS") != nullptr;
     hipStream_t st2 = serial_streams ? st : d_.stream2;
@@ -2125,7 +2158,19 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     tm.mark(5);
     tm.mark(6);
     const bool beat_sync = cfg_.enable_key_beat_synchronous && !cfg_.enable_key_log_frequency;
-    if (NK > 0) {  // join the key stream
+    // the previous sub-batch's key results (its key work ran ahead of this one's on the key stream)
+    finish_key(res);
+    // late join by default (+2 % in alternating bench runs on one box, 2,350 vs 2,301 tracks/s:
+    // the main stream otherwise idles ~45 ms per sub-batch waiting for the key tail);
+    // SDSP_NO_KEY_DEFER=1 joins at the end of each sub-batch (the tests' control)
+    const bool defer_key =
+        NK > 0 && !beat_sync && !serial_streams && !dbg_on && std::getenv("SDSP_NO_KEY_DEFER") == nullptr;
+    if (defer_key) {
+        key_pending_.reset(new KeyPending());
+        key_pending_->kt = std::move(ktp);
+        key_pending_->d_kout = d_kout;
+        for (int k = 0; k < NK; k++) key_pending_->at.push_back((size_t)idx[(size_t)R[(size_t)K[(size_t)k]]]);
+    } else if (NK > 0) {  // join the key stream
         SDSP_HIP_CHECK(hipStreamWaitEvent(st, kt.ev[2], 0));
         kout = c_.down(d_kout, (size_t)NK);
         htr("E join");
@@ -2234,7 +2279,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
             }
         }
     }
-    for (int k = 0; k < NK; k++) {
+    for (int k = 0; k < NK && !defer_key; k++) {
         TrackRes& r = res[(size_t)idx[(size_t)R[(size_t)K[(size_t)k]]]];
         const KeyOut& ko = kout[(size_t)k];
         if (!ko.ok) continue;

@@ -144,14 +144,26 @@ def test_key_peak_list_capacities(peaks):
         assert st == 0 and parity.exact_fraction(got[i], ref) == 1.0, i
 
 
-def test_sub_batches_vs_oracle(monkeypatch):
-    """A batch split into several sub-batches by a small HBM budget (two streams, per-sub-batch
-    key join): a sample against the oracle."""
+@pytest.mark.parametrize("late_join", [True, False])
+def test_sub_batches_vs_oracle(monkeypatch, late_join):
+    """A batch split into several sub-batches by a small HBM budget (two streams), with the key
+    results joined one sub-batch late (default: the key tail runs beside the next sub-batch's
+    tempo path) and at the end of each sub-batch (SDSP_NO_KEY_DEFER=1): equal results, a sample
+    against the oracle."""
     lens = [44100 * 30 + 37 * k for k in range(36)] + [5000, 44100 * 61]
     buf, offs, lens = _device_tracks(lens, 1700)
     monkeypatch.setenv("SDSP_HBM_BUDGET_GB", "1")  # several sub-batches
+    if late_join:
+        monkeypatch.delenv("SDSP_NO_KEY_DEFER", raising=False)
+    else:
+        monkeypatch.setenv("SDSP_NO_KEY_DEFER", "1")
     got = sdsp.analyze_batch_device(buf.ptr, offs, lens)
     assert sdsp.stage_times()["stft8192_launches"] >= 2
     for i in (0, 17, 35, 36, 37):
         st, ref = oracle.analyze(buf.to_host(int(offs[i]), int(lens[i])), 44100)
         assert st == 0 and parity.exact_fraction(got[i], ref) == 1.0, i
+    # every track's result equals the other join's
+    monkeypatch.setenv("SDSP_NO_KEY_DEFER", "1")
+    ctl = sdsp.analyze_batch_device(buf.ptr, offs, lens)
+    for i, (a, b) in enumerate(zip(got, ctl)):
+        assert not parity.diff_results(a, b) and parity.exact_fraction(a, b) == 1.0, i
