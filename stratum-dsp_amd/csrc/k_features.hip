@@ -13,19 +13,22 @@
 // restatement).  Each wave covers 63 frames in lanes 1-63; lane 0 is a helper holding the frame
 // before the wave's first.  The spectral flux needs X/max of every frame twice (as frame t and as
 // frame t-1 of the next); each lane divides its own frame's bins once and takes the previous
-// frame's quotients from lane - 1 (DPP wave shift), halving the per-bin IEEE divisions.  Bins are streamed through two circular LDS windows of W columns (slot =
-// bin mod W): raw magnitudes and their logs.  Each step loads the CW bins K ahead of the
-// ones it processes (coalesced row segments, log computed once per element), so the
-// SuperFlux max filter over [b-K, b+K] of the previous frame always finds its halo resident
-// and no column is loaded or logged twice.  Row stride W+1 (odd) keeps the per-thread row
-// walks bank-conflict-free.
+// frame's quotients from lane - 1 (DPP wave shift), halving the per-bin IEEE divisions.  Bins
+// are streamed through two circular LDS windows of W columns (slot = bin mod W): raw magnitudes
+// and their logs.  Each wave stages the 64 rows of its own lanes (no workgroup barrier in the
+// walk).  Each step loads the CW bins K ahead of the ones it processes (row segments, log
+// computed once per element from a two-column table, sd_logf_ge1_t2), so the SuperFlux max
+// filter over [b-K, b+K] of the previous frame always finds its halo resident and no column is
+// loaded or logged twice.  Row stride W+1 (odd) keeps the per-thread row walks
+// bank-conflict-free.
 //
 // Mel bands: every bin feeds at most two adjacent triangles (or one narrow triangle twice,
 // rising then falling edge) and the triangles start in bin order, so a thread keeps only two
 // running sums (mels mA, mA+1) in registers; the host precomputes, per bin, how many
 // finished mels to flush before the bin (uniform across the workgroup) and the ordered
 // (accumulator, weight) contributions.  Flushed mels are stored mel-major (MEL[m*total + t]),
-// coalesced across the workgroup.
+// coalesced across the workgroup.  Within the mel range the 8 plans of a chunk are packed
+// (MelChunk) and read with one scalar load.
 #include <stdexcept>
 #include <type_traits>
 
