@@ -499,7 +499,12 @@ __device__ void mode_heuristic(float sorted[24], int order[24], const float* avg
 constexpr int KV_ROW = 64;  // segment scratch row: 24 sorted, 24 order, clarity, used, cw, wsum, avg[12]
 constexpr int KV_MAXSCALE = 8;
 
-__global__ __launch_bounds__(256) void k_key_vote(const int* __restrict__ tracks, int n_items,
+// threads per track in k_key_vote: its frame loops (median smoothing, frame weights) are
+// latency-bound, so more lanes per track shorten the key stream's last kernel
+#ifndef KV_THREADS
+#define KV_THREADS 1024
+#endif
+__global__ __launch_bounds__(KV_THREADS) void k_key_vote(const int* __restrict__ tracks, int n_items,
                                                   const uint64_t* __restrict__ frame_pfx, float* __restrict__ chroma_raw,
                                                   const float* __restrict__ energy, float* __restrict__ chroma_s,
                                                   float* __restrict__ weights, float* __restrict__ seg_scratch,
@@ -507,7 +512,7 @@ __global__ __launch_bounds__(256) void k_key_vote(const int* __restrict__ tracks
                                                   KeyParams P, KeyOut* __restrict__ out, KeyDbg* __restrict__ dbg) {
     __shared__ int hist[256];
     __shared__ int misc[4];
-    __shared__ int redi[8];
+    __shared__ int redi[KV_THREADS / 64];
     __shared__ float acc[48];
     __shared__ int use_w_s, used_s;
     __shared__ float totw_s;
@@ -938,7 +943,7 @@ void launch_key_vote(const int* tracks, int n_items, const uint64_t* frame_pfx, 
                      const float* energy, float* chroma_s, float* weights, float* seg_scratch, const uint64_t* seg_off,
                      const float* tmpl, const KeyParams& P, KeyOut* out, hipStream_t st, KeyDbg* dbg) {
     if (n_items == 0) return;
-    hipLaunchKernelGGL(k_key_vote, dim3(n_items), dim3(256), 0, st, tracks, n_items, frame_pfx, chroma_raw, energy,
+    hipLaunchKernelGGL(k_key_vote, dim3(n_items), dim3(KV_THREADS), 0, st, tracks, n_items, frame_pfx, chroma_raw, energy,
                        chroma_s, weights, seg_scratch, seg_off, tmpl, P, out, dbg);
 }
 
