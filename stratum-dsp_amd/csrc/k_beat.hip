@@ -578,10 +578,52 @@ __global__ __launch_bounds__(1024) void k_beat_compact(int n, const BeatOut* __r
     }
 }
 
+// The same gather with one 64-thread workgroup per track: the wave sums the counts of the tracks
+// before its own (n/64 loads per lane, L2-resident) and copies its track.  A single-wave
+// workgroup dispatches into any free wave slot, where the 1024-thread one above waits for 16 slots
+// on one CU; on the shared chip (the key stream's STFT holds most slots) that wait stalled the
+// tempo stream behind it.  Used up to COMPACT_W_MAX tracks (the prefix work is quadratic in n).
+constexpr int COMPACT_W_MAX = 4096;
+__global__ __launch_bounds__(64) void k_beat_compact_w(int n, const BeatOut* __restrict__ out,
+                                                       const uint64_t* __restrict__ beat_off,
+                                                       const float* __restrict__ beats, const float* __restrict__ downs,
+                                                       uint64_t* __restrict__ pfx, float* __restrict__ cb,
+                                                       float* __restrict__ cd) {
+    const int i = blockIdx.x, lane = threadIdx.x;
+    uint64_t ab = 0, ad = 0;
+    for (int j = lane; j < i; j += 64) {
+        const BeatOut r = out[j];
+        ab += r.ok > 0 ? (uint64_t)r.n_beats : 0;
+        ad += r.ok > 0 ? (uint64_t)r.n_down : 0;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        ab += __shfl_xor(ab, o, 64);
+        ad += __shfl_xor(ad, o, 64);
+    }
+    const BeatOut r = out[i];
+    const uint64_t nb = r.ok > 0 ? (uint64_t)r.n_beats : 0, nd = r.ok > 0 ? (uint64_t)r.n_down : 0;
+    if (lane == 0) {
+        pfx[i] = ab;
+        pfx[n + 1 + i] = ad;
+        if (i == n - 1) {
+            pfx[n] = ab + nb;
+            pfx[2 * n + 1] = ad + nd;
+        }
+    }
+    if (r.ok <= 0) return;
+    const uint64_t src = beat_off[i];
+    for (int k = lane; k < r.n_beats; k += 64) cb[ab + k] = beats[src + k];
+    for (int k = lane; k < r.n_down; k += 64) cd[ad + k] = downs[src + k];
+}
+
 void launch_beat_compact(int n, const BeatOut* out, const uint64_t* beat_off, const float* beats, const float* downs,
                          uint64_t* pfx, float* cb, float* cd, hipStream_t st) {
     if (n == 0) return;
-    hipLaunchKernelGGL(k_beat_compact, dim3(1), dim3(1024), 0, st, n, out, beat_off, beats, downs, pfx, cb, cd);
+    if (n <= COMPACT_W_MAX)
+        hipLaunchKernelGGL(k_beat_compact_w, dim3(n), dim3(64), 0, st, n, out, beat_off, beats, downs, pfx, cb, cd);
+    else
+        hipLaunchKernelGGL(k_beat_compact, dim3(1), dim3(1024), 0, st, n, out, beat_off, beats, downs, pfx, cb, cd);
 }
 
 }  // namespace sdsp
