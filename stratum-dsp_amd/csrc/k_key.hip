@@ -499,10 +499,12 @@ __device__ void mode_heuristic(float sorted[24], int order[24], const float* avg
 constexpr int KV_ROW = 64;  // segment scratch row: 24 sorted, 24 order, clarity, used, cw, wsum, avg[12]
 constexpr int KV_MAXSCALE = 8;
 
-// threads per track in k_key_vote: its frame loops (median smoothing, frame weights) are
-// latency-bound, so more lanes per track shorten the key stream's last kernel
+// threads per track in k_key_vote.  1024 halves the kernel's serial time (its frame loops are
+// latency-bound) but triples it in the two-stream pipeline (16.9 vs 5.5 ms per launch): a
+// 1024-thread workgroup needs most of a CU's VGPRs at once, and beside the 8192-point STFT's
+// 256-VGPR waves such a CU seldom comes free
 #ifndef KV_THREADS
-#define KV_THREADS 1024
+#define KV_THREADS 256
 #endif
 __global__ __launch_bounds__(KV_THREADS) void k_key_vote(const int* __restrict__ tracks, int n_items,
                                                   const uint64_t* __restrict__ frame_pfx, float* __restrict__ chroma_raw,
