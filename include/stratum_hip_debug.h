@@ -1,0 +1,58 @@
+/*
+ * stratum_hip_debug.h -- test and probe entry points of libstratum_hip.so.
+ *
+ * Not part of the drop-in boundary (include/stratum_hip.h): no reference interface corresponds to
+ * these.  They exist for the parity tests (stage probes compared against the oracle), the
+ * benchmark's isolated kernel timing and the failure-path tests.  The library reads no test switch
+ * from the environment; the hooks below are set only through sdsp_debug_set_test_hooks.
+ */
+#ifndef STRATUM_HIP_DEBUG_H
+#define STRATUM_HIP_DEBUG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/*
+ * Test hooks, process-wide: fail_chunk >= 0 makes sdsp_analyze_batch's chunk of that index throw
+ * (the per-chunk failure path); devices[0..n_devices) replaces the device mask's worker list
+ * (repeats allowed: two workers on device 0 run the multi-device chunk path on one GPU);
+ * stft_frame_parallel != 0 forces the frame-parallel STFT kernel for every hop.  Reset with
+ * (-1, NULL, 0, 0).
+ */
+int32_t sdsp_debug_set_test_hooks(int64_t fail_chunk, const int32_t* devices, uint32_t n_devices,
+                                  int32_t stft_frame_parallel);
+
+/* Device allocations the engine has made so far (count, bytes): "a repeated call allocates nothing". */
+int32_t sdsp_debug_alloc_stats(uint64_t* n_allocs, uint64_t* bytes);
+
+/*
+ * STFT magnitudes of one host buffer (x * gain framed at hop), frames x (nfft/2 + 1) into host_out;
+ * frame maxima into host_frame_max (NULL allowed; not for nfft 8192).
+ */
+int32_t sdsp_debug_stft(const float* host_x, uint64_t n, uint64_t nfft, uint64_t hop, float gain, float* host_out,
+                        float* host_frame_max, int32_t device);
+
+/*
+ * Frame RMS of n_tracks host tracks (track t = host_x[offs[t] .. offs[t] + lens[t])), frames of fs
+ * samples every hop, the silence-trimming framing; per_frame = 1 forces the per-frame kernel.
+ */
+int32_t sdsp_debug_frame_rms(const float* host_x, uint64_t n_total, const uint64_t* offs, const uint64_t* lens,
+                             const float* gains, uint64_t n_tracks, uint64_t fs, uint64_t hop, int32_t per_frame,
+                             float* host_out, int32_t device);
+
+/*
+ * Isolated STFT kernel timing: `reps` launches over n_tracks device-resident noise tracks of len
+ * samples; mean launch time (HIP events on the launch stream) and algorithmic bytes per launch
+ * (4 N_in + 4 F (nfft/2 + 1) per track).  stride 0 = the pipeline's row stride.
+ */
+int32_t sdsp_probe_stft(int32_t device, uint64_t nfft, uint64_t hop, uint64_t n_tracks, uint64_t len, int32_t reps,
+                        int32_t stride, double* ms_per_launch, double* bytes_per_launch);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* STRATUM_HIP_DEBUG_H */

@@ -182,12 +182,16 @@ bool msadpcm_decode(const uint8_t* d, uint64_t n, int ch, int ba, const std::vec
             for (int half = 0; half < 2; half++) {
                 const int nib = half == 0 ? p[k] >> 4 : p[k] & 15;
                 const int sn = nib >= 8 ? nib - 16 : nib;
-                int pred = (s1[c] * c1[c] + s2[c] * c2[c]) / 256 + sn * delta[c];
+                // 64-bit predictor and adaptation: on corrupt nibbles delta grows without bound, and
+                // (s1 c1 + s2 c2) reaches 2^31 at the extremes; delta is capped as FFmpeg's decoder
+                // caps it (INT_MAX / 768), so every product stays well inside 64 bits
+                int64_t pred = ((int64_t)s1[c] * c1[c] + (int64_t)s2[c] * c2[c]) / 256 + (int64_t)sn * delta[c];
                 pred = pred < -32768 ? -32768 : pred > 32767 ? 32767 : pred;
                 s2[c] = s1[c];
-                s1[c] = pred;
-                delta[c] = (MS_ADAPT[nib] * delta[c]) >> 8;
-                if (delta[c] < 16) delta[c] = 16;
+                s1[c] = (int)pred;
+                int64_t nd = ((int64_t)MS_ADAPT[nib] * delta[c]) >> 8;
+                nd = nd < 16 ? 16 : nd > INT32_MAX / 768 ? INT32_MAX / 768 : nd;
+                delta[c] = (int)nd;
                 pcm->push_back((int16_t)pred);
                 c = c + 1 == ch ? 0 : c + 1;
             }
@@ -304,8 +308,9 @@ bool decode_wav(const std::vector<uint8_t>& f, std::vector<float>* out, uint32_t
 
 }  // namespace
 
-extern "C" int32_t sdsp_decode_audio_file(const char* path, float** samples, uint64_t* n_samples, uint32_t* sample_rate,
-                                          char* err, uint64_t errlen) {
+namespace {
+int32_t decode_audio_file(const char* path, float** samples, uint64_t* n_samples, uint32_t* sample_rate, char* err,
+                          uint64_t errlen) {
     if (err && errlen) err[0] = 0;
     if (!path || !samples || !n_samples || !sample_rate) return SDSP_ERR_INVALID_INPUT;
     *samples = nullptr;
@@ -363,6 +368,23 @@ extern "C" int32_t sdsp_decode_audio_file(const char* path, float** samples, uin
     *n_samples = mono.size();
     *sample_rate = sr;
     return SDSP_OK;
+}
+}  // namespace
+
+// No exception leaves the C ABI: sizes a damaged header declares can make an allocation fail
+// (std::bad_alloc / std::length_error) inside any of the decoders.
+extern "C" int32_t sdsp_decode_audio_file(const char* path, float** samples, uint64_t* n_samples, uint32_t* sample_rate,
+                                          char* err, uint64_t errlen) {
+    try {
+        return decode_audio_file(path, samples, n_samples, sample_rate, err, errlen);
+    } catch (const std::exception& e) {
+        fail(err, errlen, std::string("decoding failed: ") + e.what());
+    } catch (...) {
+        fail(err, errlen, "decoding failed");
+    }
+    if (samples) *samples = nullptr;
+    if (n_samples) *n_samples = 0;
+    return SDSP_ERR_DECODING;
 }
 
 extern "C" void sdsp_free_samples(float* samples) { std::free(samples); }

@@ -141,9 +141,12 @@ bool block_frames(const uint8_t* p, uint64_t n, uint64_t want_track, std::vector
         if (rest % (uint64_t)count) return false;
         for (int i = 0; i < count - 1; i++) sizes.push_back(rest / (uint64_t)count);
     }
+    // every laced size is checked against the bytes left, so the running sum cannot wrap
     uint64_t used = 0;
-    for (uint64_t s : sizes) used += s;
-    if (used > n - pos) return false;
+    for (uint64_t s : sizes) {
+        if (s > n - pos - used) return false;
+        used += s;
+    }
     sizes.push_back(n - pos - used);
     for (uint64_t s : sizes) {
         frames->emplace_back(p + pos, p + pos + s);

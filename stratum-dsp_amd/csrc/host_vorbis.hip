@@ -229,8 +229,11 @@ bool read_setup(LBits& b, Vorbis& v, std::string* err) {
             const float mn = float32_unpack(b.read(32)), dl = float32_unpack(b.read(32));
             const int vbits = (int)b.read(4) + 1;
             const bool seq = b.bit();
-            const uint32_t nval = c.lookup == 1 ? lookup1_values(c.entries, c.dims) : c.entries * c.dims;
-            if (c.dims == 0 || (uint64_t)nval > (1u << 24)) return fail(err, "malformed Vorbis codebook");
+            // sizes in 64 bits: entries (24 bits) x dims (16 bits) would wrap in 32
+            const uint64_t nvq = (uint64_t)c.entries * (uint64_t)c.dims;
+            if (c.dims == 0 || nvq > (1u << 24)) return fail(err, "malformed Vorbis codebook");
+            const uint32_t nval = c.lookup == 1 ? lookup1_values(c.entries, c.dims) : (uint32_t)nvq;
+            if (nval == 0 || nval > (1u << 24)) return fail(err, "malformed Vorbis codebook");
             std::vector<uint32_t> mult(nval);
             for (uint32_t i = 0; i < nval; i++) mult[i] = b.read(vbits);
             c.vq.assign((size_t)c.entries * c.dims, 0.0f);
@@ -279,6 +282,12 @@ bool read_setup(LBits& b, Vorbis& v, std::string* err) {
         f.X = {0, 1 << f.rangebits};
         for (int i = 0; i < f.partitions; i++)
             for (int j = 0; j < f.class_dim[(size_t)f.part_class[(size_t)i]]; j++) f.X.push_back((int)b.read(f.rangebits));
+        {
+            // Vorbis I §7.2.2: the X list may not repeat a value (the curve would divide by zero)
+            std::vector<int> xs = f.X;
+            std::sort(xs.begin(), xs.end());
+            if (std::adjacent_find(xs.begin(), xs.end()) != xs.end() || xs.size() > 65) return fail(err, "malformed Vorbis floor");
+        }
         for (int bk : f.class_master)
             if (bk >= nbooks) return fail(err, "malformed Vorbis floor");
         for (auto& sb : f.sub_books)
@@ -328,7 +337,11 @@ bool read_setup(LBits& b, Vorbis& v, std::string* err) {
         if (b.read(2) != 0) return fail(err, "malformed Vorbis mapping");
         m.mux.assign((size_t)v.channels, 0);
         if (m.submaps > 1)
-            for (int c = 0; c < v.channels; c++) m.mux[(size_t)c] = (int)b.read(4);
+            for (int c = 0; c < v.channels; c++) {
+                m.mux[(size_t)c] = (int)b.read(4);
+                // Vorbis I §4.2.4: a mux value past the submap count makes the stream undecodable
+                if (m.mux[(size_t)c] >= m.submaps) return fail(err, "malformed Vorbis mapping");
+            }
         for (int s = 0; s < m.submaps; s++) {
             b.read(8);
             m.sub_floor.push_back((int)b.read(8));
@@ -360,6 +373,7 @@ float inverse_db(int i) {
 }
 
 void render_line(int x0, int y0, int x1, int y1, std::vector<int>& v) {
+    if (x1 <= x0) return;  // setup parsing rejects repeated X values; a zero-width line draws nothing
     const int dy = y1 - y0, adx = x1 - x0;
     int ady = std::abs(dy);
     const int base = dy / adx;

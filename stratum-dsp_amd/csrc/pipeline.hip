@@ -2396,7 +2396,15 @@ int32_t run_locked(DeviceCtx& d, const float* d_samples, const uint64_t* offsets
     std::vector<uint64_t> off(offsets, offsets + n), ln(lens, lens + n);
     std::vector<TrackRes> res;
     Pipeline p(d, *cfg, sr, stages);
-    p.run(d_samples, off, ln, res);
+    try {
+        p.run(d_samples, off, ln, res);
+    } catch (...) {
+        // a sub-batch may have queued key-stream work (the late join) before a later one threw:
+        // nothing of this call may still run on the engine's streams once the context lock is
+        // released, or the next call's uploads into the same context buffers would race it
+        for (hipStream_t s : d.own) (void)hipStreamSynchronize(s);
+        throw;
+    }
     const float ms = (float)(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() /
                              (double)std::max<uint64_t>(n, 1));
     for (uint64_t i = 0; i < n; i++) fill_result(res[(size_t)i], sr, ms, &outs[i]);
@@ -2455,20 +2463,12 @@ void stage_release(DeviceStage* ds) {
     std::lock_guard<std::mutex> lk(g_stage_mu);
     (*g_stage_free)[ds->dev].push_back(ds);
 }
-// SDSP_DEVICE_LIST=a,b,... (test hook): the worker devices of sdsp_analyze_batch, repeats allowed
-// (two workers on device 0 exercise the multi-device chunk path on a one-GPU box)
+// test hook (sdsp_debug_set_test_hooks): the worker devices of sdsp_analyze_batch, repeats
+// allowed (two workers on device 0 exercise the multi-device chunk path on a one-GPU box)
 std::vector<int> device_list_override(int ndev) {
     std::vector<int> devs;
-    const char* e = std::getenv("SDSP_DEVICE_LIST");
-    if (!e) return devs;
-    for (const char* p = e; *p;) {
-        char* end = nullptr;
-        const long v = std::strtol(p, &end, 10);
-        if (end == p) break;
-        if (v >= 0 && v < ndev) devs.push_back((int)v);
-        p = *end == ',' ? end + 1 : end;
-        if (end == p && *p) break;
-    }
+    for (int v : test_hooks_devices())
+        if (v >= 0 && v < ndev) devs.push_back(v);
     return devs;
 }
 }  // namespace
@@ -2525,9 +2525,8 @@ int32_t sdsp_analyze_batch(const float* const* tracks, const uint64_t* lens, uin
     uint64_t max_tracks = 512;
     if (const char* e = std::getenv("SDSP_BATCH_CHUNK_TRACKS")) max_tracks = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
     const std::vector<uint64_t> cb = plan_chunks(lens, n_tracks, max_tracks, (uint64_t)2 << 30 /* 8 GB of f32 */);
-    // test hook: the chunk whose analysis throws (the per-chunk failure path)
-    const char* fe = std::getenv("SDSP_TEST_FAIL_CHUNK");
-    const long fail_chunk = fe ? std::atol(fe) : -1;
+    // test hook (sdsp_debug_set_test_hooks): the chunk whose analysis throws (the per-chunk failure path)
+    const long fail_chunk = test_hooks().fail_chunk.load();
     const size_t n_chunks = cb.size() - 1;
     // every result starts as an error; run_device overwrites the tracks it analyses
     auto mark_failed = [&](size_t c, const std::string& what) {
@@ -2570,7 +2569,7 @@ int32_t sdsp_analyze_batch(const float* const* tracks, const uint64_t* lens, uin
             SDSP_HIP_CHECK(hipEventRecord(sl.ready, ds->copy));
         };
         cd.analyze = [ds, &cb, lens, sample_rate, cfg, outs, fail_chunk](int s, size_t c) {
-            if ((long)c == fail_chunk) throw HipError("injected chunk failure (SDSP_TEST_FAIL_CHUNK)");
+            if ((long)c == fail_chunk) throw HipError("injected chunk failure (test hook)");
             const uint64_t a = cb[c], b = cb[c + 1];
             std::vector<uint64_t> off(b - a), ln(b - a);
             uint64_t tot = 0;
@@ -2583,8 +2582,14 @@ int32_t sdsp_analyze_batch(const float* const* tracks, const uint64_t* lens, uin
                        SDSP_STAGES_FULL, ds->slot[s].ready);
         };
         cd.drain = [ds]() {  // after a failed chunk: nothing may still read the slot it reuses
+            // the engine's own streams and this stage's copy stream, never the caller's streams
             SDSP_HIP_CHECK(hipSetDevice(ds->dev));
-            SDSP_HIP_CHECK(hipDeviceSynchronize());
+            DeviceCtx& c = device_ctx(ds->dev);
+            {
+                std::lock_guard<std::mutex> lk(c.mu);
+                for (hipStream_t s : c.own) SDSP_HIP_CHECK(hipStreamSynchronize(s));
+            }
+            if (ds->copy) SDSP_HIP_CHECK(hipStreamSynchronize(ds->copy));
         };
         cds.push_back(cd);
     }

@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "../../include/sdsp_fft_spec.h"
+#include "../../include/stratum_hip_debug.h"
 #include "kernels.hpp"
 #include "sdsp_runtime.hpp"
 
@@ -22,6 +23,16 @@ void note_alloc(size_t bytes) {
 
 static std::mutex g_ctx_mu;
 static std::map<int, std::unique_ptr<DeviceCtx>> g_ctx;
+
+TestHooks& test_hooks() {
+    static TestHooks h;
+    return h;
+}
+std::vector<int> test_hooks_devices() {
+    TestHooks& h = test_hooks();
+    std::lock_guard<std::mutex> lk(h.mu);
+    return h.devices;
+}
 
 DeviceCtx& device_ctx(int device) {
     std::lock_guard<std::mutex> lk(g_ctx_mu);
@@ -251,6 +262,18 @@ int32_t sdsp_last_stage_times(int32_t device, sdsp_stage_times* out) {
 // device-resident noise tracks of len samples each (one magnitude buffer, the pipeline's row
 // stride), HIP events on the launch stream.  Writes the mean launch time and the algorithmic
 // bytes per launch (4 N_in + 4 F (nfft/2+1) per track).
+// Test hooks (include/stratum_hip_debug.h).  The library reads no test switch from the
+// environment; a test sets these explicitly and resets them with (-1, NULL, 0, 0).
+int32_t sdsp_debug_set_test_hooks(int64_t fail_chunk, const int32_t* devices, uint32_t n_devices,
+                                  int32_t stft_frame_parallel) {
+    TestHooks& h = test_hooks();
+    h.fail_chunk.store((long)fail_chunk);
+    h.stft_frame_parallel.store(stft_frame_parallel != 0);
+    std::lock_guard<std::mutex> lk(h.mu);
+    h.devices.assign(devices ? devices : nullptr, devices ? devices + n_devices : nullptr);
+    return SDSP_OK;
+}
+
 // test probe: device allocations the engine has made so far (count, bytes)
 int32_t sdsp_debug_alloc_stats(uint64_t* n_allocs, uint64_t* bytes) {
     if (n_allocs) *n_allocs = g_alloc_n.load();
@@ -290,7 +313,7 @@ int32_t sdsp_probe_stft(int32_t device, uint64_t nfft, uint64_t hop, uint64_t n_
             o[t] = t * len;
             r0[t] = t * F;
         }
-        const bool frame_parallel = std::getenv("SDSP_STFT_FRAME_PARALLEL") != nullptr;  // A/B switch
+        const bool frame_parallel = test_hooks().stft_frame_parallel.load() != 0;  // test hook
         const std::vector<uint64_t> sp = stft_strips(pf);
         DevBuf strips, redo;
         strips.ensure(sp.size() * 8);
@@ -358,8 +381,8 @@ int32_t sdsp_debug_stft(const float* host_x, uint64_t n, uint64_t nfft, uint64_t
         strips.ensure(16);
         redo.ensure((frames + 1) * 4);
         SDSP_HIP_CHECK(hipMemcpy(strips.p, sp.data(), 16, hipMemcpyHostToDevice));
-        // SDSP_STFT_FRAME_PARALLEL=1: the frame-parallel kernel (k_stft_mag) for every hop
-        const bool frame_parallel = std::getenv("SDSP_STFT_FRAME_PARALLEL") != nullptr;
+        // test hook: the frame-parallel kernel (k_stft_mag) for every hop
+        const bool frame_parallel = test_hooks().stft_frame_parallel.load() != 0;
         SDSP_HIP_CHECK(hipMemcpy(x.p, host_x, n * 4, hipMemcpyHostToDevice));
         SDSP_HIP_CHECK(hipMemcpy(pfx.p, pf, 16, hipMemcpyHostToDevice));
         SDSP_HIP_CHECK(hipMemcpy(off.p, &o0, 8, hipMemcpyHostToDevice));

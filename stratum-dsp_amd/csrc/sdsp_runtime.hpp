@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -40,11 +41,11 @@ struct DevBuf {
     void ensure(size_t n) {
         if (n <= bytes) return;
         if (p) {
-            // work queued on the engine's streams may still read the old buffer
-            if (readers)
-                for (hipStream_t s : *readers) SDSP_HIP_CHECK(hipStreamSynchronize(s));
-            else
-                SDSP_HIP_CHECK(hipDeviceSynchronize());
+            // work queued on the engine's streams may still read the old buffer.  A buffer without
+            // readers belongs to one synchronous probe call and is sized once; growing it again
+            // would need a device-wide wait, which the engine never does
+            if (!readers) throw HipError("DevBuf: an unowned buffer cannot grow");
+            for (hipStream_t s : *readers) SDSP_HIP_CHECK(hipStreamSynchronize(s));
             SDSP_HIP_CHECK(hipFree(p));
         }
         p = nullptr;
@@ -95,6 +96,18 @@ struct DeviceCtx {
 };
 
 DeviceCtx& device_ctx(int device);
+
+// Test hooks, set only through sdsp_debug_set_test_hooks (never from the environment): an
+// injected chunk failure, a worker device list for sdsp_analyze_batch, and the frame-parallel
+// STFT kernel forced for every hop.
+struct TestHooks {
+    std::atomic<long> fail_chunk{-1};
+    std::atomic<int> stft_frame_parallel{0};
+    std::mutex mu;
+    std::vector<int> devices;
+};
+TestHooks& test_hooks();
+std::vector<int> test_hooks_devices();
 
 // STFT sizes with the tuned kernels (k_stft_mag / k_stft_slide: N = 2048, 8192).  Other powers of
 // two in [STFT_GEN_MIN, STFT_GEN_MAX], and N = 8192 with frame maxima, run the general kernel

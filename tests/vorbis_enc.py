@@ -353,7 +353,10 @@ def _residue_packet(w, rtype, qs, n2, psize):
                 BOOK_VQ.emit(w, int(a) + 32 + VQ_VALUES * (int(b) + 32))
 
 
-def headers(channels, rate, rtype):
+def headers(channels, rate, rtype, damage=None):
+    """damage (malformed setup headers for the decoder's rejection paths): "mux" = two submaps
+    with channel 0's mux equal to the submap count; "dup_x" = floor 0's X list repeats a value;
+    "big_dims" = an extra lookup-type-2 book whose entries x dims is 2^32 (0 in 32 bits)."""
     idh = LBitWriter()
     idh.put(0, 32)
     idh.put(channels, 8)
@@ -373,13 +376,27 @@ def headers(channels, rate, rtype):
     cw.put(1, 1)
     comment = b"\x03vorbis" + cw.bytes()
     s = LBitWriter()
-    s.put(len(BOOKS) - 1, 8)
+    s.put(len(BOOKS) - 1 + (damage == "big_dims"), 8)
     for b in BOOKS:
         b.write_header(s)
+    if damage == "big_dims":  # 2^17 entries of 17 bits (a complete tree, ordered) x 32768 dimensions
+        s.put(0x564342, 24)
+        s.put(32768, 16)
+        s.put(1 << 17, 24)
+        s.put(1, 1)  # ordered: one run of 2^17 lengths of 17
+        s.put(16, 5)
+        s.put(1 << 17, 18)
+        s.put(2, 4)
+        s.put(float32_pack(0.0), 32)
+        s.put(float32_pack(1.0), 32)
+        s.put(0, 4)
+        s.put(0, 1)
     s.put(0, 6)
     s.put(0, 16)
     s.put(len(FLOORS) - 1, 6)
-    for f in FLOORS:
+    for i, f in enumerate(FLOORS):
+        if damage == "dup_x" and i == 0:
+            f = FloorSpec(f.rangebits, [f.X[2], f.X[2]] + f.X[4:])
         _write_floor(s, f)
     s.put(1, 6)  # 2 residues: short, long
     for n2, psize in [(128, 16), (1024, 32)]:
@@ -397,7 +414,9 @@ def headers(channels, rate, rtype):
     s.put(1, 6)  # 2 mappings
     for m in range(2):
         s.put(0, 16)
-        s.put(0, 1)  # one submap
+        s.put(int(damage == "mux"), 1)  # one submap (two with the "mux" damage)
+        if damage == "mux":
+            s.put(1, 4)
         if channels == 2:
             s.put(1, 1)
             s.put(0, 8)
@@ -406,6 +425,12 @@ def headers(channels, rate, rtype):
         else:
             s.put(0, 1)
         s.put(0, 2)
+        if damage == "mux":
+            for c in range(channels):
+                s.put(2 if c == 0 else 0, 4)  # channel 0 names submap 2 of {0, 1}
+            s.put(0, 8)
+            s.put(m, 8)
+            s.put(m, 8)
         s.put(0, 8)
         s.put(m, 8)  # floor
         s.put(m, 8)  # residue
