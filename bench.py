@@ -242,6 +242,13 @@ def main():
     eng.synchronize()
     barrier()
     dt = max_over_ranks(time.perf_counter() - t0, tdist)
+    # every rank's shard (rank, tracks, first seed), gathered for the report: the ranks' tracks
+    # must be disjoint and sum to the job's batch (config 3: 8 x 1024 = 8192)
+    shard = {"rank": rank, "tracks": n, "seed0": seed0}
+    shards = [shard]
+    if tdist is not None:
+        shards = [None] * world
+        tdist.all_gather_object(shards, shard)
     n_err = sum(1 for st in res.status if st != 0)
     total_tracks = n * world * args.steps
     value = total_tracks / dt
@@ -337,6 +344,8 @@ def main():
                 "bpm_mode": bpm_mode,
                 "stages": "bpm-only (a1-a19)" if stage_mask == 1 else "full",
                 "parallelism": f"track-sharded x{world} (no collectives)",
+                "tracks_per_step_all_ranks": sum(x["tracks"] for x in shards),
+                "shards": shards,
             },
             "errors": n_err,
             "stage_ms_last_step": {k: round(v, 3) for k, v in stages.items() if k.endswith("_ms")},
@@ -350,14 +359,20 @@ def main():
         tdist.destroy_process_group()
 
 
-def isolated_stft(nfft, hop, length, tracks=32, reps=3):
+def isolated_stft(nfft, hop, length, tracks=256, reps=3):
     """sdsp_probe_stft: `reps` launches of the STFT kernel alone over `tracks` device-resident
-    noise tracks of `length` samples, HIP events on its stream."""
+    noise tracks of `length` samples, HIP events on its stream.  256 3-min tracks are 62k
+    workgroups of the 8192-point kernel (80 per workgroup slot of the chip), so the launch measures
+    the kernel and not its grid's tail; fewer when the device's free memory cannot hold them."""
     import ctypes as C
 
     if length < nfft:
         return None
     L = sdsp.lib()
+    free = sdsp.device_mem_info(0)[0]
+    frames = (length - nfft) // hop + 1
+    per_track = 4 * length + 4 * frames * (4160 if nfft == 8192 else 1028) + 4 * frames
+    tracks = int(max(8, min(tracks, 0.8 * free // per_track)))
     f = L.sdsp_probe_stft
     f.argtypes = [C.c_int32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int32, C.c_int32,
                   C.POINTER(C.c_double), C.POINTER(C.c_double)]

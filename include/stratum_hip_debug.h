@@ -25,6 +25,9 @@ extern "C" {
 int32_t sdsp_debug_set_test_hooks(int64_t fail_chunk, const int32_t* devices, uint32_t n_devices,
                                   int32_t stft_frame_parallel);
 
+/* Free and total HBM bytes of `device` (the benchmark sizes its kernel probe by them). */
+int32_t sdsp_debug_mem_info(int32_t device, uint64_t* free_bytes, uint64_t* total_bytes);
+
 /* Device allocations the engine has made so far (count, bytes): "a repeated call allocates nothing". */
 int32_t sdsp_debug_alloc_stats(uint64_t* n_allocs, uint64_t* bytes);
 

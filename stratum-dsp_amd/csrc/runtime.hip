@@ -274,6 +274,19 @@ int32_t sdsp_debug_set_test_hooks(int64_t fail_chunk, const int32_t* devices, ui
     return SDSP_OK;
 }
 
+int32_t sdsp_debug_mem_info(int32_t device, uint64_t* free_bytes, uint64_t* total_bytes) {
+    try {
+        SDSP_HIP_CHECK(hipSetDevice(device));
+        size_t fr = 0, to = 0;
+        SDSP_HIP_CHECK(hipMemGetInfo(&fr, &to));
+        if (free_bytes) *free_bytes = fr;
+        if (total_bytes) *total_bytes = to;
+        return SDSP_OK;
+    } catch (const std::exception&) {
+        return SDSP_ERR_PROCESSING;
+    }
+}
+
 // test probe: device allocations the engine has made so far (count, bytes)
 int32_t sdsp_debug_alloc_stats(uint64_t* n_allocs, uint64_t* bytes) {
     if (n_allocs) *n_allocs = g_alloc_n.load();

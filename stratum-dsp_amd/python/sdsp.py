@@ -92,6 +92,18 @@ def _fp(a):
     return a.ctypes.data_as(C.POINTER(C.c_float))
 
 
+def device_mem_info(device=0):
+    """(free, total) bytes of HBM on `device` (sdsp_debug_mem_info)."""
+    L = lib()
+    f = L.sdsp_debug_mem_info
+    f.argtypes = [C.c_int32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+    f.restype = C.c_int32
+    fr, to = C.c_uint64(), C.c_uint64()
+    if f(device, C.byref(fr), C.byref(to)) != 0:
+        raise RuntimeError("sdsp_debug_mem_info failed")
+    return fr.value, to.value
+
+
 @contextlib.contextmanager
 def test_hooks(fail_chunk=-1, devices=(), stft_frame_parallel=False):
     """Sets the library's test hooks (include/stratum_hip_debug.h, sdsp_debug_set_test_hooks)

@@ -132,3 +132,18 @@ def test_bench_spawns_eight_ranks_without_torchrun():
     assert d["n_gpus"] == 8 and d["config"]["parallelism"].startswith("track-sharded x8")
     assert d["config"]["baseline_config"] == 3
     assert abs(d["value"] - 2 * 8 / (d["ms_per_step"] / 1000.0)) / d["value"] < 1e-2
+
+
+def test_bench_eight_ranks_config3_shards():
+    """Config 3 rehearsed on the CPU (BASELINE.json: 8192 tracks over 8 GPUs): the rank-0 line says
+    n_gpus 8 and baseline config 3, and its per-rank shards are 8 disjoint seed ranges of 1024
+    tracks, 8192 in all."""
+    d = _bench_json([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--steps", "1", "--warmup", "0",
+                     "--seconds", "1", "--dry-run"])
+    c = d["config"]
+    assert d["n_gpus"] == 8 and c["baseline_config"] == 3 and c["tracks_per_gpu"] == 1024
+    sh = sorted(c["shards"], key=lambda x: x["rank"])
+    assert [x["rank"] for x in sh] == list(range(8)) and all(x["tracks"] == 1024 for x in sh)
+    assert c["tracks_per_step_all_ranks"] == 8192 == sum(x["tracks"] for x in sh)
+    ranges = sorted((x["seed0"], x["seed0"] + x["tracks"]) for x in sh)
+    assert all(a[1] <= b[0] for a, b in zip(ranges, ranges[1:]))  # disjoint

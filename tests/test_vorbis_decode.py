@@ -9,6 +9,8 @@ its defining sum, the windows, the overlap-add), so the check covers the bitstre
 and the transform to within float32 rounding.  The decoded signal must also track the encoded
 one (a lossy codec: a loose bound).  Parity against symphonia itself is unpinned.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -114,3 +116,24 @@ def test_vorbis_malformed_setup_rejected(tmp_path, damage):
     with pytest.raises(sdsp.AnalysisError) as e:
         _decode(tmp_path, ve.ogg_stream(hdr, pk, gr))
     assert e.value.kind == "DecodingError" and "Vorbis" in str(e.value), str(e.value)
+
+
+REAL_OGG = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "real_libvorbis_keypress.ogg")
+
+
+def test_vorbis_real_libvorbis_stream():
+    """A stream from a real encoder (tests/golden/real_libvorbis_keypress.ogg: MathJax's
+    a11y/invalid_keypress.ogg, Apache-2.0, vendor string "Xiph.Org libVorbis I 20070622"): its
+    codebooks, floors, residues and block switching are libvorbis's, not tests/vorbis_enc.py's.
+    No reference decode ships with it, so the checks are properties of a correct decode: the
+    stream's length and rate, a smooth waveform (a misdecoded floor, residue or window shows as a
+    click at a block edge), the 156 Hz buzz the file holds, then silence."""
+    x, sr = sdsp.decode_audio_file(REAL_OGG)
+    assert sr == 44100 and len(x) == 22050
+    assert np.all(np.isfinite(x)) and 0.3 < float(np.max(np.abs(x))) < 1.0
+    assert float(np.max(np.abs(np.diff(x)))) < 0.05
+    spec = np.abs(np.fft.rfft(x * np.hanning(len(x))))
+    f0 = float(np.fft.rfftfreq(len(x), 1.0 / sr)[np.argmax(spec)])
+    assert abs(f0 - 156.0) < 4.0, f0
+    head, tail = x[:8192], x[12288:]
+    assert float(np.sqrt(np.mean(head ** 2))) > 0.1 and float(np.sqrt(np.mean(tail ** 2))) < 1e-3

@@ -31,7 +31,14 @@ def probe(path, nfft, hop, tracks, seconds=180.0, reps=3, stride=0):
 
 
 if __name__ == "__main__":
+    # SDSP_PROBE_TRACKS: tracks per launch (default 320 for 8192, 1024 for 2048: both fill the chip
+    # many times over); SDSP_PROBE_ROUNDS: alternate the libraries this many times
     libs = sys.argv[1:] or [LIB]
-    for lib in libs:
-        for nfft, hop, n in ((8192, 512, 128), (2048, 512, 256)):
-            print(json.dumps(probe(lib, nfft, hop, n)), flush=True)
+    n8 = int(os.environ.get("SDSP_PROBE_TRACKS", "320"))
+    rounds = int(os.environ.get("SDSP_PROBE_ROUNDS", "1"))
+    only = os.environ.get("SDSP_PROBE_SIZES", "8192,2048").split(",")
+    for _ in range(rounds):
+        for lib in libs:
+            for nfft, hop, n in ((8192, 512, n8), (2048, 512, 4 * n8)):
+                if str(nfft) in only:
+                    print(json.dumps(probe(lib, nfft, hop, n)), flush=True)
