@@ -184,6 +184,7 @@ def main():
     ap.add_argument("--cpu-tracks", type=int, default=0, help="0 = 2 per thread")
     ap.add_argument("--cpu-1thread-tracks", type=int, default=2, help="tracks timed alone on one thread")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-probe", action="store_true", help="skip the isolated STFT probe (A/B runs)")
     ap.add_argument("--bpm-mode", type=int, default=-1, help="synthetic BPM mix (-1 = the workload's; 1 = config 5)")
     ap.add_argument("--dry-run", action="store_true", help="host-logic rehearsal without a GPU (tests)")
     args = ap.parse_args()
@@ -273,7 +274,7 @@ def main():
             traffic = round(ratio * bytes_per_launch)
     roofline = {
         "bound": "hbm",
-        "kernel": "k_stft_slide8 (key STFT, 8192/512)" if key_k else "k_stft_slide<2048> (tempo STFT, 2048/512)",
+        "kernel": "k_stft_slide8w3 (key STFT, 8192/512)" if key_k else "k_stft_slide2s (tempo STFT, 2048/512)",
         "achieved": round(achieved, 2),
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
@@ -287,7 +288,7 @@ def main():
         if (stft["ms2"] + stft["ms8"]) > 0 else None,
     }
 
-    if not args.dry_run and rank == 0:
+    if not args.dry_run and rank == 0 and not args.no_probe:
         # the same kernel launched alone (nothing else on the chip): the kernel's own bandwidth, as
         # opposed to `achieved` above, which is measured inside the two-stream pipeline where the
         # tempo path shares the CUs (tools/stft_probe.py)
@@ -382,7 +383,7 @@ def isolated_stft(nfft, hop, length, tracks=256, reps=3):
     if f(0, nfft, hop, tracks, length, reps, stride, C.byref(ms), C.byref(by)) != 0:
         return None
     gbs = by.value / (ms.value * 1e-3) / 1e9
-    return {"kernel": "k_stft_slide8" if nfft == 8192 else f"k_stft_slide<{nfft}>", "tracks": tracks, "ms_per_launch": round(ms.value, 3),
+    return {"kernel": "k_stft_slide8w3" if nfft == 8192 else "k_stft_slide2s", "tracks": tracks, "ms_per_launch": round(ms.value, 3),
             "ms_per_track": round(ms.value / tracks, 5), "achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
             "method": "sdsp_probe_stft: the kernel launched alone on device-resident noise tracks of the workload's "
                       "length, HIP events, mean of 3 launches"}

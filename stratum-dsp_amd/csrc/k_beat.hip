@@ -89,9 +89,9 @@ __device__ int hmm_track(float bpm, const float* on, int n, float* out, int cap,
     return nb;
 }
 
-// Stable ascending sort of a[0..n) (the reference's sort_by(partial_cmp) on NaN-free data):
-// bitonic over (value, index) keys in LDS, the index breaking ties.  n <= 2*cap_pow2 slots.
-__device__ void wave_sort_stable(float* a, int n, float* kv, int* ki, int npow2) {
+// Stable ascending sort of a[0..n) into dst[0..n) (the reference's sort_by(partial_cmp) on NaN-free
+// data): bitonic over (value, index) keys in LDS, the index breaking ties.  n <= 2*cap_pow2 slots.
+__device__ void wave_sort_stable(const float* a, float* dst, int n, float* kv, int* ki, int npow2) {
     const int lane = threadIdx.x & 63;
     for (int i = lane; i < npow2; i += 64) {
         kv[i] = i < n ? a[i] : SD_INF_F;
@@ -118,7 +118,7 @@ __device__ void wave_sort_stable(float* a, int n, float* kv, int* ki, int npow2)
             __syncthreads();
         }
     }
-    for (int i = lane; i < n; i += 64) a[i] = kv[i];
+    for (int i = lane; i < n; i += 64) dst[i] = kv[i];
     __syncthreads();
 }
 
@@ -326,8 +326,14 @@ __device__ float score_ts(const float* b, int nb, int bpb, float mean, int n_iv)
     return sd_minf(ac * 0.7f + cons * 0.3f, 1.0f);
 }
 
-constexpr int BEAT_LDS_ON = 8192;   // onsets staged in LDS up to this count
-constexpr int BEAT_SORT_MAX = 2048;  // LDS bitonic sort capacity (larger: serial merge sort)
+// LDS: 32 KB per one-wave workgroup, so k_beat fits on a CU beside the key stream's STFT.  Every
+// list the kernel walks sequentially lives in LDS when it fits (a dependent global load costs
+// microseconds on a chip whose HBM the key stream saturates; an LDS load ~100 cycles):
+constexpr int BEAT_LDS_ON = 4096;    // onsets (then, after the segment loop, the sort keys)
+constexpr int BEAT_LDS_B = 2048;     // HMM beats, when the HMM grid has at most this many frames
+constexpr int BEAT_SORT_MAX = 2048;  // LDS bitonic sort capacity (larger: serial merge sort); the
+                                     // sorted refined beats stay in LDS
+static_assert(BEAT_SORT_MAX * 8 <= BEAT_LDS_ON * 4, "sort keys alias the onset buffer");
 
 __global__ __launch_bounds__(64) void k_beat(const int* __restrict__ tracks, int n_items,
                                              const uint32_t* __restrict__ onsets, const uint64_t* __restrict__ on_off,
@@ -338,8 +344,10 @@ __global__ __launch_bounds__(64) void k_beat(const int* __restrict__ tracks, int
                                              float* __restrict__ downs, BeatOut* __restrict__ out) {
     SDSP_LATENCY_CRITICAL();
     __shared__ float s_on[BEAT_LDS_ON];
-    __shared__ float s_kv[BEAT_SORT_MAX];
-    __shared__ int s_ki[BEAT_SORT_MAX];
+    __shared__ float s_hb[BEAT_LDS_B];
+    __shared__ float s_rb[BEAT_SORT_MAX];
+    float* const s_kv = s_on;  // the onsets are not read after the segment loop
+    int* const s_ki = reinterpret_cast<int*>(s_on + BEAT_SORT_MAX);
     const int it = blockIdx.x;
     const int lane = threadIdx.x;
     const int trk = tracks[it];
@@ -371,6 +379,12 @@ __global__ __launch_bounds__(64) void k_beat(const int* __restrict__ tracks, int
     for (int k = lane; k < n; k += 64) onp[k] = (float)os[k] / (float)sr;
     __syncthreads();
     // (already ascending; the reference's sort_by(partial_cmp) is a no-op here)
+    {
+        // the HMM grid's frame count (hmm_track's nf) bounds its beats: LDS when it fits
+        const float interval = 60.0f / bpm;
+        const uint64_t nfr = sd_f2u64(__builtin_ceilf((onp[n - 1] - onp[0]) / interval)) + 1;
+        if (bpm > EPS && nfr <= (uint64_t)BEAT_LDS_B) hb = s_hb;
+    }
     int nh = hmm_track(bpm, onp, n, hb, cap, &overflow);
     __syncthreads();
     if (nh <= 0 || overflow) {
@@ -433,12 +447,13 @@ __global__ __launch_bounds__(64) void k_beat(const int* __restrict__ tracks, int
             int np2 = 1;
             while (np2 < nr) np2 <<= 1;
             if (np2 <= BEAT_SORT_MAX) {
-                wave_sort_stable(rb, nr, s_kv, s_ki, np2);
+                wave_sort_stable(rb, s_rb, nr, s_kv, s_ki, np2);
+                fin = s_rb;
             } else {
                 if (lane == 0) merge_sort_f(rb, tmp, nr);
                 __syncthreads();
+                fin = rb;
             }
-            fin = rb;
             nfin = nr;
         }
     }
@@ -477,10 +492,11 @@ __global__ __launch_bounds__(64) void k_beat(const int* __restrict__ tracks, int
         const float bi = 60.0f / bpm;
         const float bar = bi * (float)bpb;
         const float tolb = bar * 0.1f;
-        od[nd++] = fin[0];
+        float last = fin[0];
+        od[nd++] = last;
         for (int k = 1; k < nfin; k++) {
-            const float et = od[nd - 1] + bar;
-            if (sd_absf(fin[k] - et) <= tolb) od[nd++] = fin[k];
+            const float et = last + bar;
+            if (sd_absf(fin[k] - et) <= tolb) od[nd++] = last = fin[k];
         }
         // stability (mod.rs:425-485)
         float stab = 0.0f;

@@ -184,6 +184,99 @@ __global__ __launch_bounds__(MASK_T) void k_mask_r(float* __restrict__ mags, int
     }
 }
 
+// k_mask_rp: k_mask_r for the default HPCP path, which reads the masked spectrogram only on its
+// peak band [st_lo, st_hi] (extractor.rs:583-671: peaks in [pk_lo, pk_hi] and their neighbours)
+// and otherwise only folds the frame energy sum(x * x) over every bin (extractor.rs:1133).  The
+// masked value is stored only on that band; for every frame the workgroup's 64 bins (block g) fold
+// their squares in bin order into part[g][frame] (an LDS tile: lane = bin writes, then lane u folds
+// the row of frame base + u - M), and HPCP folds the 65 block sums in block order.  Only that fold's
+// association differs from the reference's one sequential sum over 4,097 bins (a GPU-only
+// re-association of the key energies); every masked value is bit-identical.
+// Lanes past the last bin stay in the wave and contribute +0 (exact: the sums are >= +0).
+template <int M, int PW>
+__global__ __launch_bounds__(MASK_T) void k_mask_rp(float* __restrict__ mags, int stride, int B,
+                                                     const uint64_t* __restrict__ frame_pfx,
+                                                     const int* __restrict__ tracks, int blocks_per_track,
+                                                     float power, int st_lo, int st_hi, float* __restrict__ part,
+                                                     uint64_t total) {
+    constexpr int R = 2 * M + 2, RX = M + 1;
+    static_assert(M >= 1 && 2 * M + 1 <= 25 && R <= MASK_T, "fast window division validated for 3..25");
+    __shared__ float tile[R][MASK_T + 1];
+    const int it = blockIdx.x / blocks_per_track;
+    const int trk = tracks[it];
+    const int gblk = blockIdx.x % blocks_per_track;
+    const int lane = threadIdx.x;
+    const int b = gblk * MASK_T + lane;
+    const int64_t F = (int64_t)(frame_pfx[trk + 1] - frame_pfx[trk]);
+    if (F <= 0) return;  // the whole workgroup
+    const bool live = b < B;
+    const bool keep = live && b >= st_lo && b <= st_hi;
+    float* col = mags + frame_pfx[trk] * (uint64_t)stride + (live ? b : 0);
+    float* pg = part + (uint64_t)gblk * total + frame_pfx[trk];
+    const float p = sd_maxf(power, 1.0f);
+    const float inv_w = 1.0f / (float)(2 * M + 1);
+    float P[R], X[RX];
+#pragma unroll
+    for (int j = 0; j < R; j++) P[j] = 0.0f;
+#pragma unroll
+    for (int j = 0; j < RX; j++) X[j] = 0.0f;
+    float prev = 0.0f;
+    auto emit = [&](float a, int64_t den, float xr, int64_t t, int u) {
+        const float v = mask_elem<M, PW>(a, den, xr, p, inv_w);
+        if (keep) __builtin_nontemporal_store(v, &col[t * stride]);
+        tile[u][lane] = live ? v * v : 0.0f;
+    };
+    // the block's partial sums: lane u folds the 64 squares of frame base + u - M in bin order
+    auto fold = [&](int64_t base) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int64_t t = base + lane - M;
+        if (lane < R && t >= 0 && t < F) {
+            float sum = 0.0f;
+#pragma unroll 16
+            for (int j = 0; j < MASK_T; j++) sum += tile[lane][j];
+            pg[t] = sum;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    for (int64_t base = 0; base < F + M; base += R) {
+        float xv[R];
+        if (base >= 2 * M && base + R <= F) {
+#pragma unroll
+            for (int u = 0; u < R; u++) xv[u] = live ? __builtin_nontemporal_load(&col[(base + u) * stride]) : 0.0f;
+#pragma unroll
+            for (int u = 0; u < R; u++) {
+                prev = prev + xv[u];
+                P[(u + 1) % R] = prev;
+                X[u % RX] = xv[u];
+                emit(P[(u + 1) % R] - P[(u + R - 2 * M) % R], 2 * M + 1, X[(u + 1) % RX], base + u - M, u);
+            }
+            fold(base);
+            continue;
+        }
+#pragma unroll
+        for (int u = 0; u < R; u++)
+            xv[u] = (live && base + u < F) ? __builtin_nontemporal_load(&col[(base + u) * stride]) : 0.0f;
+#pragma unroll
+        for (int u = 0; u < R; u++) {
+            const int64_t tin = base + u;
+            prev = prev + xv[u];
+            P[(u + 1) % R] = prev;
+            X[u % RX] = xv[u];
+            const int64_t t = tin - M;
+            if (t >= 0 && t < F) {
+                const int64_t st = t >= M ? t - M : 0;
+                const int64_t en = t + M + 1 < F ? t + M + 1 : F;
+                emit(P[(u + 1) % R] - P[(u + R - 2 * M) % R], en - st, X[(u + 1) % RX], t, u);
+            }
+        }
+        fold(base);
+    }
+}
+
 // ----------------------------------------------------------------------------------------
 constexpr int HP_CW = 16;  // bins per staged chunk (LDS row stride 17: conflict-free)
 
@@ -207,11 +300,12 @@ struct HpcpFrame {
         }
     }
     // bins c0 .. c0+cw-1 of this frame, row[j] = m[c0 + j], in bin order
+    template <bool ENERGY = true>
     __device__ __forceinline__ void walk(const float* row, int c0, int cw, const HpcpParams& P) {
         for (int j = 0; j < cw; j++) {
             const int b = c0 + j;
             const float m = row[j];
-            e += m * m;
+            if (ENERGY) e += m * m;
             const int c = b - 1;  // candidate peak bin, needs m[c-1] = m2, m[c] = m1, m[c+1] = m
             if (c >= P.pk_lo && c <= P.pk_hi && !(m1 <= m2 || m1 < m) && m1 > thr) {
                 // insertion into the descending list: gt[q] = m1 > pm[q] is false then true along
@@ -325,6 +419,65 @@ __global__ __launch_bounds__(HP_FRAMES) SDSP_HPCP_ATTR void k_hpcp(const float* 
     // pitch-class accumulators reuse the staging tile (every read of it is done)
     __syncthreads();
     static_assert(sizeof(tile) >= sizeof(float) * 12 * HP_FRAMES, "pc fits the staging tile");
+    if (!valid) return;
+    hf.finish(reinterpret_cast<float(*)[HP_FRAMES]>(&tile[0][0]), i, P, harm, chroma, energy, g0 + (uint64_t)f);
+}
+
+// k_hpcp_band: k_hpcp after k_mask_rp.  The frame energy folds the 65 block sums part[g][frame] in
+// block order; the bin walk covers only the band k_mask_rp stored, [pk_lo - 1, pk_hi + 1] (the
+// local-maximum test of candidate c reads bins c - 1 .. c + 1; starting the walk at pk_lo - 1 with
+// the walk's zero history gives exactly k_hpcp's candidates).
+template <int KCAP>
+__global__ __launch_bounds__(HP_FRAMES) SDSP_HPCP_ATTR void k_hpcp_band(const float* __restrict__ mags,
+                                                         const uint64_t* __restrict__ frame_pfx,
+                                                         const uint64_t* __restrict__ tile_pfx,
+                                                         const int* __restrict__ tracks, int n_items, HpcpParams P,
+                                                         const HarmEntry* __restrict__ harm,
+                                                         const float* __restrict__ part, int n_blocks, uint64_t total,
+                                                         float* __restrict__ chroma, float* __restrict__ energy) {
+    __shared__ float tile[HP_FRAMES][HP_CW + 1];
+    const uint64_t gb = blockIdx.x;
+    const int it = find_track(tile_pfx, n_items, gb);
+    const int trk = tracks[it];
+    const int64_t F = (int64_t)(frame_pfx[trk + 1] - frame_pfx[trk]);
+    const int64_t f0 = (int64_t)(gb - tile_pfx[it]) * HP_FRAMES;
+    const int i = threadIdx.x;
+    const int64_t f = f0 + i;
+    const bool valid = f < F;
+    const uint64_t g0 = frame_pfx[trk];
+    HpcpFrame<KCAP> hf;
+    hf.init();
+    if (valid) {
+        const float* pp = part + g0 + (uint64_t)f;
+        float e = 0.0f;
+        for (int g = 0; g < n_blocks; g++) e += pp[(uint64_t)g * total];
+        hf.e = e;
+    }
+    const int sub = i / HP_CW, jj = i % HP_CW;
+    const int64_t rows = F - f0 < HP_FRAMES ? F - f0 : HP_FRAMES;
+    constexpr int NLD = HP_CW;
+    constexpr int RSTEP = HP_FRAMES / HP_CW;
+    const float* rowp = mags + (g0 + (uint64_t)f0 + (uint64_t)sub) * (uint64_t)P.stride + jj;
+    const uint64_t rstride = (uint64_t)RSTEP * (uint64_t)P.stride;
+    const int w_lo = P.pk_lo - 1 > 0 ? P.pk_lo - 1 : 0, w_hi = P.pk_hi + 1 < P.B - 1 ? P.pk_hi + 1 : P.B - 1;
+    float nx[NLD];
+    auto load_chunk = [&](int c0) {
+        const bool col_ok = c0 + jj <= w_hi;
+#pragma unroll
+        for (int u = 0; u < NLD; u++)
+            nx[u] = (sub + u * RSTEP < rows && col_ok) ? rowp[(uint64_t)u * rstride + c0] : 0.0f;
+    };
+    if (w_lo <= w_hi) load_chunk(w_lo);
+    for (int c0 = w_lo; c0 <= w_hi; c0 += HP_CW) {
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < NLD; u++) tile[sub + u * RSTEP][jj] = nx[u];
+        __syncthreads();
+        if (c0 + HP_CW <= w_hi) load_chunk(c0 + HP_CW);
+        if (!valid) continue;
+        hf.template walk<false>(tile[i], c0, w_hi + 1 - c0 < HP_CW ? w_hi + 1 - c0 : HP_CW, P);
+    }
+    __syncthreads();
     if (!valid) return;
     hf.finish(reinterpret_cast<float(*)[HP_FRAMES]>(&tile[0][0]), i, P, harm, chroma, energy, g0 + (uint64_t)f);
 }
@@ -922,6 +1075,33 @@ void launch_mask(float* mags, int stride, int B, const uint64_t* frame_pfx, cons
     else
         hipLaunchKernelGGL(k_mask<0>, dim3(n_items * bpt), dim3(MASK_T), lds, st, mags, stride, B, frame_pfx, tracks,
                            bpt, margin, power, 0);
+}
+bool mask_band_ok(int margin, float power) { return margin == 12 && sd_maxf(power, 1.0f) == 2.0f; }
+void launch_mask_band(float* mags, int stride, int B, const uint64_t* frame_pfx, const int* tracks, int n_items,
+                      float power, int st_lo, int st_hi, float* part, uint64_t total, hipStream_t st) {
+    if (n_items == 0) return;
+    const int bpt = (B + MASK_T - 1) / MASK_T;
+    hipLaunchKernelGGL((k_mask_rp<12, 2>), dim3(n_items * bpt), dim3(MASK_T), 0, st, mags, stride, B, frame_pfx, tracks,
+                       bpt, power, st_lo, st_hi, part, total);
+}
+void launch_hpcp_band(const float* mags, const uint64_t* frame_pfx, const uint64_t* tile_pfx, const int* tracks,
+                      int n_items, uint64_t n_tiles, const HpcpParams& P, const HarmEntry* harm, const float* part,
+                      uint64_t total, float* chroma, float* energy, hipStream_t st) {
+    if (n_tiles == 0) return;
+    const int nblk = (P.B + MASK_T - 1) / MASK_T;
+    const dim3 grid((unsigned)n_tiles), block(HP_FRAMES);
+#define SDSP_HB(K)                                                                                                   \
+    hipLaunchKernelGGL(k_hpcp_band<K>, grid, block, 0, st, mags, frame_pfx, tile_pfx, tracks, n_items, P, harm, part, \
+                       nblk, total, chroma, energy)
+    if (P.K <= 8)
+        SDSP_HB(8);
+    else if (P.K <= 16)
+        SDSP_HB(16);
+    else if (P.K <= 24)
+        SDSP_HB(24);
+    else
+        SDSP_HB(HP_KMAX);
+#undef SDSP_HB
 }
 void launch_hpcp(const float* mags, const uint64_t* frame_pfx, const uint64_t* tile_pfx, const int* tracks,
                  int n_items, uint64_t n_tiles, const HpcpParams& P, const HarmEntry* harm, float* chroma,

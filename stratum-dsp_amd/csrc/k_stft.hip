@@ -762,6 +762,165 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 }
 
 // ---------------------------------------------------------------------------------------------
+// k_stft_slide2s: the sliding strip for N = 2048 (M = 1024, one wave per strip, 4 strips per
+// workgroup) with ONE frame buffer per strip and the pass-2 / post twiddles in LDS, for 3 waves
+// per SIMD (k_stft_slide<2048>: two buffers per strip, 227 VGPRs, 2 waves).  Pass 2 runs in place:
+// a thread reads its 16 slots and writes its 16 results back into them (a wave's LDS operations
+// run in issue order, so no barrier), so z[q + 256 pp + 16 k] lives where x[q + 16 pp + 64 k] was
+// read, and the trailing radix-4 reads column c, Z[c + 256 j], from (c % 16) + 68 (c / 16) + 17 j.
+// Same arithmetic as k_stft_slide (bit-identical magnitudes and frame maxima).
+template <int S, bool FRAME_MAX>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_stft_slide2s(
+    const float* __restrict__ samples, const uint64_t* __restrict__ frame_pfx, const uint64_t* __restrict__ strip_pfx,
+    int n_tracks, uint64_t n_strips, const uint64_t* __restrict__ src_off, const float* __restrict__ gain, int hop,
+    const float* __restrict__ window, const cx* __restrict__ twp, const cx* __restrict__ rtp, float* __restrict__ mags,
+    const uint64_t* __restrict__ mag_row0, int stride, float* __restrict__ frame_max, uint32_t* __restrict__ redo) {
+    constexpr int M = 1024, TPF = 64, FPB = 4;
+    constexpr int PADM = M + PADSHIFT * M / 16;  // 1088 slots
+    static_assert(S >= 1 && S <= 16, "hop = S * 128");
+    __shared__ c2 lds[FPB * PADM];
+    __shared__ __attribute__((aligned(16))) c2 tw2s[4 * 16];  // [p'][j], j < 15
+    __shared__ c2 wks[8 * TPF];                                // [slot j][lane]
+
+    const int lt = threadIdx.x % TPF;
+    const int fl = threadIdx.x / TPF;
+    const __amdgpu_buffer_rsrc_t rtw = rsrc_of(twp, 8u * 15u * (TPF + TPF / 16 + 1));
+    const __amdgpu_buffer_rsrc_t rrt = rsrc_of(rtp, 8u * (slide_rt_base<M>() + 8 * TPF + 1));
+    // the workgroup's tables (every wave of the workgroup reaches this barrier)
+    {
+        const int j = threadIdx.x / TPF * 2, l = threadIdx.x % TPF;  // 256 threads: 2 of the 8 slots each
+        wks[j * TPF + l] = ld_c2(rrt, 8 * l, 8 * (slide_rt_base<M>() + TPF * j));
+        wks[(j + 1) * TPF + l] = ld_c2(rrt, 8 * l, 8 * (slide_rt_base<M>() + TPF * (j + 1)));
+    }
+    if (threadIdx.x < 4 * 15) {
+        const int pp = threadIdx.x / 15, j = threadIdx.x % 15;
+        tw2s[pp * 16 + j] = ld_c2(rtw, 8 * (15 * TPF + j * (TPF / 16) + pp), 0);
+    }
+    __syncthreads();
+    const uint64_t strip =
+        (uint64_t)__builtin_amdgcn_readfirstlane((int)((uint64_t)xcd_block(blockIdx.x, gridDim.x) * FPB + fl));
+    if (strip >= n_strips) return;  // a whole wave
+    const int trk = find_track(strip_pfx, n_tracks, strip);
+    const uint64_t F = frame_pfx[trk + 1] - frame_pfx[trk];
+    const uint64_t f0 = (strip - strip_pfx[trk]) * (uint64_t)STRIP_T;
+    const int nf = (int)(F - f0 < (uint64_t)STRIP_T ? F - f0 : (uint64_t)STRIP_T);
+    const float gn = gain[trk];
+    c2* buf = lds + fl * PADM;
+    const int vo = 8 * lt;
+    const uint64_t cstart = f0 * (uint64_t)(hop / 2);
+    const uint64_t clen = (uint64_t)(nf - 1) * (uint64_t)(hop / 2) + (uint64_t)M;
+    const __amdgpu_buffer_rsrc_t rx = rsrc_of(samples + src_off[trk] + 2 * cstart, (uint32_t)(8u * clen));
+    const __amdgpu_buffer_rsrc_t rw = rsrc_of(window, 4u * 2048u);
+
+    c2 win[16], tw1[15], ring[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const c2 x = ld_c2(rx, vo, 8 * TPF * k);
+        ring[k] = {x.x * gn, x.y * gn};
+    }
+#pragma unroll
+    for (int k = 0; k < 16; k++) win[k] = ld_c2(rw, vo, 8 * TPF * k);
+#pragma unroll
+    for (int j = 0; j < 15; j++) tw1[j] = ld_c2(rtw, vo, 8 * TPF * j);
+    const cx rth = rtp[slide_rt_base<M>() + 8 * TPF];  // bin M/2 (wave-uniform)
+    const c2 rtH = {rth.re, rth.im};
+    const int pp2 = lt / 16, q2 = lt % 16;
+    int colA, colA2, colB, colB2;
+    slide_cols2(lt, &colA, &colA2, &colB, &colB2);
+    const bool self0 = lt == 0;
+    // pass-1 stores at 17 lt + k; pass 2 in place at q + 17 pp + 68 k; column c at (c % 16) + 68 (c / 16) + 17 j
+    const int rb2 = q2 + 17 * pp2;
+    auto colbase = [](int c) { return (c & 15) + 68 * (c >> 4); };
+    // store byte offsets in a row (bins above, M = 1024): partner offsets are based at the slot
+    // with the largest scalar offset so every scalar part is >= 0
+    const int vA = 4 * colA, vAr = 4 * (M - colA - 768);
+    const int vA2 = 4 * (self0 ? 128 : colA + 512), vA2r = 4 * (M - (self0 ? 128 : colA + 512));
+    const int vA3 = 4 * (self0 ? 384 : colA + 768), vA3r = 4 * (M - (self0 ? 384 : colA + 768));
+    const int vB = 4 * colB, vBr = 4 * (M - colB - 768);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the per-strip loads have landed
+
+    for (int i = 0; i < nf; i++) {
+        const uint64_t f = f0 + (uint64_t)i;
+        c2 nxt[S];
+#pragma unroll
+        for (int s2 = 0; s2 < S; s2++) nxt[s2] = ld_c2(rx, vo, 8 * ((i + 1) * (hop / 2) + TPF * (16 - S + s2)));
+        c2 v[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) v[k] = {ring[k].x * win[k].x, ring[k].y * win[k].y};
+        radix16<false>(v, tw1);
+        frame_sync<TPF>();  // the previous frame's column reads are done (in-order LDS)
+#pragma unroll
+        for (int k = 0; k < 16; k++) buf[P17 * lt + k] = v[k];
+        frame_sync<TPF>();
+        // pass 2 (n = M/16 = 64, s = 16), in place
+#pragma unroll
+        for (int k = 0; k < 16; k++) v[k] = buf[rb2 + 68 * k];
+        {
+            c2 tw2[15];
+#pragma unroll
+            for (int j = 0; j < 15; j++) tw2[j] = tw2s[pp2 * 16 + j];
+            radix16<false>(v, tw2);
+        }
+#pragma unroll
+        for (int k = 0; k < 16; k++) buf[rb2 + 68 * k] = v[k];
+        frame_sync<TPF>();
+        // the frame's row as a buffer resource: per-lane byte offsets fixed for the strip, the
+        // slot's bin offset a scalar constant (no 64-bit address arithmetic per store)
+        const __amdgpu_buffer_rsrc_t ro = rsrc_of(mags + (mag_row0[trk] + f) * (uint64_t)stride, 4u * (M + 1));
+        float mx = 0.0f;
+        uint32_t lo = 0xFFFFFFFFu, hi = 0u;
+        auto sq = [&](float yx, float yy) { return 0x1p-33f * sqrt_fast(__builtin_fmaf(yx, yx, yy * yy), lo, hi); };
+        auto put = [&](int voff, int soff, float mag) {
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mag), ro, voff, soff, 0);
+            if (FRAME_MAX) mx = __builtin_fmaxf(mx, mag);
+        };
+        // own bin at (vk, sk), partner bin M - k at (vr, sr)
+        auto pair = [&](c2 Zk, c2 Zr, c2 w, int vk, int sk, int vr, int sr) {
+            const float sx = Zk.x + Zr.x, sy = Zk.y - Zr.y, dx = Zk.y + Zr.y, dy = -(Zk.x - Zr.x);
+            put(vk, sk, sq(__builtin_fmaf(w.x, dx, __builtin_fmaf(-w.y, dy, sx)), __builtin_fmaf(w.x, dy, __builtin_fmaf(w.y, dx, sy))));
+            put(vr, sr, sq(__builtin_fmaf(-w.x, dx, __builtin_fmaf(w.y, dy, sx)), __builtin_fmaf(w.x, dy, __builtin_fmaf(w.y, dx, -sy))));
+        };
+        auto single = [&](c2 Z, c2 w, int k) {
+            const float sx = Z.x + Z.x, sy = Z.y - Z.y, dx = Z.y + Z.y, dy = -(Z.x - Z.x);
+            put(0, 4 * k, sq(__builtin_fmaf(w.x, dx, __builtin_fmaf(-w.y, dy, sx)), __builtin_fmaf(w.x, dy, __builtin_fmaf(w.y, dx, sy))));
+        };
+        // trailing radix-4 (n = 4, s = M/4, p = 0) on the thread's four columns
+        c2 A[4], A2[4], Bv[4], B2[4];
+        auto col4 = [&](int c, c2 (&z)[4]) {
+            const int b = colbase(c);
+            bfly4<false>(buf[b], buf[b + 17], buf[b + 34], buf[b + 51], c2{}, c2{}, c2{}, z[0], z[1], z[2], z[3]);
+        };
+        col4(colA, A);
+        col4(colA2, A2);
+        col4(colB, Bv);
+        col4(colB2, B2);
+        const c2 zk0 = A[0], zr0 = self0 ? A[0] : A2[3];
+        const c2 zk1 = A[1], zr1 = self0 ? A[3] : A2[2];
+        const c2 zk2 = self0 ? A2[0] : A[2], zr2 = self0 ? A2[3] : A2[1];
+        const c2 zk3 = self0 ? A2[1] : A[3], zr3 = self0 ? A2[2] : A2[0];
+        // bins (k, M - k): colA + 256 j for j < 2 (thread 0: 0 / 1024, 256 / 768 as well), then
+        // colA + 512, colA + 768 (thread 0: 128 / 896, 384 / 640); colB + 256 j for the B pairs
+        pair(zk0, zr0, wks[0 * TPF + lt], vA, 0, vAr, 3 * 1024);
+        pair(zk1, zr1, wks[1 * TPF + lt], vA, 1024, vAr, 2 * 1024);
+        pair(zk2, zr2, wks[2 * TPF + lt], vA2, 0, vA2r, 0);
+        pair(zk3, zr3, wks[3 * TPF + lt], vA3, 0, vA3r, 0);
+#pragma unroll
+        for (int j = 0; j < 4; j++) pair(Bv[j], B2[3 - j], wks[(4 + j) * TPF + lt], vB, 1024 * j, vBr, 1024 * (3 - j));
+        if (self0) single(A[2], rtH, M / 2);
+        const bool missed = __builtin_amdgcn_ballot_w64(sqrt_fast_missed(lo, hi)) != 0;
+        if (__builtin_expect(missed, 0) && lt == 0) redo[1 + atomicAdd(redo, 1u)] = (uint32_t)(frame_pfx[trk] + f);
+        if constexpr (FRAME_MAX) {
+            mx = wave_max(mx);
+            if (lt == 0) frame_max[mag_row0[trk] + f] = mx;
+        }
+#pragma unroll
+        for (int k = 0; k < 16 - S; k++) ring[k] = ring[k + S];
+#pragma unroll
+        for (int s2 = 0; s2 < S; s2++) ring[16 - S + s2] = {nxt[s2].x * gn, nxt[s2].y * gn};
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // k_stft_slide8: the sliding strip for N = 8192 (M = 4096 = 16^3, one 256-thread workgroup per
 // strip), software-pipelined across frames.  The kernel holds its per-strip constants in ~110
 // VGPRs, so it runs 2 waves per SIMD, and one wave alone issues a VALU instruction at most every
@@ -952,6 +1111,186 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_stft_slide8w3: the sliding strip for N = 8192 at 3 waves per SIMD (3 workgroups per CU; the
+// budget is <= 168 VGPRs and <= 53 KB of LDS per 256-thread workgroup).  k_stft_slide8 runs 2
+// waves per SIMD (229 VGPRs, two 34.8 KB frame buffers), and one wave issues a VALU instruction
+// at most every 4 cycles, so the SIMD's VALU idles whenever either wave waits.
+// What moves to fit the budget, the arithmetic unchanged (bit-identical magnitudes):
+//  * ONE frame buffer, pass 2 in place: a pass-2 thread reads its 16 slots, runs the radix-16
+//    pass and writes the 16 results back into the same slots (the threads' slot sets are
+//    disjoint, so no barrier between its reads and its writes).  Element z[q + 256 pp + 16 k]
+//    then lives where x[q + 16 pp + 256 k] was read, and the last pass reads column c, Z[c + 256 m],
+//    from slots (c % 16) + 272 (c / 16) + 17 m: conflict-free for ds_read_b64 on every lane;
+//  * a third barrier per frame, before the next frame's pass-1 stores (its pass-1 arithmetic runs
+//    before that barrier, from the register ring, while other workgroups of the CU issue);
+//  * the pass-2 twiddles (16 p' x 15, 1.9 KB, four distinct p' per wave: broadcast reads) and the
+//    post twiddles (8 slots x 256 lanes, 16 KB) from LDS instead of 46 VGPRs; the pass-3
+//    twiddles stay wave-uniform scalars; window, pass-1 twiddles and the sample ring stay in VGPRs.
+template <int S>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_stft_slide8w3(
+    const float* __restrict__ samples, const uint64_t* __restrict__ frame_pfx, const uint64_t* __restrict__ strip_pfx,
+    int n_tracks, uint64_t n_strips, const uint64_t* __restrict__ src_off, const float* __restrict__ gain, int hop,
+    const float* __restrict__ window, const cx* __restrict__ twp, const cx* __restrict__ rtp, float* __restrict__ mags,
+    const uint64_t* __restrict__ mag_row0, int stride, uint32_t* __restrict__ redo) {
+    constexpr int M = 4096, TPF = 256;
+    constexpr int PADM = M + PADSHIFT * M / 16;
+    static_assert(S >= 1 && S <= 16 && STRIP_T == 64, "hop = S * 512; the miss mask holds 64 frames");
+    __shared__ c2 buf[PADM];
+    __shared__ __attribute__((aligned(16))) c2 tw2s[16 * 16];  // [p'][j], j < 15
+    __shared__ c2 wks[8 * TPF];                                 // [slot j][lane]
+    __shared__ uint64_t miss_mask[4];
+
+    const int lt = threadIdx.x;
+    const uint64_t strip = (uint64_t)__builtin_amdgcn_readfirstlane((int)xcd_block(blockIdx.x, gridDim.x));
+    if (strip >= n_strips) return;  // the whole workgroup
+    const int trk = find_track(strip_pfx, n_tracks, strip);
+    const uint64_t F = frame_pfx[trk + 1] - frame_pfx[trk];
+    const uint64_t f0 = (strip - strip_pfx[trk]) * (uint64_t)STRIP_T;
+    const int nf = (int)(F - f0 < (uint64_t)STRIP_T ? F - f0 : (uint64_t)STRIP_T);
+    const float gn = gain[trk];
+    const int vo = 8 * lt;
+    const uint64_t cstart = f0 * (uint64_t)(hop / 2);
+    const uint64_t clen = (uint64_t)(nf - 1) * (uint64_t)(hop / 2) + (uint64_t)M;
+    const __amdgpu_buffer_rsrc_t rx = rsrc_of(samples + src_off[trk] + 2 * cstart, (uint32_t)(8u * clen));
+    const __amdgpu_buffer_rsrc_t rw = rsrc_of(window, 4u * 8192u);
+    const __amdgpu_buffer_rsrc_t rtw = rsrc_of(twp, 8u * 15u * (TPF + TPF / 16 + 1));
+    const __amdgpu_buffer_rsrc_t rrt = rsrc_of(rtp, 8u * (slide_rt_base<M>() + 8 * TPF + 1));
+    float* const row0 = mags + (mag_row0[trk] + f0) * (uint64_t)stride;
+
+    // LDS tables (published by the first frame's first barrier)
+#pragma unroll
+    for (int j = 0; j < 8; j++) wks[j * TPF + lt] = ld_c2(rrt, vo, 8 * (slide_rt_base<M>() + TPF * j));
+    if (lt < 15 * 16) {
+        const int pp = lt / 15, j = lt % 15;
+        tw2s[pp * 16 + j] = ld_c2(rtw, 8 * (15 * TPF + j * (TPF / 16) + pp), 0);
+    }
+    // per-strip register constants: window, pass-1 twiddles, the sample ring; pass 3 wave-uniform
+    c2 win[16], tw1[15], tw3[15], ring[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const c2 x = ld_c2(rx, vo, 8 * TPF * k);
+        ring[k] = {x.x * gn, x.y * gn};
+    }
+#pragma unroll
+    for (int k = 0; k < 16; k++) win[k] = ld_c2(rw, vo, 8 * TPF * k);
+#pragma unroll
+    for (int j = 0; j < 15; j++) tw1[j] = ld_c2(rtw, vo, 8 * TPF * j);
+#pragma unroll
+    for (int j = 0; j < 15; j++) {
+        const cx t = twp[15 * TPF + 15 * (TPF / 16) + j];
+        tw3[j] = c2{t.re, t.im};
+    }
+    const cx rth = rtp[slide_rt_base<M>() + 8 * TPF];  // bin M/2 (wave-uniform: scalar)
+    const c2 rtH = {rth.re, rth.im};
+    const int pp2 = lt / 16, q2 = lt % 16;
+    const int colA = slide_col8(lt);
+    const bool self0 = lt == 0, self128 = lt == 32;
+    const int src_lane = (self0 || self128) ? (lt & 63) : ((lt & 63) ^ 32);
+    // slots: pass-1 stores 17 lt + k; pass 2 reads and writes back q + 17 pp + 272 k; the last
+    // pass reads (c % 16) + 272 (c / 16) + 17 m for its column c
+    const int rb2 = q2 + 17 * pp2, rb3 = (colA & 15) + P272 * (colA >> 4);
+    const int vown = 4 * colA, vpart = 4 * (M - colA - 256 * 7), vmid = 4 * (M / 2);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the per-strip loads have landed
+
+    // prologue: pass 1 of frame 0 in registers, the ring advanced to frame 1
+    c2 v[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) v[k] = {ring[k].x * win[k].x, ring[k].y * win[k].y};
+    radix16<false>(v, tw1);
+    {
+        c2 nx[S];
+#pragma unroll
+        for (int s2 = 0; s2 < S; s2++) nx[s2] = ld_c2(rx, vo, 8 * ((hop / 2) + TPF * (16 - S + s2)));
+#pragma unroll
+        for (int k = 0; k < 16 - S; k++) ring[k] = ring[k + S];
+#pragma unroll
+        for (int s2 = 0; s2 < S; s2++) ring[16 - S + s2] = {nx[s2].x * gn, nx[s2].y * gn};
+    }
+
+    uint64_t miss = 0;  // wave-uniform: bit i = frame f0 + i met the sqrt's inexact range
+    for (int i = 0;; i++) {
+        c2 nx[S];  // the ring's new values for frame i + 2 (zeros past the strip: outside rx)
+#pragma unroll
+        for (int s2 = 0; s2 < S; s2++) nx[s2] = ld_c2(rx, vo, 8 * ((i + 2) * (hop / 2) + TPF * (16 - S + s2)));
+        if (i > 0) __syncthreads();  // every last-pass read of frame i - 1 is done
+#pragma unroll
+        for (int k = 0; k < 16; k++) buf[P17 * lt + k] = v[k];
+        __syncthreads();
+        // pass 2 (n = M/16, s = 16), in place
+#pragma unroll
+        for (int k = 0; k < 16; k++) v[k] = buf[rb2 + P272 * k];
+        {
+            c2 tw2[15];
+#pragma unroll
+            for (int j = 0; j < 15; j++) tw2[j] = tw2s[pp2 * 16 + j];
+            radix16<false>(v, tw2);
+        }
+#pragma unroll
+        for (int k = 0; k < 16; k++) buf[rb2 + P272 * k] = v[k];
+        __syncthreads();
+        // last pass (n = 16, s = 256, p' = 0) on column colA, then the (k, M-k) exchange between
+        // lanes l and l^32: every lane sends its elements 8..15; the column-0 lane sends itself 9..15, 0
+#pragma unroll
+        for (int k = 0; k < 16; k++) v[k] = buf[rb3 + P17 * k];
+        radix16<true>(v, tw3);
+        c2 P[16];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const c2 snd = self0 ? v[(9 + k) & 15] : v[8 + k];
+            P[8 + k] = {__shfl(snd.x, src_lane, 64), __shfl(snd.y, src_lane, 64)};
+            P[k] = v[k];
+        }
+        const c2 Pm = v[8];
+        {
+            // post-processing of frame i (sdsp_fft_spec.h STFT section; see k_stft_slide)
+            const __amdgpu_buffer_rsrc_t ro = rsrc_of(row0 + (int64_t)i * stride, 4u * (M + 1));
+            uint32_t lo = 0xFFFFFFFFu, hi = 0u;
+            auto sq = [&](float yx, float yy) { return 0x1p-33f * sqrt_fast(__builtin_fmaf(yx, yx, yy * yy), lo, hi); };
+            auto st = [&](float mag, int voff, int soff) {
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mag), ro, voff, soff, 0);
+            };
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const c2 Zk = P[j], Zr = P[15 - j], w = wks[j * TPF + lt];
+                const float sx = Zk.x + Zr.x, sy = Zk.y - Zr.y, dx = Zk.y + Zr.y, dy = -(Zk.x - Zr.x);
+                st(sq(__builtin_fmaf(w.x, dx, __builtin_fmaf(-w.y, dy, sx)), __builtin_fmaf(w.x, dy, __builtin_fmaf(w.y, dx, sy))),
+                   vown, 1024 * j);
+                st(sq(__builtin_fmaf(-w.x, dx, __builtin_fmaf(w.y, dy, sx)), __builtin_fmaf(w.x, dy, __builtin_fmaf(w.y, dx, -sy))),
+                   vpart, 1024 * (7 - j));
+            }
+            if (self0) {  // bin M/2, self-paired
+                const c2 Z = Pm, w = rtH;
+                const float sx = Z.x + Z.x, sy = Z.y - Z.y, dx = Z.y + Z.y, dy = -(Z.x - Z.x);
+                st(sq(__builtin_fmaf(w.x, dx, __builtin_fmaf(-w.y, dy, sx)), __builtin_fmaf(w.x, dy, __builtin_fmaf(w.y, dx, sy))),
+                   vmid, 0);
+            }
+            const bool missed = __builtin_amdgcn_ballot_w64(sqrt_fast_missed(lo, hi)) != 0;
+            miss |= (uint64_t)missed << (i & 63);
+        }
+        if (i + 1 == nf) break;
+        // pass 1 of frame i + 1 from the ring (stored after the next barrier)
+#pragma unroll
+        for (int k = 0; k < 16; k++) v[k] = {ring[k].x * win[k].x, ring[k].y * win[k].y};
+        radix16<false>(v, tw1);
+#pragma unroll
+        for (int k = 0; k < 16 - S; k++) ring[k] = ring[k + S];
+#pragma unroll
+        for (int s2 = 0; s2 < S; s2++) ring[16 - S + s2] = {nx[s2].x * gn, nx[s2].y * gn};
+    }
+    // list the strip's missed frames once (k_stft_mag recomputes them right after this kernel)
+    if ((lt & 63) == 0) miss_mask[lt >> 6] = miss;
+    __syncthreads();
+    if (lt == 0) {
+        uint64_t m = miss_mask[0] | miss_mask[1] | miss_mask[2] | miss_mask[3];
+        while (m) {
+            const int b = __builtin_ctzll(m);
+            m &= m - 1;
+            redo[1 + atomicAdd(redo, 1u)] = (uint32_t)(frame_pfx[trk] + f0 + (uint64_t)b);
+        }
+    }
+}
+
 // strips of STRIP_T frames per track: strip_pfx[t] = sum over tracks < t of ceil(F / STRIP_T)
 std::vector<uint64_t> stft_strips(const std::vector<uint64_t>& frame_pfx) {
     std::vector<uint64_t> sp(frame_pfx.size(), 0);
@@ -1063,18 +1402,38 @@ void launch_stft(int nfft, bool frame_max, const float* samples, const uint64_t*
     if (strip_pfx && n_strips && redo && stft_slide_ok(nfft, hop)) {
         // redo[0] = 0; redo[1..] receives the frames the sliding kernel could not finish exactly
         SDSP_HIP_CHECK(hipMemsetAsync(redo, 0, sizeof(uint32_t), st));
+#ifdef SDSP_STFT2_W2
 #define SDSP_SLIDE(N, S, FM)                                                                                      \
     hipLaunchKernelGGL((k_stft_slide<N, S, FM>), dim3((unsigned)((n_strips + 256 / (N / 32) - 1) / (256 / (N / 32)))), \
                        block, 0, st, samples, frame_pfx, strip_pfx, n_tracks, n_strips, src_off, gain, hop, window, twp, \
                        rtp, mags, mag_row0, stride, fmax, redo)
+#else
+#define SDSP_SLIDE(N, S, FM)                                                                                      \
+    hipLaunchKernelGGL((k_stft_slide2s<S, FM>), dim3((unsigned)((n_strips + 3) / 4)), block, 0, st, samples,         \
+                       frame_pfx, strip_pfx, n_tracks, n_strips, src_off, gain, hop, window, twp, rtp, mags, mag_row0, \
+                       stride, fmax, redo)
+#endif
         if (nfft == 8192) {
             const dim3 g8((unsigned)n_strips);
+            // SDSP_STFT8_CAP2 (experiment): 4 KB of dynamic LDS beside the 53 KB static make a
+            // workgroup too large for 3 per CU, so the kernel runs 2 per CU
+#ifdef SDSP_STFT8_CAP2
+            const size_t dyn8 = 4096;
+#else
+            const size_t dyn8 = 0;
+#endif
+#ifdef SDSP_STFT8_W2
+#define SDSP_K8 k_stft_slide8
+#else
+#define SDSP_K8 k_stft_slide8w3
+#endif
             if (hop == 512)
-                hipLaunchKernelGGL(k_stft_slide8<1>, g8, block, 0, st, samples, frame_pfx, strip_pfx, n_tracks, n_strips,
+                hipLaunchKernelGGL(SDSP_K8<1>, g8, block, dyn8, st, samples, frame_pfx, strip_pfx, n_tracks, n_strips,
                                    src_off, gain, hop, window, twp, rtp, mags, mag_row0, stride, redo);
             else
-                hipLaunchKernelGGL(k_stft_slide8<2>, g8, block, 0, st, samples, frame_pfx, strip_pfx, n_tracks, n_strips,
+                hipLaunchKernelGGL(SDSP_K8<2>, g8, block, dyn8, st, samples, frame_pfx, strip_pfx, n_tracks, n_strips,
                                    src_off, gain, hop, window, twp, rtp, mags, mag_row0, stride, redo);
+#undef SDSP_K8
         } else if (frame_max) {
             if (hop == 256)
                 SDSP_SLIDE(2048, 2, true);

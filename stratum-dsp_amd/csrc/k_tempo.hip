@@ -118,6 +118,9 @@ constexpr int FFT_TG_RMAX = 8;  // in-place LDS FFT up to M = 8192 (P = 16384)
 
 // ----------------------------------------------------------------------------------------
 // FFT tempogram.  items[i] = trk*NVAR + v.  Output entries for item i at out_off[i], count K.
+// LDS: the in-place LDS FFT (P.lds); otherwise the Stockham ping-pong through L2-resident global
+// scratch, instantiated as its own kernel so it carries none of the in-place FFT's registers.
+template <bool LDS>
 __global__ __launch_bounds__(256) void k_fft_tempogram(const int* __restrict__ items, int n_items, int T,
                                                        const float* __restrict__ nov, const float* __restrict__ nov_sum,
                                                        const uint64_t* __restrict__ frame_pfx, uint64_t total,
@@ -134,7 +137,7 @@ __global__ __launch_bounds__(256) void k_fft_tempogram(const int* __restrict__ i
     const int M = P.P / 2;
     cx* A;
     cx* Bb;
-    if (P.lds) {
+    if constexpr (LDS) {
         A = dyn;
         Bb = dyn + M;
     } else {
@@ -153,7 +156,7 @@ __global__ __launch_bounds__(256) void k_fft_tempogram(const int* __restrict__ i
     __syncthreads();
     cx* Z;
     uint64_t* keys;
-    if (P.lds) {  // one M-slot buffer + the key buffer (dyn[M ..])
+    if constexpr (LDS) {  // one M-slot buffer + the key buffer (dyn[M ..])
         Z = (M >= 2) ? fft_block_inplace<FFT_TG_RMAX>(A, M, tw) : A;
         keys = reinterpret_cast<uint64_t*>(dyn + M);
     } else {
@@ -481,7 +484,9 @@ __global__ __launch_bounds__(256) void k_tempo_select(const int* __restrict__ ac
 // loop is spread over the lanes (each phase's sums stay sequential; the max over phases is
 // order-free).
 constexpr int MR_CAP_LDS = 256;
-constexpr int MR_WM_CAP = 28672;  // novelty frames whose window maxima k_multires keeps in LDS (112 KB: 4.6 min at hop 512)
+// window maxima staged in LDS per segment of novelty frames (beat_contrast_seg): 16 KB whatever
+// the track length, so a k_multires workgroup fits beside the key stream's STFT workgroups
+constexpr int MR_SEG_BUF = 4096;
 struct CandList {
     const float* c;  // 4 floats per candidate: bpm, score, fft_norm, ac_norm
     int n;
@@ -499,10 +504,14 @@ __device__ float lookup_c(CandList L, float bpm, float tol) {
     return bs;
 }
 
-// nov_total: novelty.iter().sum() (sequential), computed once per track by the caller
-// wm (optional): the window maxima max(nov[i-2 .. i+2]) precomputed in LDS, else read per lookup
-__device__ float beat_contrast_wave(const float* nov, int n, int sr, int hop, float bpm, float nov_total,
-                                    const float* wm = nullptr) {
+// beat_contrast_score (multi_resolution.rs:162-203) by the whole wave.  nov_total:
+// novelty.iter().sum() (sequential), computed once per track by the caller.  Lane l owns the
+// phases l + 64 q (q < 8; period <= 512).  The novelty's +-2 window maxima are staged in LDS one
+// segment at a time (wbuf: MR_SEG_BUF floats; a segment of MR_SEG_BUF - period frames plus a halo
+// of `period` frames, since the half- and third-beat lookups reach at most i + 2 period / 3), and
+// each phase's sums visit their frames in increasing order across the segments: the same f32
+// folds as one pass over the whole track.  The max over phases is order-free.
+__device__ float beat_contrast_seg(const float* nov, int n, int sr, int hop, float bpm, float nov_total, float* wbuf) {
     if (n < 16 || !(sd_isfinite_f(bpm) && bpm > 0.0f) || sr == 0 || hop == 0) return 0.0f;
     const float fpb = (60.0f * (float)sr) / (bpm * (float)hop);
     if (!sd_isfinite_f(fpb) || fpb < 3.0f) return 0.0f;
@@ -510,46 +519,64 @@ __device__ float beat_contrast_wave(const float* nov, int n, int sr, int hop, fl
     if (!(pi >= 3 && pi <= 512)) return 0.0f;
     const int period = (int)pi, w = 2;
     const float total = sd_maxf(nov_total, 1e-6f);
-    auto wmax = [&](int i) {
-        if (wm) return wm[i];
-        const int s = i >= w ? i - w : 0, e = i + w + 1 < n ? i + w + 1 : n;
-        float mx = 0.0f;
-        for (int j = s; j < e; j++) mx = sd_maxf(mx, nov[j]);
-        return mx;
-    };
-    float best = -1e9f;
-    for (int ph = threadIdx.x; ph < period; ph += blockDim.x) {
-        float bs = 0.0f, hs = 0.0f, ts = 0.0f;
-        uint32_t bn = 0, hn = 0, tn = 0;
-        for (int i = ph; i < n; i += period) {
-            bs += wmax(i);
-            bn++;
-            if (period >= 6) {
-                const int j = i + period / 2;
-                if (j < n) {
-                    hs += wmax(j);
-                    hn++;
-                }
-            }
-            if (period >= 9) {
-                for (int fr = 1; fr <= 2; fr++) {
-                    const int j = i + (period * fr) / 3;
+    const int lane = threadIdx.x;  // blockDim == 64
+    constexpr int NQ = 512 / 64;
+    float bs[NQ], hs[NQ], ts[NQ];
+    uint32_t bn[NQ], hn[NQ], tn[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; q++) bs[q] = hs[q] = ts[q] = 0.0f, bn[q] = hn[q] = tn[q] = 0u;
+    const int seg = MR_SEG_BUF - period;
+    for (int s0 = 0; s0 < n; s0 += seg) {
+        const int s1 = s0 + seg < n ? s0 + seg : n;
+        const int e1 = s1 + period < n ? s1 + period : n;
+        __syncthreads();  // the previous segment's reads are done
+        for (int q = lane; q < e1 - s0; q += 64) {
+            const int i = s0 + q;
+            const int s = i >= w ? i - w : 0, e = i + w + 1 < n ? i + w + 1 : n;
+            float mx = 0.0f;
+            for (int j = s; j < e; j++) mx = sd_maxf(mx, nov[j]);
+            wbuf[q] = mx;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < NQ; q++) {
+            const int ph = lane + 64 * q;
+            if (ph >= period) continue;
+            int i = ph >= s0 ? ph : ph + ((s0 - ph + period - 1) / period) * period;
+            for (; i < s1; i += period) {
+                bs[q] += wbuf[i - s0];
+                bn[q]++;
+                if (period >= 6) {
+                    const int j = i + period / 2;
                     if (j < n) {
-                        ts += wmax(j);
-                        tn++;
+                        hs[q] += wbuf[j - s0];
+                        hn[q]++;
+                    }
+                }
+                if (period >= 9) {
+                    for (int fr = 1; fr <= 2; fr++) {
+                        const int j = i + (period * fr) / 3;
+                        if (j < n) {
+                            ts[q] += wbuf[j - s0];
+                            tn[q]++;
+                        }
                     }
                 }
             }
         }
-        const float bm = bn > 0 ? bs / (float)bn : 0.0f;
-        const float hm = hn > 0 ? hs / (float)hn : 0.0f;
-        const float tm = tn > 0 ? ts / (float)tn : 0.0f;
+    }
+    float best = -1e9f;
+#pragma unroll
+    for (int q = 0; q < NQ; q++) {
+        if (lane + 64 * q >= period) continue;
+        const float bm = bn[q] > 0 ? bs[q] / (float)bn[q] : 0.0f;
+        const float hm = hn[q] > 0 ? hs[q] / (float)hn[q] : 0.0f;
+        const float tm = tn[q] > 0 ? ts[q] / (float)tn[q] : 0.0f;
         const float contrast = bm - 0.60f * hm - 0.40f * tm;
         const float score = sd_clampf(contrast / sd_maxf(total / (float)n, 1e-6f), -10.0f, 10.0f);
         best = sd_maxf(best, score);
     }
-    best = wave_max(best);  // blockDim == 64
-    return best;
+    return wave_max(best);
 }
 
 __global__ __launch_bounds__(64) void k_multires(const int* __restrict__ tracks, int n_items,
@@ -747,25 +774,13 @@ __global__ __launch_bounds__(64) void k_multires(const int* __restrict__ tracks,
     const uint64_t g0 = fpfx512[j512];
     const int nn = (int)(fpfx512[j512 + 1] - g0) - 1;
     const float* nov = nov512 + g0;
-    __shared__ float sbuf[SEQ_CH];
-    const float nov_total = (nf >= 2 && nn > 0) ? block_seq_sum(nov, nn, sbuf) : 0.0f;
-    // the family / fold gates read every novelty frame's +-2 window maximum several times per
-    // candidate tempo: computed once into LDS when the track fits (an exact, order-free max)
-    extern __shared__ float mr_wm[];
-    const float* wm = nullptr;
-    if (nf >= 2 && nn > 0 && nn <= P.wm_cap) {
-        for (int q = threadIdx.x; q < nn; q += blockDim.x) {
-            const int s0 = q >= 2 ? q - 2 : 0, e0 = q + 3 < nn ? q + 3 : nn;
-            float mx = 0.0f;
-            for (int j = s0; j < e0; j++) mx = sd_maxf(mx, nov[j]);
-            mr_wm[q] = mx;
-        }
-        __syncthreads();
-        wm = mr_wm;
-    }
+    // one LDS buffer: block_seq_sum's staging (SEQ_CH), then beat_contrast_seg's segments
+    __shared__ float wbuf[MR_SEG_BUF];
+    static_assert(MR_SEG_BUF >= SEQ_CH, "the staging buffer is shared");
+    const float nov_total = (nf >= 2 && nn > 0) ? block_seq_sum(nov, nn, wbuf) : 0.0f;
     if (nf >= 2 && nn > 0) {
         for (int k = 0; k < nf; k++) {
-            const float a = beat_contrast_wave(nov, nn, P.sr, P.hop512, fam_bpm[k], nov_total, wm);
+            const float a = beat_contrast_seg(nov, nn, P.sr, P.hop512, fam_bpm[k], nov_total, wbuf);
             if (threadIdx.x == 0) fam_align[k] = a;
             __syncthreads();
         }
@@ -806,7 +821,7 @@ __global__ __launch_bounds__(64) void k_multires(const int* __restrict__ tracks,
     }
     __syncthreads();
     if (do_fam_s) {
-        cur_align = beat_contrast_wave(nov, nn, P.sr, P.hop512, best_bpm_s, nov_total, wm);
+        cur_align = beat_contrast_seg(nov, nn, P.sr, P.hop512, best_bpm_s, nov_total, wbuf);
         if (threadIdx.x == 0) {
             if (sd_absf(fam_bpm[4] - best_bpm_s) > 0.75f && fam_align[4] >= cur_align + 0.40f) {
                 dr.tf = 1, dr.tf_from = best_bpm_s, dr.tf_to = fam_bpm[4], dr.tf_al0 = cur_align, dr.tf_al1 = fam_align[4];
@@ -855,8 +870,12 @@ void launch_fft_tempogram(const int* items, int n_items, int T, const float* nov
     int K2 = 1;
     while (K2 < P.K) K2 <<= 1;
     const size_t lds = P.lds ? (size_t)(P.P / 2 + K2) * sizeof(cx) : 0;  // M = P/2 slots + keys
-    hipLaunchKernelGGL(k_fft_tempogram, dim3(n_items), dim3(256), lds, st, items, n_items, T, nov, nov_sum, frame_pfx,
-                       total, P, tw, rt, gscratch, out_off, out_bpm, out_pow);
+    if (P.lds)
+        hipLaunchKernelGGL(k_fft_tempogram<true>, dim3(n_items), dim3(256), lds, st, items, n_items, T, nov, nov_sum,
+                           frame_pfx, total, P, tw, rt, gscratch, out_off, out_bpm, out_pow);
+    else
+        hipLaunchKernelGGL(k_fft_tempogram<false>, dim3(n_items), dim3(256), 0, st, items, n_items, T, nov, nov_sum,
+                           frame_pfx, total, P, tw, rt, gscratch, out_off, out_bpm, out_pow);
 }
 void launch_acf_tempogram(const int* items, int n_items, const float* nov, const uint64_t* frame_pfx, uint64_t total,
                           const float* bpm_grid, const int* lag_grid, int NB, float* out_bpm, float* out_str,
@@ -877,12 +896,8 @@ void launch_multires(const int* tracks, int n_items, const float* c256, const in
                      const TempoEst* base_est, const float* nov512, const uint64_t* fpfx512, const MrParams& P,
                      TempoEst* mr_est, int* used, float* final_bpm, float* final_conf, hipStream_t st, MrDbg* dbg) {
     if (n_items == 0) return;
-    MrParams Q = P;
-    Q.wm_cap = MR_WM_CAP;
-    const size_t lds = (size_t)MR_WM_CAP * sizeof(float);
-    (void)hipFuncSetAttribute((const void*)k_multires, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(k_multires, dim3(n_items), dim3(64), lds, st, tracks, n_items, c256, n256, c512, n512, c1024,
-                       n1024, cap256, cap512, cap1024, base_est, nov512, fpfx512, Q, mr_est, used, final_bpm,
+    hipLaunchKernelGGL(k_multires, dim3(n_items), dim3(64), 0, st, tracks, n_items, c256, n256, c512, n512, c1024,
+                       n1024, cap256, cap512, cap1024, base_est, nov512, fpfx512, P, mr_est, used, final_bpm,
                        final_conf, dbg);
 }
 

@@ -98,7 +98,6 @@ struct MrParams {
     int human_prior, top_k, band;
     int sr, hop512;
     int own512;  // 1: the hop-512 lists / novelty are the escalation's own pass (item order), else the base pass's (track order)
-    int wm_cap;  // set by launch_multires: novelty window maxima kept in LDS up to this many frames
 };
 
 // debug_track_id diagnostics (src/lib.rs:461-487, 547-573, multi_resolution.rs:707-860): what
@@ -328,6 +327,14 @@ void launch_hpss_rows(const float* p, const uint64_t* row0, const uint64_t* fpfx
 void launch_beat_sync(const int* tracks, int n_items, const uint64_t* frame_pfx, const float* fchroma,
                       const float* fenergy, const float* beats, const uint64_t* beat_off, const uint64_t* row_pfx,
                       float fd, float* chroma, float* energy, hipStream_t st);
+// the default key path's band-limited mask + block energy sums and the HPCP that reads them
+// (k_key.hip k_mask_rp / k_hpcp_band; only for margin 12, power 2)
+bool mask_band_ok(int margin, float power);
+void launch_mask_band(float* mags, int stride, int B, const uint64_t* frame_pfx, const int* tracks, int n_items,
+                      float power, int st_lo, int st_hi, float* part, uint64_t total, hipStream_t st);
+void launch_hpcp_band(const float* mags, const uint64_t* frame_pfx, const uint64_t* tile_pfx, const int* tracks,
+                      int n_items, uint64_t n_tiles, const HpcpParams& P, const HarmEntry* harm, const float* part,
+                      uint64_t total, float* chroma, float* energy, hipStream_t st);
 void launch_hpcp(const float* mags, const uint64_t* frame_pfx, const uint64_t* tile_pfx, const int* tracks,
                  int n_items, uint64_t n_tiles, const HpcpParams& P, const HarmEntry* harm, float* chroma,
                  float* energy, hipStream_t st);

@@ -1303,7 +1303,14 @@ void Pipeline::tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPa
         pc.prm.b_lo = b_lo;
         pc.prm.K = K;
         pc.prm.fres = fr;
-        pc.prm.lds = kv.first <= 16384 ? 1 : 0;  // k_fft_tempogram's in-place LDS FFT: M <= 8192
+        // k_fft_tempogram's in-place LDS FFT up to P = 8192 (32 KB of LDS); larger P (3-min tracks
+        // at hop 512 have P = 16384) through L2-resident global scratch.  A 64 KB LDS workgroup
+        // waits for a CU that no key-stream STFT workgroup occupies, which the concurrent pipeline
+        // seldom offers: its launches stretched from 0.3 ms to 19 ms (round 4)
+#ifndef SDSP_FFT_TG_LDS_MAX
+#define SDSP_FFT_TG_LDS_MAX 8192
+#endif
+        pc.prm.lds = kv.first <= SDSP_FFT_TG_LDS_MAX ? 1 : 0;
         uint64_t K2 = 1;
         while (K2 < (uint64_t)K) K2 <<= 1;
         if (K > 0 && K2 > kv.first / 2) throw HipError("FFT tempogram: too many in-range bins for the key buffer");
@@ -1617,7 +1624,33 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         const bool use_log = cfg_.enable_key_log_frequency;  // :1062-1095
         const bool tuned = cfg_.enable_key_tuning_compensation && !use_log;
         const bool whiten = cfg_.enable_key_hpcp_whitening && cfg_.key_hpcp_whitening_smooth_bins >= 3;
-        if (cfg_.enable_key_hpss_harmonic) {
+        // the default key path (harmonic mask, plain HPCP, nothing else reading the masked
+        // spectrogram): the mask stores only HPCP's peak band and folds the frame energies in
+        // 64-bin blocks (k_mask_rp / k_hpcp_band); SDSP_KEY_EXACT_ENERGY builds
+        // keep the reference's one sequential energy sum (k_mask_r / k_hpcp)
+        HpcpParams hp{};
+        hp.B = B8;
+        hp.stride = ks_;
+        hp.pk_lo = 1;
+        hp.pk_hi = 0;
+        band_bins(B8, fres8, sd_maxf(100.0f, 20.0f), sd_minf(5000.0f, (float)sr_ / 2.0f), &hp.pk_lo, &hp.pk_hi);
+        hp.K = (int)std::max<uint64_t>(cfg_.key_hpcp_peaks_per_frame, 1);
+        hp.hmax = (int)std::max<uint64_t>(cfg_.key_hpcp_num_harmonics, 1);
+        hp.p = sd_clampf(cfg_.key_hpcp_mag_power, 0.05f, 1.0f);
+#ifdef SDSP_KEY_EXACT_ENERGY
+        constexpr bool band_ok = false;
+#else
+        constexpr bool band_ok = true;
+#endif
+        const bool plain_hpcp = !use_log && cfg_.enable_key_hpcp && !tuned && !whiten && !cfg_.enable_key_hpcp_bass_blend;
+        const bool band = band_ok && plain_hpcp && !cfg_.enable_key_hpss_harmonic && cfg_.enable_key_harmonic_mask &&
+                          mask_band_ok((int)cfg_.key_spectrogram_smooth_margin, cfg_.key_harmonic_mask_power) &&
+                          !(cfg_.enable_key_beat_synchronous && !cfg_.enable_key_log_frequency) && hp.pk_lo <= hp.pk_hi;
+        float* d_part = band ? c_.dev<float>("E.kpart", total8 * (uint64_t)((B8 + 63) / 64)) : nullptr;
+        if (band) {
+            launch_mask_band(mags8, ks_, B8, d_kpfx, d_kid, NK, cfg_.key_harmonic_mask_power, hp.pk_lo - 1, hp.pk_hi + 1,
+                             d_part, total8, st2);
+        } else if (cfg_.enable_key_hpss_harmonic) {
             const KeyHpssParams kh = key_hpss_params(cfg_, sr_, B8, fres8, ks_);
             if (kh.nb > 0) {  // an empty band returns the spectrogram unchanged (extractor.rs:1408-1410)
                 std::vector<uint64_t> moff(1, 0), mt(1, 0), at(1, 0);
@@ -1660,22 +1693,17 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
             const HpcpXParams hx = hpcp_x_params(cfg_, sr_, B8, fres8, whiten, ks_);
             launch_hpcp_x(mags8, d_kpfx, d_ktile, d_kid, NK, ktile.back(), hx, d_tune, d_chroma, d_energy, st2);
         } else if (cfg_.enable_key_hpcp) {
-            HpcpParams hp{};
-            hp.B = B8;
-            hp.stride = ks_;
-            hp.pk_lo = 1;
-            hp.pk_hi = 0;
-            band_bins(B8, fres8, sd_maxf(100.0f, 20.0f), sd_minf(5000.0f, (float)sr_ / 2.0f), &hp.pk_lo, &hp.pk_hi);
-            hp.K = (int)std::max<uint64_t>(cfg_.key_hpcp_peaks_per_frame, 1);
-            hp.hmax = (int)std::max<uint64_t>(cfg_.key_hpcp_num_harmonics, 1);
-            hp.p = sd_clampf(cfg_.key_hpcp_mag_power, 0.05f, 1.0f);
             std::vector<HarmEntry> ht =
                 harm_table(B8, sr_, KFS, cfg_.soft_mapping_sigma, hp.hmax, cfg_.key_hpcp_harmonic_decay);
             HarmEntry* d_ht = c_.up(EP + "harm", ht);
             // the table upload is queued on the main stream: order the key stream after it
             kt.mark(10);
             SDSP_HIP_CHECK(hipStreamWaitEvent(st2, kt.ev[10], 0));
-            launch_hpcp(mags8, d_kpfx, d_ktile, d_kid, NK, ktile.back(), hp, d_ht, d_chroma, d_energy, st2);
+            if (band)
+                launch_hpcp_band(mags8, d_kpfx, d_ktile, d_kid, NK, ktile.back(), hp, d_ht, d_part, total8, d_chroma,
+                                 d_energy, st2);
+            else
+                launch_hpcp(mags8, d_kpfx, d_ktile, d_kid, NK, ktile.back(), hp, d_ht, d_chroma, d_energy, st2);
         } else {  // :1169-1197 (the tuned variant only when |offset| > 1e-6)
             const ChromaParams cp = chroma_params(cfg_, sr_, 0, B8, fres8, ks_);
             launch_chroma(0, mags8, d_kpfx, d_ktile, d_kid, NK, ktile.back(), cp, d_tune, d_chroma, d_energy, st2);

@@ -52,11 +52,22 @@ def diff_results(got, ref, tol=TOL):
     return bad
 
 
-def exact_fraction(got, ref):
-    """1.0 when every float field is bit-identical (the design target), else the share that is."""
-    pairs = [(got["bpm"], ref["bpm"]), (got["bpm_confidence"], ref["bpm_confidence"]),
-             (got["key_confidence"], ref["key_confidence"]), (got["key_clarity"], ref["key_clarity"]),
-             (got["grid_stability"], ref["grid_stability"])]
+# The default key path folds each frame's HPCP energy in 64-bin blocks (k_mask_rp / k_hpcp_band,
+# DESIGN.md §2): a GPU-only re-association of one f32 sum (extractor.rs:1133) that the north star's
+# tolerance allows (key exact, confidences within 1e-4).  Against the oracle, key_confidence and
+# key_clarity are then compared within TOL (diff_results) instead of bit for bit; every other field
+# stays bit-identical.  GPU-against-GPU comparisons pass strict=True.
+KEY_ENERGY_FIELDS = ("key_confidence", "key_clarity")
+KEY_ENERGY_REASSOCIATED = True
+
+
+def exact_fraction(got, ref, strict=False):
+    """1.0 when every float field is bit-identical (the design target), else the share that is.
+    strict=False leaves out KEY_ENERGY_FIELDS when KEY_ENERGY_REASSOCIATED (diff_results checks
+    them within TOL)."""
+    skip = () if strict or not KEY_ENERGY_REASSOCIATED else KEY_ENERGY_FIELDS
+    pairs = [(got[k], ref[k]) for k in ("bpm", "bpm_confidence", "key_confidence", "key_clarity", "grid_stability")
+             if k not in skip]
     same = sum(1 for a, b in pairs if np.float32(a).tobytes() == np.float32(b).tobytes())
     a, b = got["beat_grid"]["beats"], ref["beat_grid"]["beats"]
     if len(a) == len(b):
@@ -88,6 +99,25 @@ def result_digest(r):
         "warnings": len(m["confidence_warnings"]),
         "mr": [m["tempogram_multi_res_triggered"], m["tempogram_multi_res_used"]],
     }
+
+
+def digests_match(got, ref, strict=False):
+    """result_digest equality; with the re-associated key energies (strict=False) the
+    KEY_ENERGY_FIELDS compare within TOL, as f32 values from their bits."""
+    skip = () if strict or not KEY_ENERGY_REASSOCIATED else KEY_ENERGY_FIELDS
+    if any(got[k] != ref[k] for k in got if k not in skip):
+        return False
+    f = lambda b: float(np.uint32(b).view(np.float32))
+    return all(abs(f(got[k]) - f(ref[k])) <= TOL for k in skip)
+
+
+def dicts_match(got, ref, strict=False):
+    """Equality of two result dicts as JSON-plain data (the committed golden vectors); with the
+    re-associated key energies (strict=False) the KEY_ENERGY_FIELDS compare within TOL."""
+    skip = () if strict or not KEY_ENERGY_REASSOCIATED else KEY_ENERGY_FIELDS
+    if {k: v for k, v in got.items() if k not in skip} != {k: v for k, v in ref.items() if k not in skip}:
+        return False
+    return all(abs(float(got[k]) - float(ref[k])) <= TOL for k in skip)
 
 
 def samples_digest(x):

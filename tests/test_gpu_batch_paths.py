@@ -99,7 +99,7 @@ def test_config2_shaped_sub_batches(monkeypatch):
         x = buf.to_host(i * L, L)
         assert parity.samples_digest(x) == gold["tracks"][i]["samples"], i  # the same input
         assert not isinstance(res[i], sdsp.AnalysisError), (i, res[i])
-        assert parity.result_digest(res[i]) == gold["tracks"][i]["result"], i
+        assert parity.digests_match(parity.result_digest(res[i]), gold["tracks"][i]["result"]), i
         if i % 8 == 3:
             xs[i] = x
     with cf.ThreadPoolExecutor(8) as ex:

@@ -166,4 +166,4 @@ def test_sub_batches_vs_oracle(monkeypatch, late_join):
     monkeypatch.setenv("SDSP_NO_KEY_DEFER", "1")
     ctl = sdsp.analyze_batch_device(buf.ptr, offs, lens)
     for i, (a, b) in enumerate(zip(got, ctl)):
-        assert not parity.diff_results(a, b) and parity.exact_fraction(a, b) == 1.0, i
+        assert not parity.diff_results(a, b) and parity.exact_fraction(a, b, strict=True) == 1.0, i

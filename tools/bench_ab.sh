@@ -10,7 +10,7 @@ i=0
 for ev in "$@"; do
   i=$((i+1))
   O=$R/gpurun_out/benchab_${tag}_$i
-  env $ev timeout -k 10 240 python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O.json 2> $O.err || { echo "[$ev] failed"; tail -5 $O.err; exit 1; }
+  env $ev timeout -k 10 240 python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-probe > $O.json 2> $O.err || { echo "[$ev] failed"; tail -5 $O.err; exit 1; }
   python3 - "$O.json" "[$ev]" <<'PY'
 import json, sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])

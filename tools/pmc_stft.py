@@ -15,7 +15,7 @@ import json
 import sys
 
 N = int(sys.argv[1])
-KERNEL = "k_stft_slide8<" if N == 8192 else f"k_stft_slide<{N},"  # the 8192-point kernel is its own (k_stft_slide8)
+KERNEL = "k_stft_slide8w3<" if N == 8192 else "k_stft_slide2s<"  # the pipeline's sliding-strip kernels
 
 
 def dispatches(path, name):
@@ -37,7 +37,7 @@ alg = rf["bytes_per_launch"] * nl
 fetch = 2.0 * sum(dispatches(sys.argv[2], "FETCH_SIZE")[:nl])
 write = sum(dispatches(sys.argv[3], "WRITE_SIZE")[:nl])
 print(json.dumps({
-    "kernel": "k_stft_slide8" if N == 8192 else f"k_stft_slide<{N}>",
+    "kernel": "k_stft_slide8w3" if N == 8192 else "k_stft_slide2s",
     "workload": f"bench.py one step, {nl} pipeline launch(es): {json.loads(line)['config']['workload']}",
     "source": f"{sys.argv[2]} (FETCH_SIZE pass), {sys.argv[3]} (WRITE_SIZE pass); "
               "separate rocprofv3 --pmc runs; tools/pmc_stft.py",
