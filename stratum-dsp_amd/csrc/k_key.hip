@@ -242,11 +242,23 @@ __global__ __launch_bounds__(MASK_T) void k_mask_rp(float* __restrict__ mags, in
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
-    for (int64_t base = 0; base < F + M; base += R) {
-        float xv[R];
+    // the next block's loads are issued as soon as the current block's values are consumed, so
+    // they are in flight during the block-sum fold (its 64-step chains would otherwise stall them)
+    float xv[R];
+    auto load_block = [&](int64_t base) {
         if (base >= 2 * M && base + R <= F) {
 #pragma unroll
             for (int u = 0; u < R; u++) xv[u] = live ? __builtin_nontemporal_load(&col[(base + u) * stride]) : 0.0f;
+        } else {
+#pragma unroll
+            for (int u = 0; u < R; u++)
+                xv[u] = (live && base + u < F) ? __builtin_nontemporal_load(&col[(base + u) * stride]) : 0.0f;
+        }
+    };
+    load_block(0);
+    for (int64_t base = 0; base < F + M; base += R) {
+        if (base >= 2 * M && base + R <= F) {
+            // interior block: every step has a full window; no edge conditions
 #pragma unroll
             for (int u = 0; u < R; u++) {
                 prev = prev + xv[u];
@@ -254,25 +266,22 @@ __global__ __launch_bounds__(MASK_T) void k_mask_rp(float* __restrict__ mags, in
                 X[u % RX] = xv[u];
                 emit(P[(u + 1) % R] - P[(u + R - 2 * M) % R], 2 * M + 1, X[(u + 1) % RX], base + u - M, u);
             }
-            fold(base);
-            continue;
-        }
+        } else {
 #pragma unroll
-        for (int u = 0; u < R; u++)
-            xv[u] = (live && base + u < F) ? __builtin_nontemporal_load(&col[(base + u) * stride]) : 0.0f;
-#pragma unroll
-        for (int u = 0; u < R; u++) {
-            const int64_t tin = base + u;
-            prev = prev + xv[u];
-            P[(u + 1) % R] = prev;
-            X[u % RX] = xv[u];
-            const int64_t t = tin - M;
-            if (t >= 0 && t < F) {
-                const int64_t st = t >= M ? t - M : 0;
-                const int64_t en = t + M + 1 < F ? t + M + 1 : F;
-                emit(P[(u + 1) % R] - P[(u + R - 2 * M) % R], en - st, X[(u + 1) % RX], t, u);
+            for (int u = 0; u < R; u++) {
+                const int64_t tin = base + u;
+                prev = prev + xv[u];  // == prev once tin >= F (x = 0)
+                P[(u + 1) % R] = prev;
+                X[u % RX] = xv[u];
+                const int64_t t = tin - M;
+                if (t >= 0 && t < F) {
+                    const int64_t st = t >= M ? t - M : 0;
+                    const int64_t en = t + M + 1 < F ? t + M + 1 : F;
+                    emit(P[(u + 1) % R] - P[(u + R - 2 * M) % R], en - st, X[(u + 1) % RX], t, u);
+                }
             }
         }
+        if (base + R < F + M) load_block(base + R);
         fold(base);
     }
 }
