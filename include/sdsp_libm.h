@@ -285,6 +285,32 @@ SD_HD float sd_logf_ge1_t2(float x, const sd_logtab2_t* tab) {
     return (float)__builtin_fma(ed, SD_LN2_HI, __builtin_fma(ed, SD_LN2_LO, t.lg + p));
 }
 
+/* ln(1 + max(v, 0)) (f32::max: NaN -> 0) as sd_logf_ge1_t2(1 + sd_maxf(v, 0), tab), with the
+ * index, the pivot and the exponent taken by integer selects and +inf by a final select instead
+ * of a branch: x = 1 + max(v, 0) is never NaN, and +inf runs the finite arithmetic harmlessly.
+ * For i >= 53, k = mant - ((i + 1) << 16) = low16 - 2^16, i.e. low16 with the high half set.
+ * The double arithmetic is unchanged; bit-identical on all 2^32 inputs (tools/check_logf_ge1.c). */
+SD_HD float sd_ln1p_max0_t2(float v, const sd_logtab2_t* tab) {
+    const float x = 1.0f + (v > 0.0f ? v : 0.0f);
+    const uint32_t b = sd_bits_f(x);
+    const uint32_t off = (b >> 16) & 0x7fu;
+    const int hi = off >= 53u;
+    const int k = (int)((b & 0xffffu) | (hi ? 0xffff0000u : 0u));
+    const int e = (int)(b >> 23) - (hi ? 126 : 127);
+    const sd_logtab2_t t = tab[off];
+    const double r = (double)k * t.s;
+    double p = -1.0 / 6.0;
+    p = __builtin_fma(p, r, 0.2);
+    p = __builtin_fma(p, r, -0.25);
+    p = __builtin_fma(p, r, 1.0 / 3.0);
+    p = __builtin_fma(p, r, -0.5);
+    p = __builtin_fma(p, r, 1.0);
+    p = p * r;
+    const double ed = (double)e;
+    const float y = (float)__builtin_fma(ed, SD_LN2_HI, __builtin_fma(ed, SD_LN2_LO, t.lg + p));
+    return x < SD_INF_F ? y : x;
+}
+
 /* f32::log10 */
 SD_HD float sd_log10f(float x) {
     if (x != x) return x;

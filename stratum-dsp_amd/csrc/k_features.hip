@@ -147,7 +147,7 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
             const float m = Mt[ro][(c0 + j) & (W - 1)];
             const float cv = cn ? m / mx_c : 0.0f;
             const float pv = __builtin_bit_cast(
-                float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, cv), 0x138, 0xf, 0xf, false));
+                float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, cv), 0x138, 0xf, 0xf, true));
             const float d = max_bnn(cv - pv, 0.0f);
             so += d * d;
         }
@@ -204,7 +204,7 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
         for (int u = 0; u < NLD; u++) {
             const int r = wrow + sub + u * RSTEP;
             Mt[r][slot] = nx[u];
-            Lt[r][slot] = sd_logf_ge1_t2(1.0f + sd_maxf(nx[u], 0.0f), ltab);
+            Lt[r][slot] = sd_ln1p_max0_t2(nx[u], ltab);
         }
     };
     __syncthreads();  // ltab; from here on each wave works on its own rows
@@ -272,19 +272,23 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
                     constexpr bool MEL = decltype(mel_tag)::value;
                     MelChunk mc{};
                     if constexpr (MEL) mc = P.mel_chunks[c0 / CW];
+                    // (float) b from the chunk's scalar-loaded weights: no conversion per bin
+                    float bfv[CW];
+#pragma unroll
+                    for (int j = 0; j < CW; j++) bfv[j] = P.mel_chunks[c0 / CW].bf[j];
 #pragma unroll
                     for (int j = 0; j < CW; j++) {
                         const int b = c0 + j;
                         const int s = b & (W - 1);
                         const float m = Mt[ro][s];
                         const float ee = m * m;
-                        const float hh = (float)b * m * m;
+                        const float hh = bfv[j] * m * m;
                         e[0] += ee;
                         h[0] += hh;
                         const float lc = Lt[ro][s];
                         const float cv = quot(m);
                         const float pv = __builtin_bit_cast(
-                            float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, cv), 0x138, 0xf, 0xf, false));
+                            float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, cv), 0x138, 0xf, 0xf, true));
                         const float d = max_bnn(cv - pv, 0.0f);
                         so += d * d;
                         const float df = max_bnn(lc - Wm[j], 0.0f);
@@ -350,7 +354,7 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
             // f - 1 for every lane that reads it: lanes 1-63; the helper's value is unused)
             const float cv = quot(m);
             const float pv = __builtin_bit_cast(
-                float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, cv), 0x138 /* wave_shr:1 */, 0xf, 0xf, false));
+                float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, cv), 0x138 /* wave_shr:1 */, 0xf, 0xf, true));
             if (P.n_mels > 0) {
                 const MelPlan mp = mel[b];
                 for (int q = 0; q < mp.nflush; q++) {

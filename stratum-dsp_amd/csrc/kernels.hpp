@@ -17,6 +17,7 @@ constexpr int NVAR = 5;  // novelty variants: full, low, mid, high, mel
 struct MelChunk {
     uint32_t bits;
     float w0[8], w1[8];
+    float bf[8];  // (float) b of the chunk's bins, the HFC weights (every chunk, mel or not)
 };
 struct FeatParams {
     int B;             // bins per frame (nfft/2+1)
@@ -30,7 +31,7 @@ struct FeatParams {
     // SuperFlux window, no mel work, full chunk)
     const int* chunk_flags;
     // FT_CHUNK_MEL chunks (bit 3: as FT_CHUNK_FAST, but with mel work): the chunk's 8 mel plans
-    // packed (MelChunk), indexed by chunk
+    // packed (MelChunk), indexed by chunk; its bf (HFC weights) is read by every fast chunk
     const MelChunk* mel_chunks;
 };
 constexpr int FT_CHUNK_FAST = 4, FT_CHUNK_MEL = 8;

@@ -1180,6 +1180,7 @@ void Pipeline::tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPa
             const int v0 = band_of(c0);
             bool fast = fp.K == 4 && c0 + 8 <= B, mel = false, mel_ok = true;
             MelChunk& m = mc[(size_t)c0 / 8];
+            for (int j = 0; j < 8; j++) m.bf[j] = (float)(c0 + j);
             for (int b = c0; fast && b < c0 + 8; b++) {
                 const int v = band_of(b);
                 if (v != v0) fast = false;

@@ -1,5 +1,7 @@
-/* Exhaustive check: sd_logf_ge1_t2 (two-column table, no m / c formed) against sd_logf_ge1 on
- * every f32 >= 1 (finite, +inf) and a NaN.  gcc -O2 -ffp-contract=off -march=x86-64-v3 -fopenmp */
+/* Exhaustive checks: sd_logf_ge1_t2 (two-column table, no m / c formed) against sd_logf_ge1 on
+ * every f32 >= 1 (finite, +inf) and a NaN; sd_ln1p_max0_t2(v) against
+ * sd_logf_ge1_t2(1 + sd_maxf(v, 0)) on all 2^32 bit patterns of v.
+ * gcc -O2 -ffp-contract=off -march=x86-64-v3 -fopenmp */
 #include <stdio.h>
 #include <stdint.h>
 #include "../include/sdsp_libm.h"
@@ -20,5 +22,18 @@ int main(void) {
         }
     }
     printf("f32 >= 1: %lld inputs, %lld differ (last 0x%08x)\n", n, diff, first);
-    return diff != 0;
+    long long diff2 = 0, n2 = 0;
+    uint32_t first2 = 0;
+#pragma omp parallel for reduction(+ : diff2, n2) schedule(static, 1 << 20)
+    for (long long u = 0; u <= 0xffffffffLL; u++) {
+        const float v = sd_from_bits_f((uint32_t)u);
+        const float a = sd_logf_ge1_t2(1.0f + sd_maxf(v, 0.0f), t2), b = sd_ln1p_max0_t2(v, t2);
+        n2++;
+        if (sd_bits_f(a) != sd_bits_f(b)) {
+            diff2++;
+            first2 = (uint32_t)u;
+        }
+    }
+    printf("ln(1 + max(v, 0)), all v: %lld inputs, %lld differ (last 0x%08x)\n", n2, diff2, first2);
+    return diff != 0 || diff2 != 0;
 }
