@@ -38,11 +38,17 @@ namespace sdsp {
 
 
 
+// the per-chunk tables (flags, packed mel plans, HFC weights) through the constant address space:
+// the kernel never writes them, so they come in by scalar loads into SGPRs (through a generic
+// pointer the compiler cannot prove that and loads them per lane, then reads the first lane)
+typedef const __attribute__((address_space(4))) int* ConstI;
+typedef const __attribute__((address_space(4))) MelChunk* ConstMC;
+
 // KK > 0: compile-time SuperFlux half width (the default 4) -- the previous frame's logs for
 // the chunk's windows are read once into registers and every bin's window max is taken from
 // them; KK = 0: runtime P.K with the per-bin window loop.
 template <int CW, int W, int KK>
-__global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
+__global__ __launch_bounds__(FT_FRAMES) __attribute__((amdgpu_waves_per_eu(KK > 0 ? 3 : 1))) void k_features(const RowMap rm,
                                                         const uint64_t* __restrict__ frame_pfx,
                                                         const uint64_t* __restrict__ tile_pfx, int T, FeatParams P,
                                                         const MelPlan* __restrict__ mel, float* __restrict__ E,
@@ -97,12 +103,12 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
     };
     float accA = 0.0f, accB = 0.0f;
     int mA = 0;
-    // MEL row m as a buffer resource of `total` floats; lanes without a frame get an offset past
+    float* melA = MEL;  // MEL row mA (wave-uniform, advanced with mA)
+    // MEL row mA as a buffer resource of `total` floats; lanes without a frame get an offset past
     // it, so their stores are dropped (no exec-mask branch per flush)
     const uint32_t mel_vo = valid ? (uint32_t)g * 4u : 0xFFFFFFF0u;
-    auto mel_rsrc = [&](int m) {
-        return __builtin_amdgcn_make_buffer_rsrc((void*)(MEL + (uint64_t)m * total), (short)0,
-                                                 (int)(uint32_t)(total * 4u), 0x00020000);
+    auto mel_rsrc = [&]() {
+        return __builtin_amdgcn_make_buffer_rsrc((void*)melA, (short)0, (int)(uint32_t)(total * 4u), 0x00020000);
     };
     // frame f of this track lives in row (f even ? A : B) r0 + (f >> 1) * step (RowMap)
     const uint64_t ra0 = rm.rowA0[trk], rb0 = rm.rowB0 ? rm.rowB0[trk] : ra0 + (uint64_t)rm.offB;
@@ -258,7 +264,7 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
             // hoisted to the chunk, so the walk issues no scalar work per bin; a mel chunk
             // (FT_CHUNK_MEL, the 30-8000 Hz range) adds the mel sums from the chunk's packed plan
             // (7.63 -> 7.17 ms per launch against the general walk for those chunks)
-            const int cf = P.chunk_flags[c0 / CW];
+            const int cf = ((ConstI)P.chunk_flags)[c0 / CW];
             if (cf & (FT_CHUNK_FAST | FT_CHUNK_MEL)) {
                 const int vbc = cf & 3;
                 if (vbc != cur) {
@@ -268,14 +274,20 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
                 const float so_start = so;
                 // MEL: the chunk's mel plans come in one scalar load; a flush stores accA through a
                 // buffer resource whose record count drops the stores of lanes without a frame
-                auto walk = [&](auto mel_tag) {
+                auto walk = [&](auto mel_tag, auto reg_tag) {
                     constexpr bool MEL = decltype(mel_tag)::value;
+                    constexpr bool REG = decltype(reg_tag)::value;
                     MelChunk mc{};
-                    if constexpr (MEL) mc = P.mel_chunks[c0 / CW];
+                    const ConstMC mcp = (ConstMC)P.mel_chunks + c0 / CW;
+                    if constexpr (MEL) {
+                        mc.bits = mcp->bits;
+#pragma unroll
+                        for (int j = 0; j < CW; j++) mc.w0[j] = mcp->w0[j], mc.w1[j] = mcp->w1[j];
+                    }
                     // (float) b from the chunk's scalar-loaded weights: no conversion per bin
                     float bfv[CW];
 #pragma unroll
-                    for (int j = 0; j < CW; j++) bfv[j] = P.mel_chunks[c0 / CW].bf[j];
+                    for (int j = 0; j < CW; j++) bfv[j] = mcp->bf[j];
 #pragma unroll
                     for (int j = 0; j < CW; j++) {
                         const int b = c0 + j;
@@ -302,27 +314,35 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
                         if constexpr (MEL) {
                             const uint32_t pb = mc.bits >> (4 * j);
                             for (uint32_t q = pb & 3; q > 0; q--) {
-                                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(accA), mel_rsrc(mA), mel_vo, 0, 0);
+                                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(accA), mel_rsrc(), mel_vo, 0, 0);
                                 accA = accB;
                                 accB = 0.0f;
                                 mA++;
+                                melA += total;
                             }
                             // as the general walk: L >= +0, so w = 0 terms are skipped, not added
-                            if (mc.w0[j] != 0.0f) {
+                            // (L = +inf would make them NaN).  REG (FT_CHUNK_MELREG): w0 goes to
+                            // accA and w1 to accB on every bin of the chunk, no accumulator select
+                            if constexpr (REG) {
+                                if (__float_as_uint(mc.w0[j]) << 1) accA += lc * mc.w0[j];
+                                if (__float_as_uint(mc.w1[j]) << 1) accB += lc * mc.w1[j];
+                            } else if (mc.w0[j] != 0.0f) {
                                 if (pb & 4) accB += lc * mc.w0[j];
                                 else accA += lc * mc.w0[j];
                             }
-                            if (mc.w1[j] != 0.0f) {
+                            if (!REG && mc.w1[j] != 0.0f) {
                                 if (pb & 8) accB += lc * mc.w1[j];
                                 else accA += lc * mc.w1[j];
                             }
                         }
                     }
                 };
-                if (cf & FT_CHUNK_MEL)
-                    walk(std::true_type{});
+                if (cf & FT_CHUNK_MELREG)
+                    walk(std::true_type{}, std::true_type{});
+                else if (cf & FT_CHUNK_MEL)
+                    walk(std::true_type{}, std::false_type{});
                 else
-                    walk(std::false_type{});
+                    walk(std::false_type{}, std::false_type{});
                 quot_redo(c0, CW, so_start);
                 continue;
             }
@@ -362,6 +382,7 @@ __global__ __launch_bounds__(FT_FRAMES) void k_features(const RowMap rm,
                     accA = accB;
                     accB = 0.0f;
                     mA++;
+                    melA += total;
                 }
                 // novelty.rs:181-186 skips v <= 0.  Here v = lc >= +0 always (sd_maxf maps NaN to 0,
                 // as f32::max), so the skipped terms are +0 * w = +0, and adding +0 to a

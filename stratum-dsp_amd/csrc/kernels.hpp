@@ -34,7 +34,8 @@ struct FeatParams {
     // packed (MelChunk), indexed by chunk; its bf (HFC weights) is read by every fast chunk
     const MelChunk* mel_chunks;
 };
-constexpr int FT_CHUNK_FAST = 4, FT_CHUNK_MEL = 8;
+// FT_CHUNK_MELREG (with FT_CHUNK_MEL): every bin's w0 goes to accumulator 0 and w1 to 1 (or is 0)
+constexpr int FT_CHUNK_FAST = 4, FT_CHUNK_MEL = 8, FT_CHUNK_MELREG = 16;
 // per-bin mel accumulation plan (k_features): flush `nflush` finished mels before the bin,
 // then, in the reference's contribution order, add L*w0 to accumulator s0 and L*w1 to s1
 // (accumulator 0 = mel mA, 1 = mel mA+1; w = 0 means no contribution)

@@ -1178,7 +1178,7 @@ void Pipeline::tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPa
         std::vector<MelChunk> mc((size_t)(B + 7) / 8 + 1, MelChunk{});
         for (int c0 = 0; c0 < B; c0 += 8) {
             const int v0 = band_of(c0);
-            bool fast = fp.K == 4 && c0 + 8 <= B, mel = false, mel_ok = true;
+            bool fast = fp.K == 4 && c0 + 8 <= B, mel = false, mel_ok = true, mel_reg = true;
             MelChunk& m = mc[(size_t)c0 / 8];
             for (int j = 0; j < 8; j++) m.bf[j] = (float)(c0 + j);
             for (int b = c0; fast && b < c0 + 8; b++) {
@@ -1192,6 +1192,7 @@ void Pipeline::tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPa
                     const MelPlan& q = mplan[(size_t)b];
                     if (q.nflush != 0 || q.w0 != 0.0f || q.w1 != 0.0f) mel = true;
                     if (q.nflush < 0 || q.nflush > 3 || (q.s0 & ~1) || (q.s1 & ~1)) mel_ok = false;
+                    if ((q.w0 != 0.0f && q.s0 != 0) || (q.w1 != 0.0f && q.s1 != 1)) mel_reg = false;
                     const int j = b - c0;
                     m.bits |= (uint32_t)(q.nflush & 3) << (4 * j) | (uint32_t)(q.s0 & 1) << (4 * j + 2) |
                               (uint32_t)(q.s1 & 1) << (4 * j + 3);
@@ -1199,7 +1200,8 @@ void Pipeline::tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPa
                     m.w1[j] = q.w1;
                 }
             }
-            cf[(size_t)c0 / 8] = v0 | (fast && !mel ? FT_CHUNK_FAST : 0) | (fast && mel && mel_ok ? FT_CHUNK_MEL : 0);
+            cf[(size_t)c0 / 8] = v0 | (fast && !mel ? FT_CHUNK_FAST : 0) | (fast && mel && mel_ok ? FT_CHUNK_MEL : 0) |
+                                 (fast && mel && mel_ok && mel_reg ? FT_CHUNK_MELREG : 0);
         }
         fp.chunk_flags = c_.up(tag + "ftchunk", cf);
         fp.mel_chunks = c_.up(tag + "ftmelchunk", mc);
