@@ -193,6 +193,16 @@ __global__ __launch_bounds__(MASK_T) void k_mask_r(float* __restrict__ mags, int
 // association differs from the reference's one sequential sum over 4,097 bins (a GPU-only
 // re-association of the key energies); every masked value is bit-identical.
 // Lanes past the last bin stay in the wave and contribute +0 (exact: the sums are >= +0).
+// max_bnn(v, 0) for a v that is never a signalling NaN (the spectrogram and everything computed
+// from it are results of arithmetic, whose NaNs are quiet): the IEEE-mode v_max_f32 already returns
+// 0 for a quiet NaN and +0 for -0, so the canonicalising max the compiler adds in front of a value
+// it cannot see the origin of (a load, a phi) is left out
+__device__ __forceinline__ float max0_quiet(float v) {
+    float r;
+    asm("v_max_f32 %0, 0, %1" : "=v"(r) : "v"(v));
+    return r;
+}
+
 template <int M, int PW>
 __global__ __launch_bounds__(MASK_T) void k_mask_rp(float* __restrict__ mags, int stride, int B,
                                                      const uint64_t* __restrict__ frame_pfx,
@@ -211,7 +221,17 @@ __global__ __launch_bounds__(MASK_T) void k_mask_rp(float* __restrict__ mags, in
     if (F <= 0) return;  // the whole workgroup
     const bool live = b < B;
     const bool keep = live && b >= st_lo && b <= st_hi;
-    float* col = mags + frame_pfx[trk] * (uint64_t)stride + (live ? b : 0);
+    // Rows are addressed through buffer resources whose base is the row (wave-uniform, advanced in
+    // SGPRs) and lane offsets in VGPRs: no 64-bit address arithmetic per element.  A store
+    // resource spans one row (B floats) and the lanes off HPCP's band carry an offset past it, so
+    // the hardware drops their stores without an exec-mask branch per element.
+    float* const trk0 = mags + frame_pfx[trk] * (uint64_t)stride;
+    const uint32_t lvo = (uint32_t)(live ? b : 0) * 4u;
+    const uint32_t svo = keep ? (uint32_t)b * 4u : 0x80000000u;
+    const uint32_t rowb = (uint32_t)stride * 4u;
+    auto row_rsrc = [&](int64_t row, uint32_t bytes) {
+        return __builtin_amdgcn_make_buffer_rsrc((void*)(trk0 + row * (int64_t)stride), (short)0, (int)bytes, 0x00020000);
+    };
     float* pg = part + (uint64_t)gblk * total + frame_pfx[trk];
     const float p = sd_maxf(power, 1.0f);
     const float inv_w = 1.0f / (float)(2 * M + 1);
@@ -221,10 +241,27 @@ __global__ __launch_bounds__(MASK_T) void k_mask_rp(float* __restrict__ mags, in
 #pragma unroll
     for (int j = 0; j < RX; j++) X[j] = 0.0f;
     float prev = 0.0f;
-    auto emit = [&](float a, int64_t den, float xr, int64_t t, int u) {
-        const float v = mask_elem<M, PW>(a, den, xr, p, inv_w);
-        if (keep) __builtin_nontemporal_store(v, &col[t * stride]);
+    auto finish = [&](float v, int64_t t, int u) {
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), row_rsrc(t, (uint32_t)B * 4u), svo, 0, 2 /* nt */);
         tile[u][lane] = live ? v * v : 0.0f;
+    };
+    // interior element: the full window's quotient by the product + FMA correction, exact on
+    // {0} U [2^-90, 2^120] (mask_elem); a wave with a lane outside that range (tiny non-zero or huge
+    // window sums) redoes that lane by the IEEE division, behind a wave-uniform branch
+    auto emit_full = [&](float a, float xr, int64_t t, int u) {
+        const float q0 = a * inv_w;
+        float hm = __builtin_fmaf(__builtin_fmaf(-q0, (float)(2 * M + 1), a), inv_w, q0);
+        // outside {+-0} U [2^-90, 2^120] (negative, NaN: sign or exponent bits above the range)
+        const uint32_t ab = __float_as_uint(a);
+        const bool bad = ((ab << 1) != 0u) & (ab - 0x12800000u > 0x7B800000u - 0x12800000u);
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0))
+            if (bad) hm = a / (float)(2 * M + 1);
+        const float x = max0_quiet(xr);
+        const float h = max0_quiet(hm);
+        const float r = max_bnn(x - h, 0.0f);
+        const float hp = mask_pow<PW>(h, p);
+        const float rp = mask_pow<PW>(r, p);
+        finish(x * (hp / (hp + rp + 1e-12f)), t, u);
     };
     // the block's partial sums: lane u folds the 64 squares of frame base + u - M in bin order
     auto fold = [&](int64_t base) {
@@ -246,13 +283,16 @@ __global__ __launch_bounds__(MASK_T) void k_mask_rp(float* __restrict__ mags, in
     // they are in flight during the block-sum fold (its 64-step chains would otherwise stall them)
     float xv[R];
     auto load_block = [&](int64_t base) {
+        const auto rs = row_rsrc(base, 0x7FFFFFFFu);
         if (base >= 2 * M && base + R <= F) {
 #pragma unroll
-            for (int u = 0; u < R; u++) xv[u] = live ? __builtin_nontemporal_load(&col[(base + u) * stride]) : 0.0f;
+            for (int u = 0; u < R; u++)
+                xv[u] = live ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, lvo, (uint32_t)u * rowb, 2)) : 0.0f;
         } else {
 #pragma unroll
             for (int u = 0; u < R; u++)
-                xv[u] = (live && base + u < F) ? __builtin_nontemporal_load(&col[(base + u) * stride]) : 0.0f;
+                xv[u] = (live && base + u < F) ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, lvo, (uint32_t)u * rowb, 2))
+                                               : 0.0f;
         }
     };
     load_block(0);
@@ -264,7 +304,7 @@ __global__ __launch_bounds__(MASK_T) void k_mask_rp(float* __restrict__ mags, in
                 prev = prev + xv[u];
                 P[(u + 1) % R] = prev;
                 X[u % RX] = xv[u];
-                emit(P[(u + 1) % R] - P[(u + R - 2 * M) % R], 2 * M + 1, X[(u + 1) % RX], base + u - M, u);
+                emit_full(P[(u + 1) % R] - P[(u + R - 2 * M) % R], X[(u + 1) % RX], base + u - M, u);
             }
         } else {
 #pragma unroll
@@ -277,7 +317,8 @@ __global__ __launch_bounds__(MASK_T) void k_mask_rp(float* __restrict__ mags, in
                 if (t >= 0 && t < F) {
                     const int64_t st = t >= M ? t - M : 0;
                     const int64_t en = t + M + 1 < F ? t + M + 1 : F;
-                    emit(P[(u + 1) % R] - P[(u + R - 2 * M) % R], en - st, X[(u + 1) % RX], t, u);
+                    finish(mask_elem<M, PW>(P[(u + 1) % R] - P[(u + R - 2 * M) % R], en - st, X[(u + 1) % RX], p, inv_w),
+                           t, u);
                 }
             }
         }
