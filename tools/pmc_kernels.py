@@ -17,9 +17,14 @@ import re
 import sys
 
 F8, B8, B2 = 15488, 4097, 1025
+BAND, NBLK = 912, 65  # default key path at 44.1 kHz: HPCP's peak band [18, 929] and 65 64-bin block sums
 KERNELS = {
     "k_mask_r": lambda grid: grid / (65 * 64) * F8 * B8 * 4 * 2,
     "k_hpcp": lambda grid: grid * B8 * 4,
+    # band path: the mask reads every bin, writes the band and the block sums;
+    # HPCP reads the band and the block sums
+    "k_mask_rp": lambda grid: grid / (65 * 64) * F8 * (B8 + BAND + NBLK) * 4,
+    "k_hpcp_band": lambda grid: grid * (BAND + NBLK) * 4,
     "k_features": lambda grid: grid / 256 * 252 * B2 * 4,
 }
 
