@@ -476,7 +476,10 @@ __global__ __launch_bounds__(HP_FRAMES) SDSP_HPCP_ATTR void k_hpcp(const float* 
 // k_hpcp_band: k_hpcp after k_mask_rp.  The frame energy folds the 65 block sums part[g][frame] in
 // block order; the bin walk covers only the band k_mask_rp stored, [pk_lo - 1, pk_hi + 1] (the
 // local-maximum test of candidate c reads bins c - 1 .. c + 1; starting the walk at pk_lo - 1 with
-// the walk's zero history gives exactly k_hpcp's candidates).
+// the walk's zero history gives exactly k_hpcp's candidates).  Each wave stages the 64 rows of its
+// own frames, so the waves run without workgroup barriers: a wave whose frames insert more peaks
+// does not hold the others at a barrier per chunk (a wave's LDS operations execute in order; a
+// wave-level fence keeps the staging writes and the walk's reads in program order).
 template <int KCAP>
 __global__ __launch_bounds__(HP_FRAMES) SDSP_HPCP_ATTR void k_hpcp_band(const float* __restrict__ mags,
                                                          const uint64_t* __restrict__ frame_pfx,
@@ -486,6 +489,7 @@ __global__ __launch_bounds__(HP_FRAMES) SDSP_HPCP_ATTR void k_hpcp_band(const fl
                                                          const float* __restrict__ part, int n_blocks, uint64_t total,
                                                          float* __restrict__ chroma, float* __restrict__ energy) {
     __shared__ float tile[HP_FRAMES][HP_CW + 1];
+    __shared__ float pcs[12][HP_FRAMES];  // pitch-class accumulators (a column per thread)
     const uint64_t gb = blockIdx.x;
     const int it = find_track(tile_pfx, n_items, gb);
     const int trk = tracks[it];
@@ -494,6 +498,9 @@ __global__ __launch_bounds__(HP_FRAMES) SDSP_HPCP_ATTR void k_hpcp_band(const fl
     const int i = threadIdx.x;
     const int64_t f = f0 + i;
     const bool valid = f < F;
+    const int lane = i & 63, wrow = i & ~63;
+    const int64_t rows = F - f0 < HP_FRAMES ? F - f0 : HP_FRAMES;
+    if (wrow >= rows) return;  // the whole wave is past the track's end
     const uint64_t g0 = frame_pfx[trk];
     HpcpFrame<KCAP> hf;
     hf.init();
@@ -503,11 +510,11 @@ __global__ __launch_bounds__(HP_FRAMES) SDSP_HPCP_ATTR void k_hpcp_band(const fl
         for (int g = 0; g < n_blocks; g++) e += pp[(uint64_t)g * total];
         hf.e = e;
     }
-    const int sub = i / HP_CW, jj = i % HP_CW;
-    const int64_t rows = F - f0 < HP_FRAMES ? F - f0 : HP_FRAMES;
-    constexpr int NLD = HP_CW;
-    constexpr int RSTEP = HP_FRAMES / HP_CW;
-    const float* rowp = mags + (g0 + (uint64_t)f0 + (uint64_t)sub) * (uint64_t)P.stride + jj;
+    // lane (sub, jj) stages column jj of rows wrow + sub + RSTEP u of its own wave
+    constexpr int RSTEP = 64 / HP_CW;
+    constexpr int NLD = 64 / RSTEP;
+    const int sub = lane / HP_CW, jj = lane % HP_CW;
+    const float* rowp = mags + (g0 + (uint64_t)f0 + (uint64_t)(wrow + sub)) * (uint64_t)P.stride + jj;
     const uint64_t rstride = (uint64_t)RSTEP * (uint64_t)P.stride;
     const int w_lo = P.pk_lo - 1 > 0 ? P.pk_lo - 1 : 0, w_hi = P.pk_hi + 1 < P.B - 1 ? P.pk_hi + 1 : P.B - 1;
     float nx[NLD];
@@ -515,21 +522,25 @@ __global__ __launch_bounds__(HP_FRAMES) SDSP_HPCP_ATTR void k_hpcp_band(const fl
         const bool col_ok = c0 + jj <= w_hi;
 #pragma unroll
         for (int u = 0; u < NLD; u++)
-            nx[u] = (sub + u * RSTEP < rows && col_ok) ? rowp[(uint64_t)u * rstride + c0] : 0.0f;
+            nx[u] = (wrow + sub + u * RSTEP < rows && col_ok) ? rowp[(uint64_t)u * rstride + c0] : 0.0f;
+    };
+    auto wave_sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
     if (w_lo <= w_hi) load_chunk(w_lo);
     for (int c0 = w_lo; c0 <= w_hi; c0 += HP_CW) {
-        __syncthreads();
+        wave_sync();  // the previous chunk's walk has read its rows
 #pragma unroll
-        for (int u = 0; u < NLD; u++) tile[sub + u * RSTEP][jj] = nx[u];
-        __syncthreads();
+        for (int u = 0; u < NLD; u++) tile[wrow + sub + u * RSTEP][jj] = nx[u];
+        wave_sync();
         if (c0 + HP_CW <= w_hi) load_chunk(c0 + HP_CW);
         if (!valid) continue;
         hf.template walk<false>(tile[i], c0, w_hi + 1 - c0 < HP_CW ? w_hi + 1 - c0 : HP_CW, P);
     }
-    __syncthreads();
     if (!valid) return;
-    hf.finish(reinterpret_cast<float(*)[HP_FRAMES]>(&tile[0][0]), i, P, harm, chroma, energy, g0 + (uint64_t)f);
+    hf.finish(pcs, i, P, harm, chroma, energy, g0 + (uint64_t)f);
 }
 
 // ----------------------------------------------------------------------------------------
