@@ -1590,6 +1590,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     // SDSP_SERIAL_STREAMS=1 keeps the key path on the main stream (per-kernel profiling)
     static const bool serial_streams = std::getenv("SDSP_SERIAL_STREAMS") != nullptr;
     hipStream_t st2 = serial_streams ? st : d_.stream2;
+    hipStream_t st3 = serial_streams ? st : d_.stream3;  // the key vote
     float* d_tune = nullptr;  // per key track tuning offset (tuning compensation)
     float* mags8 = nullptr;
     uint64_t* d_kpfx = nullptr;
@@ -1689,6 +1690,9 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         }
         float* d_chroma = c_.dev<float>("E.chroma", total8 * 12);
         float* d_energy = c_.dev<float>("E.energy", total8);
+        // the previous sub-batch's key vote (stream3) reads E.chroma / E.energy: the producers
+        // below wait for it (an event never recorded counts as complete)
+        SDSP_HIP_CHECK(hipStreamWaitEvent(st2, d_.vote_done, 0));
         if (use_log) {  // :1120-1131
             const ChromaParams cp = chroma_params(cfg_, sr_, 1, B8, fres8, ks_);
             launch_chroma(1, mags8, d_kpfx, d_ktile, d_kid, NK, ktile.back(), cp, nullptr, d_chroma, d_energy, st2);
@@ -1747,13 +1751,16 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         float* d_w = c_.dev<float>("E.weights", total8);
         float* d_sscr = c_.dev<float>("E.segscr", std::max<uint64_t>(kseg.back(), 1));
         d_kout = c_.dev<KeyOut>(EP + "kout", (size_t)NK);
-        // the template upload above is on the main stream too
+        // the template upload above is on the main stream too; the vote follows the chroma on st2
         kt.mark(8);
-        SDSP_HIP_CHECK(hipStreamWaitEvent(st2, kt.ev[8], 0));
+        kt.mark(11, st2);
+        SDSP_HIP_CHECK(hipStreamWaitEvent(st3, kt.ev[8], 0));
+        SDSP_HIP_CHECK(hipStreamWaitEvent(st3, kt.ev[11], 0));
         d_kdbg = dbg_on ? c_.dev<KeyDbg>(EP + "kdbg", (size_t)NK) : nullptr;
-        launch_key_vote(d_kid, NK, d_kpfx, d_chroma, d_energy, d_cs, d_w, d_sscr, d_kseg, d_tpl, kp, d_kout, st2, d_kdbg);
+        launch_key_vote(d_kid, NK, d_kpfx, d_chroma, d_energy, d_cs, d_w, d_sscr, d_kseg, d_tpl, kp, d_kout, st3, d_kdbg);
         SDSP_HIP_CHECK(hipGetLastError());
-        kt.mark(2, st2);
+        kt.mark(2, st3);
+        SDSP_HIP_CHECK(hipEventRecord(d_.vote_done, st3));
         times_.stft8192_launches += 1;
         times_.stft8192_bytes += key_in_bytes + 4.0 * (double)total8 * (double)B8;
     }

@@ -50,7 +50,11 @@ DeviceCtx& device_ctx(int device) {
         SDSP_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
         SDSP_HIP_CHECK(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi));
         SDSP_HIP_CHECK(hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, lo));
-        for (hipStream_t s : {c->stream, c->stream2}) c->own.push_back(s);
+        // k_key_vote (one 256-thread workgroup per track: latency-bound, a few waves per CU) runs on
+        // its own stream so the next sub-batch's 8192-point STFT and mask need not wait behind it
+        SDSP_HIP_CHECK(hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, lo));
+        SDSP_HIP_CHECK(hipEventCreateWithFlags(&c->vote_done, hipEventDisableTiming));
+        for (hipStream_t s : {c->stream, c->stream2, c->stream3}) c->own.push_back(s);
     }
     return *c;
 }

@@ -79,6 +79,8 @@ struct DeviceCtx {
     int device = 0;
     hipStream_t stream = nullptr;   // main (tempo / beat) stream
     hipStream_t stream2 = nullptr;  // key-path stream, forked from and joined to `stream`
+    hipStream_t stream3 = nullptr;  // key vote (k_key_vote), forked from stream2 after the chroma
+    hipEvent_t vote_done = nullptr;  // the last key vote's end: the next chroma producer waits on it
     std::vector<hipStream_t> own;   // the streams above
     std::mutex mu;
     std::map<int, std::unique_ptr<FftTables>> fft;  // keyed by real FFT size N
