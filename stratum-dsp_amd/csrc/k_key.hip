@@ -415,14 +415,16 @@ struct HpcpFrame {
     }
 };
 
-// 4 waves per SIMD (128 VGPRs for KCAP = 24, a 16-byte spill outside the bin walk): 8 % faster
-// than the 129-VGPR / 3-wave build in the serial profile (14.6 vs 15.9 ms per 256-track launch)
+// 4 waves per SIMD: round 3 measured it 8 % faster than the 3-wave build (14.6 vs 15.9 ms per
+// 256-track launch, then at 128 VGPRs with a 16-byte spill); with per-wave staging and the
+// pitch-class scratch in its own LDS array the HPCP kernels take 112 VGPRs, no spill
 #ifndef SDSP_HPCP_ATTR
 #define SDSP_HPCP_ATTR __attribute__((amdgpu_waves_per_eu(4)))
 #endif
 // One thread per frame, HP_FRAMES frames per workgroup.  Bins are staged through LDS in
 // HP_CW-column chunks (coalesced row segments) and each thread walks its frame's bins in
-// order (HpcpFrame).
+// order (HpcpFrame).  Each wave stages the rows of its own 64 frames, so no workgroup barrier
+// holds the waves together per chunk (as k_hpcp_band).
 template <int KCAP>
 __global__ __launch_bounds__(HP_FRAMES) SDSP_HPCP_ATTR void k_hpcp(const float* __restrict__ mags,
                                                     const uint64_t* __restrict__ frame_pfx,
@@ -431,6 +433,7 @@ __global__ __launch_bounds__(HP_FRAMES) SDSP_HPCP_ATTR void k_hpcp(const float* 
                                                     const HarmEntry* __restrict__ harm, float* __restrict__ chroma,
                                                     float* __restrict__ energy) {
     __shared__ float tile[HP_FRAMES][HP_CW + 1];
+    __shared__ float pcs[12][HP_FRAMES];  // pitch-class accumulators (a column per thread)
     const uint64_t gb = blockIdx.x;
     const int it = find_track(tile_pfx, n_items, gb);
     const int trk = tracks[it];
@@ -439,38 +442,42 @@ __global__ __launch_bounds__(HP_FRAMES) SDSP_HPCP_ATTR void k_hpcp(const float* 
     const int i = threadIdx.x;
     const int64_t f = f0 + i;
     const bool valid = f < F;
+    const int lane = i & 63, wrow = i & ~63;
+    const int64_t rows = F - f0 < HP_FRAMES ? F - f0 : HP_FRAMES;
+    if (wrow >= rows) return;  // the whole wave is past the track's end
     const uint64_t g0 = frame_pfx[trk];
     HpcpFrame<KCAP> hf;
     hf.init();
-    const int sub = i / HP_CW, jj = i % HP_CW;
-    const int64_t rows = F - f0 < HP_FRAMES ? F - f0 : HP_FRAMES;
+    constexpr int RSTEP = 64 / HP_CW;
+    constexpr int NLD = 64 / RSTEP;
+    const int sub = lane / HP_CW, jj = lane % HP_CW;
     // software pipeline: chunk c0+HP_CW is loaded into registers while chunk c0 is walked
-    constexpr int NLD = HP_FRAMES * HP_CW / HP_FRAMES;  // loads per thread per chunk
-    constexpr int RSTEP = HP_FRAMES / HP_CW;
-    const float* rowp = mags + (g0 + (uint64_t)f0 + (uint64_t)sub) * (uint64_t)P.stride + jj;
+    const float* rowp = mags + (g0 + (uint64_t)f0 + (uint64_t)(wrow + sub)) * (uint64_t)P.stride + jj;
     const uint64_t rstride = (uint64_t)RSTEP * (uint64_t)P.stride;
     float nx[NLD];
     auto load_chunk = [&](int c0) {
         const bool col_ok = c0 + jj < P.B;
 #pragma unroll
         for (int u = 0; u < NLD; u++)
-            nx[u] = (sub + u * RSTEP < rows && col_ok) ? rowp[(uint64_t)u * rstride + c0] : 0.0f;
+            nx[u] = (wrow + sub + u * RSTEP < rows && col_ok) ? rowp[(uint64_t)u * rstride + c0] : 0.0f;
+    };
+    auto wave_sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
     load_chunk(0);
     for (int c0 = 0; c0 < P.B; c0 += HP_CW) {
-        __syncthreads();
+        wave_sync();  // the previous chunk's walk has read its rows
 #pragma unroll
-        for (int u = 0; u < NLD; u++) tile[sub + u * RSTEP][jj] = nx[u];
-        __syncthreads();
+        for (int u = 0; u < NLD; u++) tile[wrow + sub + u * RSTEP][jj] = nx[u];
+        wave_sync();
         if (c0 + HP_CW < P.B) load_chunk(c0 + HP_CW);
         if (!valid) continue;
         hf.walk(tile[i], c0, P.B - c0 < HP_CW ? P.B - c0 : HP_CW, P);
     }
-    // pitch-class accumulators reuse the staging tile (every read of it is done)
-    __syncthreads();
-    static_assert(sizeof(tile) >= sizeof(float) * 12 * HP_FRAMES, "pc fits the staging tile");
     if (!valid) return;
-    hf.finish(reinterpret_cast<float(*)[HP_FRAMES]>(&tile[0][0]), i, P, harm, chroma, energy, g0 + (uint64_t)f);
+    hf.finish(pcs, i, P, harm, chroma, energy, g0 + (uint64_t)f);
 }
 
 // k_hpcp_band: k_hpcp after k_mask_rp.  The frame energy folds the 65 block sums part[g][frame] in
