@@ -17,17 +17,21 @@
 
 namespace sdsp {
 
-// ---- peak |x| per track (order-free max via atomicMax on the IEEE bits of |x| >= 0) ----
+// ---- peak |x| per track (an order-free max of |x| >= 0, taken on the IEEE bits) ----
 // PK_CH samples per workgroup: the 16-B aligned body as float4 loads, all PK_U of a thread in
 // flight at once (a 4-B stream kept too few bytes in flight to reach HBM bandwidth); the < 4
-// unaligned samples at either end as scalars.
+// unaligned samples at either end as scalars.  Each workgroup writes its chunk's maximum and
+// k_peak_fold takes the maximum over a track's chunks: the round-3 form, one atomicMax per wave
+// on the track's word, serialised the ~2,000 waves of a track on one L2 line (k_peak_abs lasted
+// ~25 us per workgroup whatever its size).
 constexpr int PK_U = PK_CH / (4 * 256);  // float4 loads per thread
 static_assert(PK_U * 4 * 256 == PK_CH, "PK_CH = 1024 * PK_U");
 __global__ __launch_bounds__(256) void k_peak_abs(const float* __restrict__ x, const uint64_t* __restrict__ in_off,
                                                   const uint64_t* __restrict__ n_raw,
                                                   const uint64_t* __restrict__ chunk_pfx, int T,
-                                                  unsigned int* __restrict__ peak_bits) {
+                                                  unsigned int* __restrict__ chunk_bits) {
     typedef float f4 __attribute__((ext_vector_type(4)));
+    __shared__ float wmax[4];
     const uint64_t g = blockIdx.x;
     const int trk = find_track(chunk_pfx, T, g);
     const uint64_t c = g - chunk_pfx[trk];
@@ -56,7 +60,22 @@ __global__ __launch_bounds__(256) void k_peak_abs(const float* __restrict__ x, c
     for (int u = 0; u < PK_U; u++)
         m = sd_maxf(m, sd_maxf(sd_maxf(sd_absf(v[u].x), sd_absf(v[u].y)), sd_maxf(sd_absf(v[u].z), sd_absf(v[u].w))));
     m = wave_max(m);
-    if ((threadIdx.x & 63) == 0 && m > 0.0f) atomicMax(&peak_bits[trk], sd_bits_f(m));
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) chunk_bits[g] = sd_bits_f(sd_maxf(sd_maxf(wmax[0], wmax[1]), sd_maxf(wmax[2], wmax[3])));
+}
+
+// peak_bits[t] = the maximum of track t's chunk maxima (every one a float >= +0 or +inf, so the
+// unsigned maximum of the bits is the float maximum), one wave per track
+__global__ __launch_bounds__(64) void k_peak_fold(const uint64_t* __restrict__ chunk_pfx, int T,
+                                                  const unsigned int* __restrict__ chunk_bits,
+                                                  unsigned int* __restrict__ peak_bits) {
+    const int t = blockIdx.x;
+    if (t >= T) return;
+    unsigned int m = 0;
+    for (uint64_t c = chunk_pfx[t] + threadIdx.x; c < chunk_pfx[t + 1]; c += 64) m = max(m, chunk_bits[c]);
+    for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned int)__shfl_xor((int)m, o, 64));
+    if (threadIdx.x == 0) peak_bits[t] = m;
 }
 
 // gain = min(10^(-headroom/20)/peak, 1/peak); peak <= 1e-10 leaves the samples untouched.
@@ -393,12 +412,16 @@ __global__ __launch_bounds__(256) void k_consensus(const uint32_t* __restrict__ 
 }
 
 // ---- launchers ----
+static void launch_peak(const float* x, const uint64_t* in_off, const uint64_t* n_raw, const uint64_t* chunk_pfx, int T,
+                        uint64_t n_chunks, unsigned int* chunk_bits, unsigned int* peak_bits, hipStream_t st) {
+    if (n_chunks) hipLaunchKernelGGL(k_peak_abs, dim3((unsigned)n_chunks), dim3(256), 0, st, x, in_off, n_raw, chunk_pfx, T, chunk_bits);
+    hipLaunchKernelGGL(k_peak_fold, dim3((unsigned)T), dim3(64), 0, st, chunk_pfx, T, chunk_bits, peak_bits);
+}
 void launch_peak_gain(const float* x, const uint64_t* in_off, const uint64_t* n_raw, const uint64_t* chunk_pfx, int T,
-                      uint64_t n_chunks, unsigned int* peak_bits, float target, int enable, float* gain,
-                      hipStream_t st) {
+                      uint64_t n_chunks, unsigned int* chunk_bits, unsigned int* peak_bits, float target, int enable,
+                      float* gain, hipStream_t st) {
     if (T == 0) return;
-    (void)hipMemsetAsync(peak_bits, 0, (size_t)T * sizeof(unsigned int), st);
-    if (n_chunks) hipLaunchKernelGGL(k_peak_abs, dim3((unsigned)n_chunks), dim3(256), 0, st, x, in_off, n_raw, chunk_pfx, T, peak_bits);
+    launch_peak(x, in_off, n_raw, chunk_pfx, T, n_chunks, chunk_bits, peak_bits, st);
     hipLaunchKernelGGL(k_gain, dim3((T + 255) / 256), dim3(256), 0, st, peak_bits, T, target, enable, gain);
 }
 // ---- RMS / LUFS gain (normalization.rs:325-470): one lane per track ----
@@ -586,11 +609,10 @@ __global__ __launch_bounds__(64 * (1 + LG_LOADERS)) void k_loudness_gain(
 }
 
 void launch_loudness_gain(const float* x, const uint64_t* in_off, const uint64_t* n_raw, const uint64_t* chunk_pfx,
-                          int T, uint64_t n_chunks, unsigned int* peak_bits, const LoudnessParams& P, float* gain,
-                          int* status, hipStream_t st) {
+                          int T, uint64_t n_chunks, unsigned int* chunk_bits, unsigned int* peak_bits,
+                          const LoudnessParams& P, float* gain, int* status, hipStream_t st) {
     if (T == 0) return;
-    (void)hipMemsetAsync(peak_bits, 0, (size_t)T * sizeof(unsigned int), st);
-    if (n_chunks) hipLaunchKernelGGL(k_peak_abs, dim3((unsigned)n_chunks), dim3(256), 0, st, x, in_off, n_raw, chunk_pfx, T, peak_bits);
+    launch_peak(x, in_off, n_raw, chunk_pfx, T, n_chunks, chunk_bits, peak_bits, st);
     const size_t lds = 2 * LG_TPW * LG_ROW * sizeof(float);
     auto kern = P.method == 1 ? k_loudness_gain<true> : k_loudness_gain<false>;
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

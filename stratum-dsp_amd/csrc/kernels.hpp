@@ -44,7 +44,10 @@ struct MelPlan {
     int s0, s1;
     float w0, w1;
 };
-constexpr int PK_CH = 16384;  // samples per k_peak_abs workgroup
+#ifndef SDSP_PK_CH
+#define SDSP_PK_CH 16384
+#endif
+constexpr int PK_CH = SDSP_PK_CH;  // samples per k_peak_abs workgroup
 constexpr int FT_FRAMES = 256;
 // frames per k_features tile: lane 0 of each wave is a helper that computes the normalised
 // magnitudes of the frame before the wave's first (k_features.hip)
@@ -245,9 +248,10 @@ constexpr int LG_COMB_MAX = 2048, LG_AC_MAX = 512;  // comb candidates; autocorr
 
 // ---- launchers ----
 // launch_stft, stft_strips, stft_slide_ok: sdsp_runtime.hpp
+// chunk_bits: n_chunks words of scratch (each k_peak_abs workgroup's maximum)
 void launch_peak_gain(const float* x, const uint64_t* in_off, const uint64_t* n_raw, const uint64_t* chunk_pfx, int T,
-                      uint64_t n_chunks, unsigned int* peak_bits, float target, int enable, float* gain,
-                      hipStream_t st);
+                      uint64_t n_chunks, unsigned int* chunk_bits, unsigned int* peak_bits, float target, int enable,
+                      float* gain, hipStream_t st);
 // RMS / LUFS normalization constants, computed on the host (normalization.rs:119-158, 325-470)
 struct LoudnessParams {
     int method;          // 1 RMS, 2 LUFS
@@ -259,8 +263,8 @@ struct LoudnessParams {
     float b0, b1, b2, a1, a2;  // K-weighting biquad, normalised by a0
 };
 void launch_loudness_gain(const float* x, const uint64_t* in_off, const uint64_t* n_raw, const uint64_t* chunk_pfx,
-                          int T, uint64_t n_chunks, unsigned int* peak_bits, const LoudnessParams& P, float* gain,
-                          int* status, hipStream_t st);
+                          int T, uint64_t n_chunks, unsigned int* chunk_bits, unsigned int* peak_bits,
+                          const LoudnessParams& P, float* gain, int* status, hipStream_t st);
 void launch_frame_rms(const float* x, const uint64_t* src_off, const float* gain, const uint64_t* n_len,
                       const uint64_t* frame_pfx, int T, uint64_t total, int fs, int hop, float* rms, hipStream_t st, bool per_frame_kernel = false);
 // base_pfx / stride: trim frame f of track t at rms[base_pfx[t] + f * stride] (default: frame_pfx, 1)

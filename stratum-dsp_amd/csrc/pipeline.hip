@@ -961,7 +961,9 @@ void Pipeline::loudness_prepass(const float* d_samples, const std::vector<uint64
     unsigned int* d_peak = c_.dev<unsigned int>("L.peak", (size_t)L);
     float* d_gain = c_.dev<float>("L.gain", (size_t)L);
     int* d_stat = c_.dev<int>("L.stat", (size_t)L);
-    launch_loudness_gain(d_samples, d_off, d_nr, d_cpfx, L, cpfx.back(), d_peak, lp, d_gain, d_stat, d_.stream);
+    launch_loudness_gain(d_samples, d_off, d_nr, d_cpfx, L, cpfx.back(),
+                         c_.dev<unsigned int>("L.peakchunk", std::max<uint64_t>(cpfx.back(), 1)), d_peak, lp, d_gain,
+                         d_stat, d_.stream);
     SDSP_HIP_CHECK(hipGetLastError());
     const std::vector<float> g = c_.down(d_gain, (size_t)L);
     const std::vector<int> st = c_.down(d_stat, (size_t)L);
@@ -1458,8 +1460,9 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         }
         d_gain = c_.up("A.gain", g);
     } else {
-        launch_peak_gain(d_samples, d_off, d_nr, d_cpfx, T, cpfx[(size_t)T], d_peak, target, cfg_.enable_normalization,
-                         d_gain, st);
+        launch_peak_gain(d_samples, d_off, d_nr, d_cpfx, T, cpfx[(size_t)T],
+                         c_.dev<unsigned int>("A.peakchunk", std::max<uint64_t>(cpfx[(size_t)T], 1)), d_peak, target,
+                         cfg_.enable_normalization, d_gain, st);
     }
     // One read of the samples for both frame-RMS passes: with trimming on and the trim hop (fs / 2)
     // a multiple of the energy hop, the trim pass runs on the raw signal at the energy hop (trim
