@@ -695,7 +695,7 @@ __global__ __launch_bounds__(256) void k_frame_rms(const float* __restrict__ x,
 // (bit-identical to k_frame_rms, which re-reads every sample G times from L2; its overlap
 // re-reads mostly miss L2, 33 % hits).  Samples past the track's end load as 0 and add +0.
 template <int G>
-__global__ __launch_bounds__(256) void k_frame_rms_run(const float* __restrict__ x, const uint64_t* __restrict__ src_off,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_frame_rms_run(const float* __restrict__ x, const uint64_t* __restrict__ src_off,
                                                        const float* __restrict__ gain, const uint64_t* __restrict__ n_len,
                                                        const uint64_t* __restrict__ frame_pfx, int T, uint64_t total,
                                                        int fs, int hop, float* __restrict__ rms) {
@@ -753,6 +753,27 @@ __global__ __launch_bounds__(256) void k_frame_rms_run(const float* __restrict__
                 f4 nb[8];
 #pragma unroll
                 for (int e = 0; e < 8; e++) nb[e] = load(bi + (uint64_t)e);
+                // the common step: 16-B aligned piece, all 32 samples inside the track, on every
+                // lane of the wave: the samples are the blocks' own components, no selects
+                const bool plain = d == 0 && p0 + 32 * (c + 1) <= ls;
+                if (__builtin_expect(__builtin_amdgcn_ballot_w64(!plain) == 0, 1)) {
+#pragma unroll
+                    for (int e = 0; e < 8; e++) {
+                        const float v[4] = {buf[e].x, buf[e].y, buf[e].z, buf[e].w};
+#pragma unroll
+                        for (int w = 0; w < 4; w++) {
+                            const float y = v[w] * gn;
+                            const float yy = y * y;
+#pragma unroll
+                            for (int t = 0; t < G; t++) acc[t] += yy;
+                        }
+                    }
+                    buf[0] = buf[8];
+#pragma unroll
+                    for (int e = 0; e < 8; e++) buf[e + 1] = nb[e];
+                    bi += 8;
+                    continue;
+                }
 #pragma unroll
                 for (int e = 0; e < 8; e++) {
                     const f4 cur = buf[e], nxt = buf[e + 1];
