@@ -58,8 +58,10 @@ __global__ __launch_bounds__(FT_FRAMES) __attribute__((amdgpu_waves_per_eu(KK > 
     static_assert((W & (W - 1)) == 0, "W must be a power of two");
     constexpr int ROWS = FT_FRAMES;  // row i: lane i's frame (each wave stages its own 64 rows)
     constexpr int LS = W + 1;
-    __shared__ float Mt[ROWS][LS];
-    __shared__ float Lt[ROWS][LS];
+    // slot s of row r: {magnitude, ln(1 + max(magnitude, 0))} side by side, so the walk reads both
+    // with one ds_read_b64 at a per-chunk base plus an immediate offset (the chunk's 8 slots never
+    // wrap: CW divides W), and the staging writes both with one ds_write_b64
+    __shared__ float2 ML[ROWS][LS];
     __shared__ sd_logtab2_t ltab[128];  // sd_logf's table {s, ln c}, read per element by the staging
     static_assert(KK == 0 || CW + 2 * KK <= W, "window halo must fit the ring");
     for (int q = threadIdx.x; q < 128; q += FT_FRAMES) ltab[q] = sd_logtab2_from(SD_LOGTAB_D, q);
@@ -150,7 +152,7 @@ __global__ __launch_bounds__(FT_FRAMES) __attribute__((amdgpu_waves_per_eu(KK > 
         if (__builtin_expect(__builtin_amdgcn_ballot_w64(miss) == 0, 1)) return;
         so = so_start;
         for (int j = 0; j < nb; j++) {
-            const float m = Mt[ro][(c0 + j) & (W - 1)];
+            const float m = ML[ro][(c0 + j) & (W - 1)].x;
             const float cv = cn ? m / mx_c : 0.0f;
             const float pv = __builtin_bit_cast(
                 float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, cv), 0x138, 0xf, 0xf, true));
@@ -209,8 +211,7 @@ __global__ __launch_bounds__(FT_FRAMES) __attribute__((amdgpu_waves_per_eu(KK > 
 #pragma unroll
         for (int u = 0; u < NLD; u++) {
             const int r = wrow + sub + u * RSTEP;
-            Mt[r][slot] = nx[u];
-            Lt[r][slot] = sd_ln1p_max0_t2(nx[u], ltab);
+            ML[r][slot] = make_float2(nx[u], sd_ln1p_max0_t2(nx[u], ltab));
         }
     };
     __syncthreads();  // ltab; from here on each wave works on its own rows
@@ -220,7 +221,7 @@ __global__ __launch_bounds__(FT_FRAMES) __attribute__((amdgpu_waves_per_eu(KK > 
         commit(0);
     }
     if (KK > 0)
-        for (int q = 0; q < KK; q++) Lt[ro][W - KK + q] = 0.0f;
+        for (int q = 0; q < KK; q++) ML[ro][W - KK + q].y = 0.0f;
     load(K);
     for (int c0 = 0; c0 < B; c0 += CW) {
         // the wave's walk of the previous step has issued its reads of the slots overwritten here
@@ -245,7 +246,7 @@ __global__ __launch_bounds__(FT_FRAMES) __attribute__((amdgpu_waves_per_eu(KK > 
         const int rp = lane > 0 ? ro - 1 : ro;
         if (KK > 0) {
 #pragma unroll
-            for (int q = 0; q < (KK > 0 ? CW + 2 * KK : 1); q++) Rw[q] = Lt[rp][(c0 - KK + q) & (W - 1)];
+            for (int q = 0; q < (KK > 0 ? CW + 2 * KK : 1); q++) Rw[q] = ML[rp][(c0 - KK + q) & (W - 1)].y;
             if constexpr (VHK) {
                 float suf[CW], pre[CW];
                 suf[CW - 1] = Rw[CW - 1];
@@ -292,12 +293,13 @@ __global__ __launch_bounds__(FT_FRAMES) __attribute__((amdgpu_waves_per_eu(KK > 
                     for (int j = 0; j < CW; j++) {
                         const int b = c0 + j;
                         const int s = b & (W - 1);
-                        const float m = Mt[ro][s];
+                        const float2 ml = ML[ro][s];
+                        const float m = ml.x;
                         const float ee = m * m;
                         const float hh = bfv[j] * m * m;
                         e[0] += ee;
                         h[0] += hh;
-                        const float lc = Lt[ro][s];
+                        const float lc = ml.y;
                         const float cv = quot(m);
                         const float pv = __builtin_bit_cast(
                             float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, cv), 0x138, 0xf, 0xf, true));
@@ -355,7 +357,8 @@ __global__ __launch_bounds__(FT_FRAMES) __attribute__((amdgpu_waves_per_eu(KK > 
             if (j >= nb) continue;
             const int b = c0 + j;
             const int s = b & (W - 1);
-            const float m = Mt[ro][s];
+            const float2 ml = ML[ro][s];
+            const float m = ml.x;
             const float ee = m * m;
             const float hh = (float)b * m * m;
             e[0] += ee;
@@ -369,7 +372,7 @@ __global__ __launch_bounds__(FT_FRAMES) __attribute__((amdgpu_waves_per_eu(KK > 
                 eb += ee;
                 hb += hh;
             }
-            const float lc = Lt[ro][s];
+            const float lc = ml.y;
             // X/max of this lane's frame, and of the previous frame from lane - 1 (its frame is
             // f - 1 for every lane that reads it: lanes 1-63; the helper's value is unused)
             const float cv = quot(m);
@@ -414,7 +417,7 @@ __global__ __launch_bounds__(FT_FRAMES) __attribute__((amdgpu_waves_per_eu(KK > 
                         for (int q = 1; q <= 2 * KK; q++) pm = max_bnn(pm, Rw[j + q]);
                     }
                 } else {
-                    for (int q = lo; q < hi; q++) pm = max_bnn(pm, Lt[rp][q & (W - 1)]);  // L is never NaN
+                    for (int q = lo; q < hi; q++) pm = max_bnn(pm, ML[rp][q & (W - 1)].y);  // L is never NaN
                 }
                 const float df = max_bnn(lc - pm, 0.0f);
                 const float df2 = df * df;
@@ -430,7 +433,7 @@ __global__ __launch_bounds__(FT_FRAMES) __attribute__((amdgpu_waves_per_eu(KK > 
                             for (int q = 0; q <= 2 * KK; q++)
                                 if (b - KK + q >= lb && b - KK + q < hbd) pmb = max_bnn(pmb, Rw[j + q]);
                         } else {
-                            for (int q = lb; q < hbd; q++) pmb = max_bnn(pmb, Lt[rp][q & (W - 1)]);
+                            for (int q = lb; q < hbd; q++) pmb = max_bnn(pmb, ML[rp][q & (W - 1)].y);
                         }
                         const float db = max_bnn(lc - pmb, 0.0f);
                         sb += db * db;

@@ -12,7 +12,7 @@ base=$(basename $src .hip)
 make -s -j8 >/dev/null
 mkdir -p lib_exp build/exp
 HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fhip-fp32-correctly-rounded-divide-sqrt -Wno-unused-result -I$(pwd)/csrc"
-[ "$base" = k_stft ] && HIPFLAGS="$HIPFLAGS -fno-slp-vectorize"
+case "$base" in k_stft|k_features) HIPFLAGS="$HIPFLAGS -fno-slp-vectorize";; esac
 others=$(ls build/*.o | grep -v "build/$base.o")
 names=()
 while [ $# -ge 2 ]; do

@@ -13,7 +13,7 @@ skip=""
 for spec in "$@"; do
   f=${spec%%:*}; fl=${spec#*:}
   base=$(basename $f .hip)
-  extra=""; [ "$base" = k_stft ] && extra="-fno-slp-vectorize"
+  extra=""; case "$base" in k_stft|k_features) extra="-fno-slp-vectorize";; esac
   /opt/rocm/bin/hipcc $HIPFLAGS $extra $fl -c csrc/$f -o build/exp/${base}_$name.o &
   objs="$objs build/exp/${base}_$name.o"
   skip="$skip build/$base.o"
