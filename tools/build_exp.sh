@@ -11,8 +11,7 @@ base=$(basename $src .hip)
 [ -f "$src" ] || src=csrc/$src
 make -s -j8 >/dev/null
 mkdir -p lib_exp build/exp
-HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fhip-fp32-correctly-rounded-divide-sqrt -Wno-unused-result -I$(pwd)/csrc"
-case "$base" in k_stft|k_features) HIPFLAGS="$HIPFLAGS -fno-slp-vectorize";; esac
+HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fhip-fp32-correctly-rounded-divide-sqrt -Wno-unused-result -fno-slp-vectorize -I$(pwd)/csrc"
 others=$(ls build/*.o | grep -v "build/$base.o")
 names=()
 while [ $# -ge 2 ]; do

@@ -7,13 +7,13 @@ cd "$(dirname "$0")/../stratum-dsp_amd"
 name=$1; shift
 make -s -j8 >/dev/null
 mkdir -p lib_exp build/exp
-HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fhip-fp32-correctly-rounded-divide-sqrt -Wno-unused-result -I$(pwd)/csrc"
+HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fhip-fp32-correctly-rounded-divide-sqrt -Wno-unused-result -fno-slp-vectorize -I$(pwd)/csrc"
 objs=""
 skip=""
 for spec in "$@"; do
   f=${spec%%:*}; fl=${spec#*:}
   base=$(basename $f .hip)
-  extra=""; case "$base" in k_stft|k_features) extra="-fno-slp-vectorize";; esac
+  extra=""
   /opt/rocm/bin/hipcc $HIPFLAGS $extra $fl -c csrc/$f -o build/exp/${base}_$name.o &
   objs="$objs build/exp/${base}_$name.o"
   skip="$skip build/$base.o"
