@@ -35,6 +35,34 @@ BAND_DEFAULT = dict(enabled=True, low_max_hz=200.0, mid_max_hz=2000.0, high_max_
                     w_mel=0.15, nw=(0.30, 0.35, 0.35), local_mean=16, smooth=5, superflux_k=4)
 
 
+def normalize_peak64(x, headroom_db=1.0):
+    """normalize_peak in float64 (src/preprocessing/normalization.rs:262-322, src/lib.rs:116-127):
+    gain = min(10^(-headroom/20) / peak, 1 / peak) for peak > 1e-10, else the signal unchanged.
+    NaN samples are ignored by the peak, as f32::max does."""
+    x = np.asarray(x, np.float64)
+    a = np.abs(x[np.isfinite(x) | np.isinf(x)])
+    peak = float(a.max()) if a.size else 0.0
+    if not peak > 1e-10:
+        return x
+    return x * min(10.0 ** (-headroom_db / 20.0) / peak, 1.0 / peak)
+
+
+def stft64(x, frame_size=2048, hop=512):
+    """compute_stft in float64 with numpy's FFT (src/features/chroma/extractor.rs:301-359):
+    frames at multiples of hop while a whole frame fits, the symmetric Hann window
+    0.5 (1 - cos(2 pi i / (N - 1))), |rfft| of each windowed frame.  Independent of the CPU
+    restatement's FFT and libm (include/sdsp_fft_spec.h, sdsp_libm.h)."""
+    x = np.asarray(x, np.float64)
+    n = x.size
+    if n < frame_size:
+        return np.zeros((0, frame_size // 2 + 1))
+    nf = (n - frame_size) // hop + 1
+    i = np.arange(frame_size)
+    w = 0.5 * (1.0 - np.cos(2.0 * np.pi * i / (frame_size - 1)))
+    idx = np.arange(nf)[:, None] * hop + i[None, :]
+    return np.abs(np.fft.rfft(x[idx] * w, axis=1))
+
+
 def _normalize(v):
     mx = max(float(v.max()), 0.0) if v.size else 0.0
     return v / mx if mx > EPS else v

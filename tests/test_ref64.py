@@ -146,3 +146,25 @@ def test_branches_and_tie_rate():
         refined += bool(tr["beat_refined"])
     assert refined >= 1
     assert outcomes.count("exact") + outcomes.count("ts-tie") >= 0.75 * len([o for o in outcomes if o])
+
+
+@pytest.mark.parametrize("kind,what", CASES, ids=[f"{k}-{w}" for k, w in CASES])
+def test_tempogram_estimate_float64_front_end(kind, what):
+    """The tempogram estimate from a float64 front end that shares nothing with the CPU
+    restatement but the trim bounds: peak normalisation and the STFT in float64 with numpy's FFT
+    (ref64.normalize_peak64 / stft64), then ref64's novelty and tempogram.  The oracle's BPM (f32,
+    the spec FFT) is the float64 pick, or a candidate the float64 reading scores within 1e-4 of
+    it (a near tie decided by rounding)."""
+    x, sr = _load(kind, what)
+    _, _, tr, _ = _stage_inputs(kind, what)
+    xt = ref64.normalize_peak64(x)[tr["trim_start"]:tr["trim_end"]]
+    mags = ref64.stft64(xt, 2048, 512)
+    bpm, conf, agree, scored = ref64.estimate_bpm_tempogram(mags, sr, 512, 40.0, 240.0, 1.0)
+    obpm, oconf, oagree = tr["base"]
+    if abs(bpm - obpm) <= 1e-4:
+        assert abs(conf - oconf) <= 1e-4, (conf, oconf)
+        return
+    ties = ref64.estimate_bpm_tempogram.lookup_ties
+    s64 = {round(c[0], 4): c[1] for c in scored}
+    assert any(abs(t - obpm) <= 1e-4 for t in ties) or abs(s64.get(round(obpm, 4), -1.0) - s64[round(bpm, 4)]) <= 1e-4, (bpm, obpm)
+
