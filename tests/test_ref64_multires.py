@@ -121,3 +121,67 @@ def test_escalation_coverage_and_tie_rate():
     assert sum(bool(o["used"]) for o in ran) >= 8
     tied = sum(bool(o["mr_ties"]) for o in ran)
     assert tied <= 0.25 * len(ran), tied
+
+
+_cache64 = {}
+
+
+def _run64(kind, what):
+    """_run's chain from a float64 front end sharing nothing with the CPU restatement but the trim
+    bounds: float64 peak normalisation and numpy-FFT STFTs (ref64.normalize_peak64 / stft64) for
+    the base pass and every escalation hop."""
+    key = (kind, str(what))
+    if key in _cache64:
+        return _cache64[key]
+    tr = _run(kind, what)["tr"]
+    if kind == "fixture":
+        x, sr = parity.load_wav(os.path.join(HERE, "golden", what))
+    elif kind == "synth":
+        x, *_ = synth.make_track(what[0], seconds=what[1])
+        sr = 44100
+    else:
+        x, *_ = synth.make_track(what[0], seconds=20.0, bpm=what[1])
+        sr = 44100
+    xt = ref64.normalize_peak64(x)[tr["trim_start"]:tr["trim_end"]]
+    ties = ref64.Ties()
+    bpm, conf, agree, scored = ref64.estimate_bpm_tempogram(ref64.stft64(xt, 2048, 512), sr, 512, 40.0, 240.0, 1.0)
+    base_tie = bool(ref64.estimate_bpm_tempogram.lookup_ties)
+    amb, tl, th = ref64.escalation_gate(bpm, conf, agree, scored[:ref64.MR_DEFAULT["base_top_n"]], 1.0, ties)
+    out = dict(tr=tr, base=(bpm, conf, agree), base_tie=base_tie, amb=amb, gate_ties=list(ties), mr=None, used=False,
+               mr_ties=[])
+    if amb:
+        mties = ref64.Ties()
+        out["mr"] = ref64.multi_resolution(xt, sr, ref64.stft64, ties=mties)
+        out["mr_ties"] = list(mties)
+        out["used"] = ref64.accept_multi_resolution((bpm, conf, agree), out["mr"], tl, th, mties)
+    _cache64[key] = out
+    return out
+
+
+@pytest.mark.parametrize("kind,what", CASES, ids=[f"{k}-{w}" for k, w in CASES])
+def test_escalation_float64_front_end(kind, what):
+    """Gate, multi-resolution estimate and acceptance from the float64 front end against the
+    oracle's (f32, spec FFT), with the near-tie rules of the tests above.  Measured: every base
+    estimate equal, 24 escalations, 21 of them equal to 1e-4 with the same acceptance, 3 decided
+    by an f32 near tie inside the fusion (tempo-family members)."""
+    o = _run64(kind, what)
+    tr = o["tr"]
+    if not _base_equal(o):
+        assert o["base_tie"], (o["base"], tr["base"])
+        return
+    if o["gate_ties"]:
+        return
+    assert o["amb"] == bool(tr["ambiguous"]), (o["base"], o["amb"])
+    if o["mr"] is None:
+        return
+    mb, mc, ma = o["mr"]
+    ob, oc, oa = tr["mr"]
+    if o["mr_ties"]:
+        rel = max(ob / mb, mb / ob)
+        assert min(abs(rel - f) for f in (1.0, 2.0, 1.5, 4.0 / 3.0, 9.0 / 8.0, 3.0)) < 0.05, (mb, ob)
+        return
+    assert abs(mb - ob) <= 1e-4, (mb, ob)
+    assert abs(mc - oc) <= 1e-4, (mc, oc)
+    assert ma == oa
+    assert o["used"] == bool(tr["used_mr"]), (o["base"], o["mr"], o["used"])
+
