@@ -104,3 +104,37 @@ def test_vote_onsets_known_answers():
     c = v([[1000, 20000, 50000], [1050, 20050, 50500], [980, 20100], [1020, 19950]], q, 50, 44100)  # _sorted_by_confidence
     assert len(c) >= 2 and c[0][2] == 4
     assert all(c[i][1] <= c[i - 1][1] for i in range(1, len(c)))
+
+
+_cache64 = {}
+
+
+def _run64(kind, what):
+    """_run's float64 reading from a front end sharing nothing with the CPU restatement but the trim
+    bounds (ref64.normalize_peak64, ref64.stft64)."""
+    key = (kind, str(what))
+    if key not in _cache64:
+        tr = _run(kind, what)[0]
+        if kind == "fixture":
+            x, sr = parity.load_wav(os.path.join(HERE, "golden", what))
+        else:
+            x, *_ = synth.make_track(what[0], seconds=what[1])
+            sr = 44100
+        xt = ref64.normalize_peak64(x)[tr["trim_start"]:tr["trim_end"]]
+        ties = ref64.Ties()
+        got = ref64.consensus_onsets(xt, sr, ref64.stft64(xt, 2048, 512), ties=ties)
+        _cache64[key] = (tr, got, list(ties))
+    return _cache64[key]
+
+
+@pytest.mark.parametrize("kind,what", CASES, ids=[f"{k}-{w}" for k, w in CASES])
+def test_onset_lists_float64_front_end(kind, what):
+    """The onset lists from the float64 front end against the oracle's, with the near-tie rule of
+    test_onset_lists (the energy, spectral-flux and HFC lists and the consensus)."""
+    tr, (energy, spectral, hfc, chosen), ties = _run64(kind, what)
+    _compare(tr["energy_onsets"], energy, _tie_positions(ties, "energy-peak"))
+    _compare(tr["spectral_onsets"], spectral, _tie_positions(ties, "spectral-peak"))
+    _compare(tr["hfc_onsets"], hfc, _tie_positions(ties, "hfc-peak"))
+    if not ties:
+        assert list(tr["chosen_onsets"]) == list(chosen)
+
