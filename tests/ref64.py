@@ -926,3 +926,193 @@ def consensus_onsets(x, sr, M, frame=2048, hop=512, cfg=ONSET_DEFAULT, ties=None
         if pick:
             chosen = pick
     return energy, spectral, hfc, chosen
+
+
+# ---- key path (src/lib.rs:961-1540, default AnalysisConfig, config.rs:669-739) ----
+# The 8192 / 512 key STFT, the harmonic time mask (extractor.rs:1246-1349, margin 12, power 2),
+# HPCP (extractor.rs:529-680, 1097-1150: peaks 24, harmonics 4, decay 0.6, magnitude power 0.5,
+# sigma 0.5, 100-5000 Hz, no tuning or whitening), the 5-frame median (smoothing.rs:37-94), the
+# frame weights (lib.rs:1236-1287: tonalness^2 x (energy / median)^0.5), segment voting
+# (lib.rs:1331-1436: 1024-frame segments, hop 512, clarity >= 0.2) over detect_key_weighted
+# (detector.rs:68-313, Krumhansl-Kessler templates, templates.rs:64-140) and the key clarity
+# (key_clarity.rs:51-93).  Float64 throughout.
+KK_MAJOR = (6.35, 2.23, 3.48, 2.33, 4.38, 4.09, 2.52, 5.19, 2.39, 3.66, 2.29, 2.88)
+KK_MINOR = (6.33, 2.68, 3.52, 5.38, 2.60, 3.53, 2.54, 4.75, 3.98, 2.69, 3.34, 3.17)
+KEY_DEFAULT = dict(margin=12, mask_power=2.0, peaks=24, harmonics=4, decay=0.6, mag_power=0.5, sigma=0.5,
+                   fmin=100.0, fmax=5000.0, tonal_pow=2.0, energy_pow=0.5, min_tonal=0.0, seg_len=1024, seg_hop=512,
+                   min_clarity=0.2)
+
+
+def key_templates64():
+    """(major[12][12], minor[12][12]): the base profiles rotated to every tonic, L2-normalised."""
+    def rot(base):
+        t = np.array([[base[(s + 12 - k) % 12] for s in range(12)] for k in range(12)], np.float64)
+        n = np.sqrt((t * t).sum(axis=1))
+        return t / np.where(n > 1e-12, n, 1.0)[:, None]
+    return rot(KK_MAJOR), rot(KK_MINOR)
+
+
+def harmonic_mask64(M, margin=12, power=2.0):
+    """harmonic_spectrogram_time_mask: X * H^p / (H^p + max(X - H, 0)^p + 1e-12), H the moving
+    average over frames t - margin .. t + margin (clipped to the track)."""
+    M = np.asarray(M, np.float64)
+    F = M.shape[0]
+    if F == 0:
+        return M
+    P = np.vstack([np.zeros((1, M.shape[1])), np.cumsum(M, axis=0)])
+    t = np.arange(F)
+    st, en = np.maximum(t - margin, 0), np.minimum(t + margin + 1, F)
+    H = (P[en] - P[st]) / np.maximum(en - st, 1)[:, None]
+    p = max(power, 1.0)
+    x, h = np.maximum(M, 0.0), np.maximum(H, 0.0)
+    r = np.maximum(x - h, 0.0)
+    hp, rp = h ** p, r ** p
+    return x * (hp / (hp + rp + 1e-12))
+
+
+def hpcp64(M, sr, fft_size, cfg=KEY_DEFAULT):
+    """Per-frame HPCP (frame_to_hpcp_tuned_band) and frame energies sum(x^2).  The top-K peaks are
+    taken by magnitude, ties broken by the lower bin (the reference's select_nth_unstable order is
+    unspecified; the sum is order-insensitive but for rounding)."""
+    M = np.asarray(M, np.float64)
+    F, nb = M.shape
+    energy = (M * M).sum(axis=1)
+    pc = np.zeros((F, 12))
+    fres = sr / fft_size
+    fmin, fmax = max(cfg["fmin"], 20.0), min(cfg["fmax"], sr / 2.0)
+    b = np.arange(1, nb - 1)
+    fb = b * fres
+    b = b[(fb >= fmin) & (fb <= fmax)]
+    if F == 0 or b.size == 0:
+        return pc, energy
+    m, mp, mn = M[:, b], M[:, b - 1], M[:, b + 1]
+    cand = ~((m <= mp) | (m < mn))
+    score = np.where(cand, m, -np.inf)
+    k = cfg["peaks"]
+    # stable descending order by magnitude, the lower bin first among equals
+    order = np.argsort(-score, axis=1, kind="stable")[:, :k]
+    sigma, decay, p = max(cfg["sigma"], 1e-6), min(max(cfg["decay"], 0.0), 1.0), min(max(cfg["mag_power"], 0.05), 1.0)
+    rows = np.arange(F)[:, None]
+    ok = np.isfinite(score[rows, order])
+    pbin = b[order]
+    w0 = np.where(ok, np.maximum(M[rows, pbin], 0.0) ** p, 0.0)
+    f0 = pbin * fres
+    for h in range(1, max(cfg["harmonics"], 1) + 1):
+        fh = f0 * h
+        live = ok & (w0 > 0) & (f0 > 0) & (fh >= fmin) & (fh <= fmax)
+        # a harmonic above fmax ends the peak's loop; below fmin only skips it (h grows)
+        semi = 12.0 * np.log2(np.where(live, fh, 440.0) / 440.0) + 57.0
+        spc = np.mod(semi, 12.0)
+        prim = np.mod(np.floor(spc + 0.5), 12.0).astype(int)  # f32::round (half away; spc >= 0)
+        hw = decay ** (h - 1) / h
+        for off in (-1, 0, 1):
+            tc = (prim + off) % 12
+            d = np.abs(spc - tc)
+            d = np.minimum(d, 12.0 - d)
+            wgt = np.exp(-d * d / (2.0 * sigma * sigma))
+            np.add.at(pc, (np.broadcast_to(rows, tc.shape)[live], tc[live]), (w0 * hw * wgt)[live])
+    n = np.sqrt((pc * pc).sum(axis=1))
+    pc = np.where((n > 1e-10)[:, None], pc / np.where(n > 1e-10, n, 1.0)[:, None], pc)
+    return pc, energy
+
+
+def smooth_chroma64(C, window=5):
+    """smooth_chroma: per pitch class, the median of the frames t - 2 .. t + 2 present in the
+    track (element len // 2 of the sorted window)."""
+    C = np.asarray(C, np.float64)
+    F = C.shape[0]
+    half = window // 2
+    out = np.empty_like(C)
+    for t in range(F):
+        w = np.sort(C[max(t - half, 0):min(t + half + 1, F)], axis=0)
+        out[t] = w[w.shape[0] // 2]
+    return out
+
+
+def key_weights64(C, E, cfg=KEY_DEFAULT):
+    """The frame weights of lib.rs:1236-1287, or None where the reference falls back to unweighted."""
+    s = C.sum(axis=1)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        P = C / np.where(s > 1e-12, s, 1.0)[:, None]
+        ent = -np.where(P > 1e-12, P * np.log(np.where(P > 1e-12, P, 1.0)), 0.0).sum(axis=1)
+    tonal = np.where(s <= 1e-12, 0.0, np.clip(1.0 - ent / math.log(12.0), 0.0, 1.0))
+    tonal = np.where(tonal < cfg["min_tonal"], 0.0, tonal)
+    med = max(float(np.sort(E)[E.size // 2]), 1e-12)
+    w = np.maximum(tonal ** max(cfg["tonal_pow"], 0.0) * np.maximum(E / med, 0.0) ** max(cfg["energy_pow"], 0.0), 0.0)
+    if w.sum() <= 1e-12 or int((w > 0).sum()) < 10:
+        return None
+    return w
+
+
+def key_clarity64(scores):
+    """compute_key_clarity over (key, score) pairs in the caller's order: (first - mean) / range."""
+    v = np.array([s for _, s in scores], np.float64)
+    if v.size < 2:
+        return 0.0
+    rng = v.max() - v.min()
+    return float(np.clip((v[0] - v.mean()) / rng, 0.0, 1.0)) if rng > 1e-10 else 0.0
+
+
+def detect_key_weighted64(C, w, templates):
+    """detect_key_weighted: (sorted (key, score) list, key, confidence); key k < 12 major, else
+    minor k - 12.  The top-3 HashMap vote's pick is unspecified in the reference (iteration
+    order); like the CPU restatement this takes the first sorted key."""
+    maj, mnr = templates
+    ww = np.ones(C.shape[0]) if w is None else np.where(w > 0, w, 0.0)
+    raw = np.concatenate([(C @ maj.T * ww[:, None]).sum(axis=0), (C @ mnr.T * ww[:, None]).sum(axis=0)])
+    mM, mm = max(0.0, raw[:12].max()), max(0.0, raw[12:].max())
+    sc = raw.copy()
+    if mM > 1e-9 and mm > 1e-9:
+        sc[:12] /= mM
+        sc[12:] /= mm
+    tM = 11 - int(np.argmax(sc[:12][::-1]))  # max_by keeps the last maximum
+    tm = 11 - int(np.argmax(sc[12:][::-1]))
+    cof = [0, 7, 2, 9, 4, 11, 6, 1, 8, 3, 10, 5]
+    ref = sc.copy()
+    for k in range(24):
+        rt, rs = (tM, sc[tM]) if k < 12 else (tm, sc[12 + tm])
+        if rs > 1e-9:
+            d = abs(cof.index(k % 12) - cof.index(rt))
+            d = min(d, 12 - d)
+            if d <= 2:
+                ref[k] += rs * (0.20 * (1.0 - d * 0.5))
+    order = sorted(range(24), key=lambda k: -ref[k])  # stable: majors, then minors, by index
+    scores = [(k, float(ref[k])) for k in order]
+    best = scores[0][1]
+    conf = float(np.clip((best - scores[1][1]) / best, 0.0, 1.0)) if best > 0 else 0.0
+    return scores, scores[0][0], conf
+
+
+def key_path64(M8, sr, fft_size=8192, cfg=KEY_DEFAULT, ties=None):
+    """(key, confidence, clarity) of the default key path from an 8192-point magnitude spectrogram
+    (frames x bins); ties (ref64.Ties) records segments whose clarity is within 1e-4 of the
+    threshold, where the reference's f32 rounding decides whether the segment votes."""
+    H = harmonic_mask64(M8, cfg["margin"], cfg["mask_power"])
+    C, E = hpcp64(H, sr, fft_size, cfg)
+    if C.shape[0] > 5:
+        C = smooth_chroma64(C, 5)
+    w = key_weights64(C, E, cfg)
+    T = key_templates64()
+    F = C.shape[0]
+    if F >= max(cfg["seg_len"], 1) and cfg["seg_len"] >= 120:
+        L = min(cfg["seg_len"], F)
+        hop = max(min(cfg["seg_hop"], L), 1)
+        acc = np.zeros(24)
+        used = 0
+        for st in range(0, F - L + 1, hop):
+            scores, _, _ = detect_key_weighted64(C[st:st + L], None if w is None else w[st:st + L], T)
+            cl = key_clarity64(scores)
+            if ties is not None and abs(cl - cfg["min_clarity"]) < 1e-4:
+                ties.append(("segment-clarity", cl, cfg["min_clarity"]))
+            if cl >= cfg["min_clarity"]:
+                used += 1
+                for k, s in scores:
+                    acc[k] += s * cl
+        if used:
+            order = sorted(range(24), key=lambda k: -acc[k])
+            scores = [(k, float(acc[k])) for k in order]
+            best = scores[0][1]
+            conf = float(np.clip((best - scores[1][1]) / best, 0.0, 1.0)) if best > 0 else 0.0
+            return scores[0][0], conf, key_clarity64(scores)
+    scores, key, conf = detect_key_weighted64(C, w, T)
+    return key, conf, key_clarity64(scores)
