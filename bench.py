@@ -23,6 +23,7 @@ import argparse
 import concurrent.futures as cf
 import json
 import os
+import re
 import socket
 import subprocess
 import sys
@@ -223,6 +224,9 @@ def main():
         eng.analyze(buf, offs, lens, sr, stage_mask).free()
     barrier()
     eng.synchronize()
+    clock = ClockSampler(local) if (rank == 0 and not args.dry_run) else None
+    if clock:
+        clock.__enter__()
     t0 = time.perf_counter()
     stft = {"ms8": 0.0, "b8": 0.0, "l8": 0, "ms2": 0.0, "b2": 0.0, "l2": 0}
     step_s = []
@@ -243,6 +247,8 @@ def main():
     eng.synchronize()
     barrier()
     dt = max_over_ranks(time.perf_counter() - t0, tdist)
+    if clock:
+        clock.__exit__(None, None, None)
     # every rank's shard (rank, tracks, first seed), gathered for the report: the ranks' tracks
     # must be disjoint and sum to the job's batch (config 3: 8 x 1024 = 8192)
     shard = {"rank": rank, "tracks": n, "seed0": seed0}
@@ -297,6 +303,8 @@ def main():
     cpu = None
     parity = None
     extras = {}
+    if clock and clock.report():
+        extras["sclk_mhz_timed"] = clock.report()
     ss = sorted(step_s)
     extras["step_ms"] = {"median": round(1e3 * ss[len(ss) // 2], 3), "min": round(1e3 * ss[0], 3),
                          "max": round(1e3 * ss[-1], 3), "all": [round(1e3 * t, 3) for t in step_s]}
@@ -358,6 +366,47 @@ def main():
         print(json.dumps(out), flush=True)
     if tdist is not None:
         tdist.destroy_process_group()
+
+
+class ClockSampler:
+    """Samples the shader clock of GPU `gpu` (rocm-smi --showclocks, about once a second) on a
+    daemon thread while the timed steps run.  The box runs bench processes in one of two clock
+    states (~2.0 vs ~1.75 GHz), so the line reports which one it measured.  Host-side
+    only (a sysfs read through rocm-smi); absent rocm-smi, it reports nothing."""
+
+    def __init__(self, gpu=0):
+        import shutil
+        import threading
+
+        self.gpu, self.mhz, self.stop = gpu, [], threading.Event()
+        self.exe = shutil.which("rocm-smi")
+        self.th = threading.Thread(target=self._run, daemon=True) if self.exe else None
+
+    def _run(self):
+        pat = re.compile(r"GPU\[%d\].*sclk clock level: \d+: \((\d+)Mhz\)" % self.gpu)
+        while not self.stop.is_set():
+            try:
+                out = subprocess.run([self.exe, "--showclocks"], capture_output=True, text=True, timeout=10).stdout
+                self.mhz += [int(m) for m in pat.findall(out)]
+            except Exception:
+                return
+            self.stop.wait(1.0)
+
+    def __enter__(self):
+        if self.th:
+            self.th.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.stop.set()
+        if self.th:
+            self.th.join(timeout=15)
+
+    def report(self):
+        if not self.mhz:
+            return None
+        v = sorted(self.mhz)
+        return {"median": v[len(v) // 2], "min": v[0], "max": v[-1], "samples": len(v), "source": "rocm-smi --showclocks"}
 
 
 def isolated_stft(nfft, hop, length, tracks=256, reps=3):

@@ -25,6 +25,21 @@ extern "C" {
 int32_t sdsp_debug_set_test_hooks(int64_t fail_chunk, const int32_t* devices, uint32_t n_devices,
                                   int32_t stft_frame_parallel);
 
+/*
+ * Schedule knobs, process-wide (0 = the product's schedule): serial_streams != 0 runs the key path
+ * on the main stream (per-kernel profiling); no_key_defer != 0 joins each sub-batch's key stream at
+ * its own end instead of one sub-batch late; no_row_reuse != 0 recomputes the escalation passes'
+ * hop-512 rows instead of reading the base pass's; host_trace != 0 prints per-stage host times on
+ * stderr; batch_chunk_tracks > 0 sets sdsp_analyze_batch's chunk size (default 512 tracks);
+ * hbm_budget_gb > 0 sets the sub-batch HBM budget (default: 80 % of free HBM / 1.125).  Every
+ * setting gives the same results; the tests use them to reach the other schedules and the tools
+ * to profile.  The Python layer maps SDSP_SERIAL_STREAMS, SDSP_NO_KEY_DEFER, SDSP_NO_ROW_REUSE,
+ * SDSP_HOST_TRACE, SDSP_BATCH_CHUNK_TRACKS and SDSP_HBM_BUDGET_GB onto this call; the library
+ * itself reads no environment variable.
+ */
+int32_t sdsp_debug_set_schedule(int32_t serial_streams, int32_t no_key_defer, int32_t no_row_reuse, int32_t host_trace,
+                                uint64_t batch_chunk_tracks, double hbm_budget_gb);
+
 /* Free and total HBM bytes of `device` (the benchmark sizes its kernel probe by them). */
 int32_t sdsp_debug_mem_info(int32_t device, uint64_t* free_bytes, uint64_t* total_bytes);
 

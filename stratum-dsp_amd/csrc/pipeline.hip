@@ -884,7 +884,8 @@ void Pipeline::run(const float* d_samples, const std::vector<uint64_t>& in_off, 
             for (auto& kv : d_.bufs) held += (double)kv.second->bytes;
             budget = std::max(4e9, ((double)fr + held) * 0.80 / 1.125);
         }
-        if (const char* e = std::getenv("SDSP_HBM_BUDGET_GB")) budget = std::max(1.0, std::atof(e)) * 1e9;
+        // schedule knob (sdsp_debug_set_schedule): the tests' several-sub-batch paths
+        if (const double gb = test_hooks().hbm_budget_gb.load(); gb > 0.0) budget = std::max(1.0, gb) * 1e9;
     }
     const uint64_t hop = cfg_.hop_size, khop = (uint64_t)khop_;
     std::vector<int> cur;
@@ -1412,7 +1413,7 @@ void Pipeline::finish_key(std::vector<TrackRes>& res) {
 }
 
 struct HostTrace {
-    bool on = std::getenv("SDSP_HOST_TRACE") != nullptr;
+    bool on = test_hooks().host_trace.load() != 0;  // sdsp_debug_set_schedule
     std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now(), tp = t0;
     void operator()(const char* tag) {
         if (!on) return;
@@ -1590,8 +1591,8 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     // what the main stream uploads for the key stream (read by it before the sub-batch's join)
     sb_parity_ ^= 1;
     const std::string EP = sb_parity_ ? "E1." : "E0.";
-    // SDSP_SERIAL_STREAMS=1 keeps the key path on the main stream (per-kernel profiling)
-    static const bool serial_streams = std::getenv("SDSP_SERIAL_STREAMS") != nullptr;
+    // schedule knob (sdsp_debug_set_schedule): the key path on the main stream (per-kernel profiling)
+    const bool serial_streams = test_hooks().serial_streams.load() != 0;
     hipStream_t st2 = serial_streams ? st : d_.stream2;
     hipStream_t st3 = serial_streams ? st : d_.stream3;  // the key vote
     float* d_tune = nullptr;  // per key track tuning offset (tuning compensation)
@@ -1961,7 +1962,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         for (int k = 0; k < NE; k++) ein.base_row0.push_back(b512.fpfx[own512 ? (size_t)k : (size_t)E[(size_t)k]]);
         ein.top_n = aux_k;
         ein.cand_cap = aux_k;
-        const bool reuse_on = std::getenv("SDSP_NO_ROW_REUSE") == nullptr;  // read per call (tests flip it)
+        const bool reuse_on = test_hooks().no_row_reuse.load() == 0;  // the tests' control (sdsp_debug_set_schedule)
         ein.hop = 256;
         ein.reuse = reuse_on ? 2 : 0;
         tempo_pass("C256.", ein, o256);
@@ -2203,9 +2204,9 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     finish_key(res);
     // late join by default (+2 % in alternating bench runs on one box, 2,350 vs 2,301 tracks/s:
     // the main stream otherwise idles ~45 ms per sub-batch waiting for the key tail);
-    // SDSP_NO_KEY_DEFER=1 joins at the end of each sub-batch (the tests' control)
+    // no_key_defer (sdsp_debug_set_schedule) joins at the end of each sub-batch (the tests' control)
     const bool defer_key =
-        NK > 0 && !beat_sync && !serial_streams && !dbg_on && std::getenv("SDSP_NO_KEY_DEFER") == nullptr;
+        NK > 0 && !beat_sync && !serial_streams && !dbg_on && test_hooks().no_key_defer.load() == 0;
     if (defer_key) {
         key_pending_.reset(new KeyPending());
         key_pending_->kt = std::move(ktp);
@@ -2564,7 +2565,7 @@ int32_t sdsp_analyze_batch(const float* const* tracks, const uint64_t* lens, uin
             if (device_mask == 0 ? d == 0 : ((device_mask >> d) & 1u)) devs.push_back(d);
     if (devs.empty()) devs.push_back(0);
     uint64_t max_tracks = 512;
-    if (const char* e = std::getenv("SDSP_BATCH_CHUNK_TRACKS")) max_tracks = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
+    if (const uint64_t t = test_hooks().batch_chunk_tracks.load()) max_tracks = t;  // sdsp_debug_set_schedule
     const std::vector<uint64_t> cb = plan_chunks(lens, n_tracks, max_tracks, (uint64_t)2 << 30 /* 8 GB of f32 */);
     // test hook (sdsp_debug_set_test_hooks): the chunk whose analysis throws (the per-chunk failure path)
     const long fail_chunk = test_hooks().fail_chunk.load();

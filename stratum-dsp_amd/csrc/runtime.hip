@@ -278,6 +278,18 @@ int32_t sdsp_debug_set_test_hooks(int64_t fail_chunk, const int32_t* devices, ui
     return SDSP_OK;
 }
 
+int32_t sdsp_debug_set_schedule(int32_t serial_streams, int32_t no_key_defer, int32_t no_row_reuse, int32_t host_trace,
+                                uint64_t batch_chunk_tracks, double hbm_budget_gb) {
+    TestHooks& h = test_hooks();
+    h.serial_streams.store(serial_streams != 0);
+    h.no_key_defer.store(no_key_defer != 0);
+    h.no_row_reuse.store(no_row_reuse != 0);
+    h.host_trace.store(host_trace != 0);
+    h.batch_chunk_tracks.store(batch_chunk_tracks);
+    h.hbm_budget_gb.store(hbm_budget_gb > 0.0 ? hbm_budget_gb : 0.0);
+    return SDSP_OK;
+}
+
 int32_t sdsp_debug_mem_info(int32_t device, uint64_t* free_bytes, uint64_t* total_bytes) {
     try {
         SDSP_HIP_CHECK(hipSetDevice(device));

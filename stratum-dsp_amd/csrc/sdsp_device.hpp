@@ -17,7 +17,8 @@ constexpr int WAVE = 64;
 
 // Raises the issuing wave's priority on its SIMD.  Used at the top of the short, latency-bound
 // tempo-path kernels so that, running beside the key stream's VALU-heavy STFT waves, they are
-// not starved of issue slots (the main stream is the pipeline's critical path).
+// not starved of issue slots (their one-wave-per-track chains would otherwise stretch the tempo
+// stream by far more than they cost the STFT).
 #ifdef SDSP_NO_SETPRIO
 #define SDSP_LATENCY_CRITICAL() ((void)0)
 #else

@@ -99,12 +99,19 @@ struct DeviceCtx {
 
 DeviceCtx& device_ctx(int device);
 
-// Test hooks, set only through sdsp_debug_set_test_hooks (never from the environment): an
-// injected chunk failure, a worker device list for sdsp_analyze_batch, and the frame-parallel
-// STFT kernel forced for every hop.
+// Test hooks, set only through sdsp_debug_set_test_hooks / sdsp_debug_set_schedule (never from
+// the environment): an injected chunk failure, a worker device list for sdsp_analyze_batch, the
+// frame-parallel STFT kernel forced for every hop, and the schedule knobs below.
 struct TestHooks {
     std::atomic<long> fail_chunk{-1};
     std::atomic<int> stft_frame_parallel{0};
+    // schedule knobs (sdsp_debug_set_schedule; 0 = the product's schedule): the key path on the
+    // main stream (per-kernel profiling), the key join at the end of each sub-batch, the
+    // escalation passes without hop-512 row reuse, a per-stage host trace on stderr, the
+    // sdsp_analyze_batch chunk size, and the sub-batch HBM budget in GB
+    std::atomic<int> serial_streams{0}, no_key_defer{0}, no_row_reuse{0}, host_trace{0};
+    std::atomic<uint64_t> batch_chunk_tracks{0};
+    std::atomic<double> hbm_budget_gb{0.0};
     std::mutex mu;
     std::vector<int> devices;
 };

@@ -121,6 +121,31 @@ def test_hooks(fail_chunk=-1, devices=(), stft_frame_parallel=False):
         f(-1, None, 0, 0)
 
 
+_SCHEDULE_ENV = ("SDSP_SERIAL_STREAMS", "SDSP_NO_KEY_DEFER", "SDSP_NO_ROW_REUSE", "SDSP_HOST_TRACE",
+                 "SDSP_BATCH_CHUNK_TRACKS", "SDSP_HBM_BUDGET_GB")
+_schedule_set = None
+
+
+def _schedule_from_env():
+    """The library reads no environment variable: the test and profiling schedule switches
+    (SDSP_SERIAL_STREAMS, SDSP_NO_KEY_DEFER, SDSP_NO_ROW_REUSE, SDSP_HOST_TRACE,
+    SDSP_BATCH_CHUNK_TRACKS, SDSP_HBM_BUDGET_GB) are read here, before each analysis call, and passed
+    through sdsp_debug_set_schedule (include/stratum_hip_debug.h) when they change."""
+    global _schedule_set
+    e = os.environ
+    knobs = (int(bool(e.get("SDSP_SERIAL_STREAMS"))), int(bool(e.get("SDSP_NO_KEY_DEFER"))),
+             int(bool(e.get("SDSP_NO_ROW_REUSE"))), int(bool(e.get("SDSP_HOST_TRACE"))),
+             max(int(e.get("SDSP_BATCH_CHUNK_TRACKS") or 0), 0), max(float(e.get("SDSP_HBM_BUDGET_GB") or 0.0), 0.0))
+    if knobs == _schedule_set:
+        return
+    f = lib().sdsp_debug_set_schedule
+    f.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_uint64, C.c_double]
+    f.restype = C.c_int32
+    if f(*knobs) != 0:
+        raise RuntimeError("sdsp_debug_set_schedule failed")
+    _schedule_set = knobs
+
+
 def default_config():
     """AnalysisConfig::default() (reference src/config.rs:594-744)."""
     c = SdspConfig()
@@ -138,6 +163,7 @@ def analyze_audio(samples, sample_rate=44100, config=None):
     cfg = config if config is not None else default_config()
     r = SdspResult()
     err = C.create_string_buffer(512)
+    _schedule_from_env()
     st = lib().sdsp_analyze_audio(_fp(x), x.size, sample_rate, C.byref(cfg), C.byref(r), err, 512)
     if st != 0:
         raise AnalysisError(st, err.value.decode())
@@ -165,6 +191,7 @@ def analyze_batch(tracks, sample_rate=44100, config=None, device_mask=0, strict=
     lens = np.array([a.size for a in arrs], dtype=np.uint64)
     outs = (SdspResult * n)()
     cfg = config if config is not None else default_config()
+    _schedule_from_env()
     st = lib().sdsp_analyze_batch(ptrs, lens.ctypes.data_as(C.POINTER(C.c_uint64)), n, sample_rate, C.byref(cfg),
                                   device_mask, outs)
     if st != 0 and strict:
@@ -272,6 +299,7 @@ def analyze_batch_device(d_ptr, offsets, lens, sample_rate=44100, config=None, d
     n = ln.size
     outs = (SdspResult * n)()
     cfg = config if config is not None else default_config()
+    _schedule_from_env()
     st = lib().sdsp_analyze_batch_device_ex(C.c_void_p(d_ptr), offs.ctypes.data_as(C.POINTER(C.c_uint64)),
                                             ln.ctypes.data_as(C.POINTER(C.c_uint64)), n, sample_rate, C.byref(cfg),
                                             device, C.c_void_p(stream or 0), stages, outs)
