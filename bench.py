@@ -188,6 +188,9 @@ def main():
     ap.add_argument("--no-probe", action="store_true", help="skip the isolated STFT probe (A/B runs)")
     ap.add_argument("--bpm-mode", type=int, default=-1, help="synthetic BPM mix (-1 = the workload's; 1 = config 5)")
     ap.add_argument("--dry-run", action="store_true", help="host-logic rehearsal without a GPU (tests)")
+    ap.add_argument("--share-device", action="store_true",
+                    help="rehearsal on a box with fewer GPUs than ranks: every rank runs on device 0 (the "
+                         "line is labelled; not a scaling measurement)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -199,7 +202,7 @@ def main():
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     cfg_no, n_default, mix_default, stage_mask = WORKLOADS[args.workload]
     bpm_mode = mix_default if args.bpm_mode < 0 else args.bpm_mode
-    eng = (DryEngine if args.dry_run else Engine)(local)
+    eng = (DryEngine if args.dry_run else Engine)(0 if args.share_device else local)
     tdist = None
     if args.dry_run and os.environ.get("SDSP_BENCH_FAIL_RANK") == str(rank):
         raise SystemExit(3)  # test hook (dry runs only): this rank dies before the process group
@@ -343,7 +346,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (seeded on-device generator: kick/hat/triad/diatonic line, 44.1 kHz mono)"
-            + (" [DRY RUN: no GPU, not a measurement]" if args.dry_run else ""),
+            + (" [DRY RUN: no GPU, not a measurement]" if args.dry_run else "")
+            + (f" [REHEARSAL: {world} ranks sharing device 0, not a scaling measurement]" if args.share_device else ""),
             "config": {
                 "workload": wl,
                 "baseline_config": cfg_no if world == 1 or cfg_no != 2 else 3,

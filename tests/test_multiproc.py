@@ -147,3 +147,11 @@ def test_bench_eight_ranks_config3_shards():
     assert c["tracks_per_step_all_ranks"] == 8192 == sum(x["tracks"] for x in sh)
     ranges = sorted((x["seed0"], x["seed0"] + x["tracks"]) for x in sh)
     assert all(a[1] <= b[0] for a, b in zip(ranges, ranges[1:]))  # disjoint
+
+
+def test_bench_share_device_rehearsal_is_labelled():
+    """--share-device (a multi-rank rehearsal on a box with fewer GPUs than ranks: every rank on
+    device 0) labels its line, so it cannot pass for a scaling measurement."""
+    d = _bench_json([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0",
+                     "--tracks", "2", "--seconds", "1", "--dry-run", "--share-device"])
+    assert d["n_gpus"] == 2 and "REHEARSAL: 2 ranks sharing device 0" in d["data"]
