@@ -15,7 +15,7 @@ for i in $(seq 1 $n); do
     : > $O/${mode}_${i}_smi.txt
     sleep 4
     while kill -0 $pid 2>/dev/null; do
-      timeout 10 rocm-smi --showclocks --showpower >> $O/${mode}_${i}_smi.txt 2>&1
+      timeout 10 rocm-smi --showclocks --showpower --showtemp >> $O/${mode}_${i}_smi.txt 2>&1
       sleep 0.5
     done
     wait $pid || { echo "bench $mode $i failed"; tail -3 $O/${mode}_$i.err; exit 1; }
