@@ -56,8 +56,19 @@ def test_no_test_switch_read_from_environment():
     """The shipping library reads no test hook from the environment (they are set only through
     sdsp_debug_set_test_hooks), so a user's environment cannot fail or re-route real work."""
     data = open(sdsp.lib()._name, "rb").read()
-    for name in (b"SDSP_TEST_FAIL_CHUNK", b"SDSP_DEVICE_LIST", b"SDSP_STFT_FRAME_PARALLEL"):
+    for name in (b"SDSP_TEST_FAIL_CHUNK", b"SDSP_DEVICE_LIST", b"SDSP_STFT_FRAME_PARALLEL", b"SDSP_SERIAL_STREAMS",
+                 b"SDSP_NO_KEY_DEFER", b"SDSP_NO_ROW_REUSE", b"SDSP_HOST_TRACE", b"SDSP_BATCH_CHUNK_TRACKS",
+                 b"SDSP_HBM_BUDGET_GB"):
         assert name not in data, name
+
+
+def test_library_reads_no_environment():
+    """The schedule switches reach the library only through sdsp_debug_set_schedule (the Python
+    layer maps the SDSP_* variables onto it): no source of the shipping library calls getenv."""
+    src = os.path.join(ROOT, "stratum-dsp_amd", "csrc")
+    for f in sorted(os.listdir(src)):
+        if f.endswith((".hip", ".hpp", ".h", ".cpp")):
+            assert "getenv" not in open(os.path.join(src, f)).read(), f
 
 
 def test_version():
