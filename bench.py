@@ -191,6 +191,9 @@ def main():
     ap.add_argument("--share-device", action="store_true",
                     help="rehearsal on a box with fewer GPUs than ranks: every rank runs on device 0 (the "
                          "line is labelled; not a scaling measurement)")
+    ap.add_argument("--rank-shard", type=int, default=-1,
+                    help="config 3 on a one-GPU box: run rank R's shard of an 8-rank job (seeds R*tracks ..) "
+                         "alone on device 0 (the line is labelled; not a scaling measurement)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -217,7 +220,12 @@ def main():
 
     sr = 44100
     n = args.tracks or n_default
-    seed0 = shard_seed0(rank, n)
+    shard_rank = rank
+    if args.rank_shard >= 0:
+        if world != 1:
+            raise SystemExit("bench.py: --rank-shard runs one shard in one process (--gpus 1)")
+        shard_rank = args.rank_shard
+    seed0 = shard_seed0(shard_rank, n)
     lens = track_lengths(args.workload, n, args.seconds, sr, seed0)
     buf, offs = eng.generate(lens, sr, seed0, bpm_mode)
 
@@ -227,11 +235,11 @@ def main():
         eng.analyze(buf, offs, lens, sr, stage_mask).free()
     barrier()
     eng.synchronize()
-    clock = ClockSampler(local) if (rank == 0 and not args.dry_run) else None
+    clock = ClockSampler(eng.dev) if (rank == 0 and not args.dry_run) else None
     if clock:
         clock.__enter__()
     t0 = time.perf_counter()
-    stft = {"ms8": 0.0, "b8": 0.0, "l8": 0, "ms2": 0.0, "b2": 0.0, "l2": 0}
+    stft = {"ms8": 0.0, "b8": 0.0, "l8": 0, "f8": 0, "ms2": 0.0, "b2": 0.0, "l2": 0, "f2": 0}
     step_s = []
     res = None
     for _ in range(args.steps):
@@ -247,6 +255,8 @@ def main():
         stft["ms2"] += st["stft2048_ms"]
         stft["b2"] += st["stft2048_bytes"]
         stft["l2"] += st["stft2048_launches"]
+        stft["f8"] += st.get("stft8192_frames", 0)
+        stft["f2"] += st.get("stft2048_frames", 0)
     eng.synchronize()
     barrier()
     dt = max_over_ranks(time.perf_counter() - t0, tdist)
@@ -254,7 +264,7 @@ def main():
         clock.__exit__(None, None, None)
     # every rank's shard (rank, tracks, first seed), gathered for the report: the ranks' tracks
     # must be disjoint and sum to the job's batch (config 3: 8 x 1024 = 8192)
-    shard = {"rank": rank, "tracks": n, "seed0": seed0}
+    shard = {"rank": shard_rank, "tracks": n, "seed0": seed0}
     shards = [shard]
     if tdist is not None:
         shards = [None] * world
@@ -282,7 +292,7 @@ def main():
         if ratio is not None:
             traffic = round(ratio * bytes_per_launch)
     roofline = {
-        "bound": "hbm",
+        "bound": None,  # set below from the measured HBM and VALU-issue fractions
         "kernel": "k_stft_slide8w3 (key STFT, 8192/512)" if key_k else "k_stft_slide2s (tempo STFT, 2048/512)",
         "achieved": round(achieved, 2),
         "peak": HBM_PEAK_GBS,
@@ -301,13 +311,21 @@ def main():
         # the same kernel launched alone (nothing else on the chip): the kernel's own bandwidth, as
         # opposed to `achieved` above, which is measured inside the two-stream pipeline where the
         # tempo path shares the CUs (tools/stft_probe.py)
-        roofline["isolated"] = isolated_stft(8192 if key_k else 2048, 512, int(lens.max()) if len(lens) else 0)
+        roofline["isolated"] = isolated_stft(8192 if key_k else 2048, 512, int(lens.max()) if len(lens) else 0,
+                                             sclk=clock.report() if clock else None)
 
     cpu = None
     parity = None
     extras = {}
     if clock and clock.report():
         extras["sclk_mhz_timed"] = clock.report()
+    # The kernel's other roofline: VALU issue.  valu_frac = VALU wave-instructions the launches
+    # issued (the frame loop's census from the kernel's ISA, profiles/isa_census_stft.json, x the
+    # frames computed) / what the chip can issue in the launch time (1,024 SIMDs, one wave64 VALU
+    # instruction per 2 cycles, MI355X_MICROARCH.md) at the shader clock sampled while it ran (the
+    # 2,400 MHz peak when none was sampled).  "bound" names the larger of the two fractions.
+    roofline.update(valu_roofline(key_k, stft, extras.get("sclk_mhz_timed")))
+    roofline["bound"] = "valu-issue" if (roofline.get("valu_frac") or 0) > roofline["frac"] else "hbm"
     ss = sorted(step_s)
     extras["step_ms"] = {"median": round(1e3 * ss[len(ss) // 2], 3), "min": round(1e3 * ss[0], 3),
                          "max": round(1e3 * ss[-1], 3), "all": [round(1e3 * t, 3) for t in step_s]}
@@ -347,7 +365,9 @@ def main():
             "dtype": "f32",
             "data": "synthetic (seeded on-device generator: kick/hat/triad/diatonic line, 44.1 kHz mono)"
             + (" [DRY RUN: no GPU, not a measurement]" if args.dry_run else "")
-            + (f" [REHEARSAL: {world} ranks sharing device 0, not a scaling measurement]" if args.share_device else ""),
+            + (f" [REHEARSAL: {world} ranks sharing device 0, not a scaling measurement]" if args.share_device else "")
+            + (f" [CONFIG-3 SHARD: rank {shard_rank}'s 1024-track seed range of the 8-GPU job, alone on device 0; "
+               "not a scaling measurement]" if args.rank_shard >= 0 else ""),
             "config": {
                 "workload": wl,
                 "baseline_config": cfg_no if world == 1 or cfg_no != 2 else 3,
@@ -362,6 +382,9 @@ def main():
             },
             "errors": n_err,
             "stage_ms_last_step": {k: round(v, 3) for k, v in stages.items() if k.endswith("_ms")},
+            # tracks of the last step analysed again with the sequential key-energy fold (their key
+            # vote was near a decision under the block-folded energies)
+            "key_reruns_last_step": int(stages.get("key_reruns", 0)),
             "roofline": roofline,
             "cpu_baseline": cpu,
             "parity_sample": parity,
@@ -373,26 +396,40 @@ def main():
 
 
 class ClockSampler:
-    """Samples the shader clock of GPU `gpu` (rocm-smi --showclocks, about once a second) on a
-    daemon thread while the timed steps run.  The box runs bench processes in one of two clock
-    states (~2.0 vs ~1.75 GHz), so the line reports which one it measured.  Host-side
-    only (a sysfs read through rocm-smi); absent rocm-smi, it reports nothing."""
+    """Samples the shader clock of HIP device `dev` about once a second on a daemon thread while the
+    timed steps run: the current level (the line marked *) of its card's sysfs pp_dpm_sclk, the
+    card found by the device's PCI bus id (sdsp_debug_device_pci_bus_id), so HIP_VISIBLE_DEVICES /
+    ROCR_VISIBLE_DEVICES renumbering cannot point it at another card, and no subprocess runs inside
+    the timed window.  The box runs bench processes in one of two clock states (~2.0 vs ~1.75 GHz,
+    DESIGN.md §6), so the line reports which one it measured.  Absent the file, it reports nothing."""
 
-    def __init__(self, gpu=0):
-        import shutil
+    def __init__(self, dev=0):
         import threading
 
-        self.gpu, self.mhz, self.stop = gpu, [], threading.Event()
-        self.exe = shutil.which("rocm-smi")
-        self.th = threading.Thread(target=self._run, daemon=True) if self.exe else None
+        self.mhz, self.stop, self.path = [], threading.Event(), None
+        try:
+            import ctypes as C
+
+            b = C.create_string_buffer(64)
+            L = sdsp.lib()
+            L.sdsp_debug_device_pci_bus_id.argtypes = [C.c_int32, C.c_char_p, C.c_uint32]
+            if L.sdsp_debug_device_pci_bus_id(dev, b, 64) == 0:
+                p = os.path.join("/sys/bus/pci/devices", b.value.decode().lower(), "pp_dpm_sclk")
+                if os.path.exists(p):
+                    self.path, self.bus = p, b.value.decode().lower()
+        except Exception:
+            self.path = None
+        self.th = threading.Thread(target=self._run, daemon=True) if self.path else None
 
     def _run(self):
-        pat = re.compile(r"GPU\[%d\].*sclk clock level: \d+: \((\d+)Mhz\)" % self.gpu)
+        pat = re.compile(r"(\d+)\s*Mhz\s*\*", re.I)
         while not self.stop.is_set():
             try:
-                out = subprocess.run([self.exe, "--showclocks"], capture_output=True, text=True, timeout=10).stdout
-                self.mhz += [int(m) for m in pat.findall(out)]
-            except Exception:
+                with open(self.path) as f:
+                    m = pat.search(f.read())
+                if m:
+                    self.mhz.append(int(m.group(1)))
+            except OSError:
                 return
             self.stop.wait(1.0)
 
@@ -410,10 +447,35 @@ class ClockSampler:
         if not self.mhz:
             return None
         v = sorted(self.mhz)
-        return {"median": v[len(v) // 2], "min": v[0], "max": v[-1], "samples": len(v), "source": "rocm-smi --showclocks"}
+        return {"median": v[len(v) // 2], "min": v[0], "max": v[-1], "samples": len(v),
+                "source": f"sysfs pp_dpm_sclk of PCI {self.bus} (the HIP device's card)"}
 
 
-def isolated_stft(nfft, hop, length, tracks=256, reps=3):
+CENSUS_KERNELS = {True: "k_stft_slide8w3ILi1E", False: "k_stft_slide2sILi4ELb1E"}
+
+
+def valu_roofline(key_k, stft, sclk):
+    """VALU-issue fraction of the dominant STFT kernel's launches (see the caller)."""
+    path = os.path.join(ROOT, "profiles", "isa_census_stft.json")
+    tag = "8" if key_k else "2"
+    frames, ms, nl = stft["f" + tag], stft["ms" + tag], max(stft["l" + tag], 1)
+    if not os.path.exists(path) or frames <= 0 or ms <= 0:
+        return {"valu_frac": None}
+    with open(path) as f:
+        census = json.load(f)["kernels"]
+    ent = next((v for k, v in census.items() if CENSUS_KERNELS[key_k] in k), None)
+    if ent is None:
+        return {"valu_frac": None}
+    mhz = float(sclk["median"]) if sclk else 2400.0
+    issued = ent["valu_per_frame"] * frames / nl
+    capacity = (ms / nl) * 1e-3 * 1024 * mhz * 1e6 / 2.0
+    return {"valu_frac": round(issued / capacity, 4), "valu_per_frame": ent["valu_per_frame"],
+            "frames_per_launch": round(frames / nl, 1), "valu_sclk_mhz": mhz,
+            "valu_method": "frame-loop VALU census from the kernel's ISA (tools/isa_census.py, "
+                           "profiles/isa_census_stft.json) x frames / (launch time x 1024 SIMDs x sclk / 2)"}
+
+
+def isolated_stft(nfft, hop, length, tracks=256, reps=3, sclk=None):
     """sdsp_probe_stft: `reps` launches of the STFT kernel alone over `tracks` device-resident
     noise tracks of `length` samples, HIP events on its stream.  256 3-min tracks are 62k
     workgroups of the 8192-point kernel (80 per workgroup slot of the chip), so the launch measures
@@ -436,7 +498,10 @@ def isolated_stft(nfft, hop, length, tracks=256, reps=3):
     if f(0, nfft, hop, tracks, length, reps, stride, C.byref(ms), C.byref(by)) != 0:
         return None
     gbs = by.value / (ms.value * 1e-3) / 1e9
+    vr = valu_roofline(nfft == 8192, {"f8": tracks * frames, "ms8": ms.value, "l8": 1, "f2": tracks * frames,
+                                      "ms2": ms.value, "l2": 1}, sclk)
     return {"kernel": "k_stft_slide8w3" if nfft == 8192 else "k_stft_slide2s", "tracks": tracks, "ms_per_launch": round(ms.value, 3),
+            "valu_frac": vr.get("valu_frac"), "valu_sclk_mhz": vr.get("valu_sclk_mhz"),
             "ms_per_track": round(ms.value / tracks, 5), "achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
             "method": "sdsp_probe_stft: the kernel launched alone on device-resident noise tracks of the workload's "
                       "length, HIP events, mean of 3 launches"}
@@ -511,7 +576,12 @@ def cpu_baseline(buf, offs, lens, res, n, sr, args):
     per_track = [o[1] for o in outs]
     outs = [o[0] for o in outs]
     match = sum(1 for i, (st, ref) in enumerate(outs) if st == 0 and not parity.diff_results(res[i], ref))
-    exact = sum(1 for i, (st, ref) in enumerate(outs) if st == 0 and parity.exact_fraction(res[i], ref) == 1.0)
+    # bit_exact: every field bit for bit (strict); bit_exact_except_key_energy: every field but the
+    # default key path's two block-folded energy fields, which diff_results checks
+    # within the north star's 1e-4 (within_tolerance)
+    exact = sum(1 for i, (st, ref) in enumerate(outs) if st == 0 and parity.exact_fraction(res[i], ref, strict=True) == 1.0)
+    exact_nk = sum(1 for i, (st, ref) in enumerate(outs) if st == 0 and parity.exact_fraction(res[i], ref) == 1.0)
+    key_eq = sum(1 for i, (st, ref) in enumerate(outs) if st == 0 and res[i]["key"] == ref["key"])
     cpu = {
         "value": round(k / dt, 4),
         "unit": "tracks/s",
@@ -538,7 +608,8 @@ def cpu_baseline(buf, offs, lens, res, n, sr, args):
         one(x)
     cpu["value_1thread"] = round(k1 / (time.perf_counter() - t0), 4)
     cpu["value_1thread_sample"] = f"{k1} tracks, alone on one thread"
-    par = {"checked": k, "within_tolerance": match, "bit_exact": exact}
+    par = {"checked": k, "within_tolerance": match, "key_equal": key_eq, "bit_exact": exact,
+           "bit_exact_except_key_energy": exact_nk}
     return cpu, par
 
 

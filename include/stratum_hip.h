@@ -363,6 +363,11 @@ typedef struct sdsp_stage_times {
     uint64_t stft8192_launches;
     double stft2048_bytes;  /* algorithmic bytes: 4*N_in + 4*F*(nfft/2+1) per STFT */
     double stft8192_bytes;
+    uint64_t stft2048_frames; /* frames the STFT launches computed (the VALU census is per frame) */
+    uint64_t stft8192_frames;
+    uint64_t key_reruns;      /* tracks analysed again with the sequential key-energy fold (near a
+                                 key decision under the block-folded energies) */
+    double rerun_ms;          /* wall time of that rerun (included in total_ms) */
 } sdsp_stage_times;
 int32_t sdsp_last_stage_times(int32_t device, sdsp_stage_times* out);
 

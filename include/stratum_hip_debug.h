@@ -11,6 +11,8 @@
 
 #include <stdint.h>
 
+#include "stratum_hip.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -40,8 +42,26 @@ int32_t sdsp_debug_set_test_hooks(int64_t fail_chunk, const int32_t* devices, ui
 int32_t sdsp_debug_set_schedule(int32_t serial_streams, int32_t no_key_defer, int32_t no_row_reuse, int32_t host_trace,
                                 uint64_t batch_chunk_tracks, double hbm_budget_gb);
 
+/*
+ * 1 when `cfg` at `sample_rate` takes the default key path's band-limited mask with HPCP frame
+ * energies folded in 64-bin blocks (k_mask_rp / k_hpcp_band: key_confidence and key_clarity are
+ * then a re-associated sum of the reference's), 0 when it keeps the reference's
+ * single sequential energy fold, -1 on a NULL config or a zero rate.  No device is touched.
+ */
+int32_t sdsp_debug_key_energy_blocked(const sdsp_config* cfg, uint32_t sample_rate);
+
+/*
+ * Per track of the last analysis call on `device` (n entries): 1 where the block-folded key
+ * energies left a key decision within its margin, so the track was analysed again with the
+ * sequential energy fold (sdsp_stage_times.key_reruns counts them), else 0.
+ */
+int32_t sdsp_debug_last_key_near(int32_t device, uint8_t* out, uint64_t n);
+
 /* Free and total HBM bytes of `device` (the benchmark sizes its kernel probe by them). */
 int32_t sdsp_debug_mem_info(int32_t device, uint64_t* free_bytes, uint64_t* total_bytes);
+
+/* PCI bus id of HIP device `device` ("dddd:bb:dd.f", NUL-terminated; len >= 13). */
+int32_t sdsp_debug_device_pci_bus_id(int32_t device, char* out, uint32_t len);
 
 /* Device allocations the engine has made so far (count, bytes): "a repeated call allocates nothing". */
 int32_t sdsp_debug_alloc_stats(uint64_t* n_allocs, uint64_t* bytes);

@@ -643,6 +643,7 @@ void analyze(const float* samples, size_t n, uint32_t sr, const sdsp_config& c, 
                                           : detect_key_weighted(chroma.data() + st * 12, seg_len, wp ? wp + st : nullptr,
                                                                 maj, mnr);
                     const float cl = key_clarity(sr_.scores, 24);
+                    if (g_key_trace) g_key_trace->push_back(cl);
                     if (cl >= min_cl) {
                         used++;
                         for (int i = 0; i < 24; i++) acc[sr_.order[i]] += sr_.scores[i] * cl;

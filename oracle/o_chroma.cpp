@@ -59,6 +59,14 @@ void l2_normalize(float* pc, float eps) {
 
 float frame_energy(const float* m, size_t bins) {
     float e = 0.0f;
+    if (g_block_energy) {  // the GPU's block order: 64-bin partial sums, then those in block order
+        for (size_t g = 0; g < bins; g += 64) {
+            float p = 0.0f;
+            for (size_t b = g; b < g + 64 && b < bins; b++) p += m[b] * m[b];
+            e += p;
+        }
+        return e;
+    }
     for (size_t b = 0; b < bins; b++) e += m[b] * m[b];
     return e;
 }

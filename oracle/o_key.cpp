@@ -8,6 +8,8 @@
 #include "oracle_internal.hpp"
 
 namespace orc {
+int g_block_energy = 0;
+std::vector<float>* g_key_trace = nullptr;
 
 // extractor.rs:1246-1290 + 1306-1349, streamed: the per-bin prefix sums are the reference's
 // sequential f32 prefix (prefix[t+1] = prefix[t] + x), kept in a ring of 2*margin+2 rows.
@@ -219,6 +221,7 @@ KeyResult detect_key_weighted(const float* ch, size_t frames, const float* w, co
     float sc[24];
     for (int k = 0; k < 12; k++) sc[k] = weighted_sum_dot(ch, frames, w, maj[k]);
     for (int k = 0; k < 12; k++) sc[12 + k] = weighted_sum_dot(ch, frames, w, mnr[k]);
+    if (g_key_trace) g_key_trace->insert(g_key_trace->end(), sc, sc + 24);
     float mM = 0.0f, mm = 0.0f;
     for (int k = 0; k < 12; k++) mM = sd_maxf(mM, sc[k]);
     for (int k = 0; k < 12; k++) mm = sd_maxf(mm, sc[12 + k]);
@@ -549,4 +552,18 @@ float sdsp_oracle_dot(const float* a, const float* b, uint64_t n) {
     for (uint64_t i = 0; i < n; i++) acc += a[i] * b[i];
     return acc;
 }
+}
+
+// study switches (oracle_internal.hpp): not used by the parity tests
+extern "C" void sdsp_oracle_study_block_energy(int32_t on) { orc::g_block_energy = on; }
+extern "C" void sdsp_oracle_study_key_trace(int32_t on) {
+    static std::vector<float> tr;
+    tr.clear();
+    orc::g_key_trace = on ? &tr : nullptr;
+}
+extern "C" uint64_t sdsp_oracle_study_key_trace_get(float* out, uint64_t cap) {
+    if (!orc::g_key_trace) return 0;
+    const uint64_t n = orc::g_key_trace->size();
+    for (uint64_t i = 0; i < n && i < cap; i++) out[i] = (*orc::g_key_trace)[(size_t)i];
+    return n;
 }

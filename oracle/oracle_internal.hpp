@@ -184,6 +184,13 @@ bool detect_key_multi_scale(const float* chroma, size_t frames, const float* wei
 // 0 on success or -(AnalysisError code) on error, with the message kept for
 // sdsp_oracle_probe_error().
 extern std::string g_probe_err;
+// Study switches (tools/key_near_study.py; never set by the parity tests): g_block_energy folds
+// each HPCP frame energy in 64-bin blocks the way the GPU's default key path does (k_mask_rp /
+// k_hpcp_band) instead of the reference's one sequential sum; g_key_trace, when
+// non-null, receives per detect_key_weighted call its 24 raw scores and, in segment voting, the
+// segment's clarity after them.
+extern int g_block_energy;
+extern std::vector<float>* g_key_trace;
 template <class F>
 int64_t probe_call(F f) {
     try {

@@ -551,6 +551,30 @@ __global__ __launch_bounds__(HP_FRAMES) SDSP_HPCP_ATTR void k_hpcp_band(const fl
 }
 
 // ----------------------------------------------------------------------------------------
+// KeyParams::near_check: whether a weight perturbation of the size the block-folded energies make
+// could change one of key_from_raw's discrete decisions on these raw scores: the within-mode
+// argmax (a top-two gap of at most KV_NEAR_CONF relative) or the normalisation guard.  The argmax
+// is what fixes the winners' normalised scores (exactly 1 each), so ties between the final
+// winners are exact and stay exact while these decisions hold.
+__device__ bool key_raw_near(const float raw[24]) {
+    bool near = false;
+    for (int m = 0; m < 2; m++) {
+        float t1 = 0.0f, t2 = 0.0f;  // the fold keeps 0 as the floor, as key_from_raw's max does
+        for (int k = 0; k < 12; k++) {
+            const float v = raw[12 * m + k];
+            if (v > t1) {
+                t2 = t1;
+                t1 = v;
+            } else if (v > t2) {
+                t2 = v;
+            }
+        }
+        near |= t1 > 0.0f && !(t1 - t2 > KV_NEAR_CONF * t1);
+        near |= sd_absf(t1 - 1e-9f) <= KV_NEAR_REL * 1e-9f;
+    }
+    return near;
+}
+
 __device__ void key_from_raw(const float raw[24], float sorted[24], int order[24]) {
     float sc[24];
     for (int k = 0; k < 24; k++) sc[k] = raw[k];
@@ -737,7 +761,7 @@ __global__ __launch_bounds__(KV_THREADS) void k_key_vote(const int* __restrict__
     __shared__ int misc[4];
     __shared__ int redi[KV_THREADS / 64];
     __shared__ float acc[48];
-    __shared__ int use_w_s, used_s;
+    __shared__ int use_w_s, used_s, near_s;
     __shared__ float totw_s;
     __shared__ float tpl[48][12];
     __shared__ int sc_len[KV_MAXSCALE], sc_pfx[KV_MAXSCALE + 1];
@@ -748,8 +772,9 @@ __global__ __launch_bounds__(KV_THREADS) void k_key_vote(const int* __restrict__
     const uint64_t g0 = frame_pfx[trk];
     float* cr = chroma_raw + g0 * 12;
     for (int k = threadIdx.x; k < 576; k += blockDim.x) tpl[k / 12][k % 12] = tmpl[k];
+    if (threadIdx.x == 0) near_s = 0;  // published by the barriers below before any reader
     if (F_all <= 0) {
-        if (threadIdx.x == 0) out[trk] = KeyOut{0, 0, 0.0f, 0.0f, 0, 0, 0};
+        if (threadIdx.x == 0) out[trk] = KeyOut{0, 0, 0.0f, 0.0f, 0, 0, 0, 0};
         return;
     }
     // chroma sharpening (src/lib.rs:1200-1208 -> chroma/normalization.rs:41-65), in place
@@ -865,7 +890,11 @@ __global__ __launch_bounds__(KV_THREADS) void k_key_vote(const int* __restrict__
         __syncthreads();
         __shared__ float sbuf[SEQ_CH];
         const float sw = block_seq_sum(w, F, sbuf);  // weights.iter().sum(), in order
-        if (threadIdx.x == 0) use_w_s = !(sw <= 1e-12f || used < 10);
+        if (threadIdx.x == 0) {
+            use_w_s = !(sw <= 1e-12f || used < 10);
+            // the unweighted fallback (src/lib.rs:1278-1285) is decided by a sum of energy-derived weights
+            if (P.near_check && sd_absf(sw - 1e-12f) <= KV_NEAR_REL * 1e-12f) near_s = 1;
+        }
     } else if (threadIdx.x == 0) {
         use_w_s = 0;
     }
@@ -951,6 +980,9 @@ __global__ __launch_bounds__(KV_THREADS) void k_key_vote(const int* __restrict__
         r.ok = 1;
         r.used_segments = used;
         r.weights_used = use_w;
+        // the key is the argmax of the accumulated scores: a relative gap in (0, margin] could flip
+        // it (an exact tie of winners is structural and stays exact, key_raw_near)
+        r.near = P.near_check && (near_s || (conf > 0.0f && !(conf > KV_NEAR_CONF)));
         out[trk] = r;
     };
     // full-slice detection: detect_key_weighted (+ the mode heuristic)
@@ -963,6 +995,7 @@ __global__ __launch_bounds__(KV_THREADS) void k_key_vote(const int* __restrict__
             float raw[24], sorted[24];
             int order[24];
             for (int k = 0; k < 24; k++) raw[k] = acc[k];
+            if (P.near_check && key_raw_near(raw)) near_s = 1;
             key_from_raw(raw, sorted, order);
             int key = order[0];
             float conf = sorted[0] > 0.0f ? sd_clampf((sorted[0] - sorted[1]) / sorted[0], 0.0f, 1.0f) : 0.0f;
@@ -1053,6 +1086,7 @@ __global__ __launch_bounds__(KV_THREADS) void k_key_vote(const int* __restrict__
         float raw[24], sorted[24];
         int order[24];
         for (int k = 0; k < 24; k++) raw[k] = row[k];
+        if (P.near_check && key_raw_near(raw)) near_s = 1;
         key_from_raw(raw, sorted, order);
         if (P.mh_on) {
             int key;
@@ -1069,7 +1103,9 @@ __global__ __launch_bounds__(KV_THREADS) void k_key_vote(const int* __restrict__
             row[24 + k] = (float)order[k];
         }
         row[48] = cl;
-        row[49] = cl >= (mode == 1 ? P.ms_min_cl : P.min_clarity) ? 1.0f : 0.0f;
+        const float gate = mode == 1 ? P.ms_min_cl : P.min_clarity;
+        row[49] = cl >= gate ? 1.0f : 0.0f;
+        if (P.near_check && sd_absf(cl - gate) <= KV_NEAR_CLARITY) near_s = 1;  // the segment gate (src/lib.rs:1380)
         row[50] = cl * sw;
     }
     __syncthreads();

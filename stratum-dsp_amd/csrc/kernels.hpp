@@ -172,13 +172,24 @@ struct KeyParams {
     float ms_min_cl;
     int ms_len[8];
     float ms_w[8];
+    // the default key path's block-folded frame energies are in use: report in
+    // KeyOut::near whether a discrete decision downstream of the energies is within a margin the
+    // re-association could cross, so the host reruns that track with the sequential fold
+    int near_check;
 };
+// near-decision margins (k_key_vote, KeyParams::near_check): a segment clarity within
+// KV_NEAR_CLARITY of its gate, a final (best - second) / best below KV_NEAR_CONF, or a weight sum
+// within KV_NEAR_REL of the 1e-12 fallback threshold.  The re-association moves clarities by
+// <= 1e-6 and relative score gaps by <= 1e-6 on every track measured (profiles/r05_key_scale.jsonl),
+// so the margins hold a factor of 100.
+constexpr float KV_NEAR_CLARITY = 1e-4f, KV_NEAR_CONF = 1e-4f, KV_NEAR_REL = 1e-3f;
 struct KeyOut {
     int mode, tonic;
     float conf, clarity;
     int ok;
     int used_segments;
     int weights_used;
+    int near;  // near_check only: some energy-dependent decision within its margin (rerun exactly)
 };
 
 // ---- k_chroma (opt-in chroma front-ends) ----

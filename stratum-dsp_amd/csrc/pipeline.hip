@@ -227,6 +227,34 @@ void band_bins(int B, float fres, float fmin, float fmax, int* lo, int* hi) {
     if (l >= 0) *lo = l, *hi = h;
 }
 
+// HPCP's peak band of the key spectrogram (bins pk_lo .. pk_hi; empty when lo > hi), and whether a
+// configuration takes the default key path's band-limited mask with block-folded frame energies
+// (k_mask_rp / k_hpcp_band): the harmonic mask at margin 12 and power 2, plain HPCP,
+// nothing else reading the masked spectrogram.  SDSP_KEY_EXACT_ENERGY builds never take it.
+void key_peak_band(const sdsp_config& c, uint32_t sr, int* lo, int* hi) {
+    const int kfs = (int)std::min<uint64_t>(key_fft(c), STFT_GEN_MAX);
+    band_bins(kfs / 2 + 1, (float)sr / (float)kfs, sd_maxf(100.0f, 20.0f), sd_minf(5000.0f, (float)sr / 2.0f), lo, hi);
+}
+bool key_energy_blocked(const sdsp_config& c, uint32_t sr) {
+#ifdef SDSP_KEY_EXACT_ENERGY
+    return false;
+#else
+    const bool use_log = c.enable_key_log_frequency;
+    const bool tuned = c.enable_key_tuning_compensation && !use_log;
+    const bool whiten = c.enable_key_hpcp_whitening && c.key_hpcp_whitening_smooth_bins >= 3;
+    const bool plain_hpcp = !use_log && c.enable_key_hpcp && !tuned && !whiten && !c.enable_key_hpcp_bass_blend;
+    int lo = 1, hi = 0;
+    key_peak_band(c, sr, &lo, &hi);
+    // the scoring whose energy-dependent decisions k_key_vote certifies (KeyParams::near_check):
+    // segment voting or the full slice, without the mode heuristic, ensemble or multi-scale voting
+    const bool plain_scoring = !c.enable_key_mode_heuristic && !c.enable_key_minor_harmonic_bonus &&
+                               !c.enable_key_ensemble && !(c.enable_key_multi_scale && c.key_multi_scale_lengths_len > 0);
+    return plain_hpcp && plain_scoring && !c.enable_key_hpss_harmonic && c.enable_key_harmonic_mask &&
+           mask_band_ok((int)c.key_spectrogram_smooth_margin, c.key_harmonic_mask_power) &&
+           !(c.enable_key_beat_synchronous && !c.enable_key_log_frequency) && lo <= hi;
+#endif
+}
+
 // estimate_tuning_offset_semitones_from_spectrogram over [80, 2000] Hz (src/lib.rs:1101-1109,
 // extractor.rs:98-140): the band is every bin with fmin <= f <= fmax
 TuningParams tuning_params(const sdsp_config& c, uint32_t sr, int B, float fres, int stride) {
@@ -525,6 +553,7 @@ struct TrackRes {
     int8_t mr_trig = -1, mr_used = -1, perc_trig = -1, perc_used = -1;
     bool has_cands = false;
     std::vector<sdsp_tempo_candidate> cands;
+    bool key_near = false;  // block-folded key energies near a decision: rerun with the sequential fold
 };
 
 // Configuration support (everything the default path and its numeric knobs need).
@@ -601,6 +630,7 @@ struct TempoPassOut {
     std::vector<int> active_h;
     double stft_ms = 0, feat_ms = 0, tempo_ms = 0;
     uint64_t stft_launch = 0;
+    uint64_t stft_frames = 0;
     double stft_bytes = 0;
 };
 
@@ -797,12 +827,13 @@ void print_debug(const sdsp_config& c, const TrackDbg& d) {
 // ---------------------------------------------------------------------------------------
 class Pipeline {
    public:
-    Pipeline(DeviceCtx& d, const sdsp_config& cfg, uint32_t sr, int stages = SDSP_STAGES_FULL)
+    Pipeline(DeviceCtx& d, const sdsp_config& cfg, uint32_t sr, int stages = SDSP_STAGES_FULL, bool exact_energy = false)
         : c_(d),
           d_(d),
           cfg_(cfg),
           sr_(sr),
           bpm_only_(stages == SDSP_STAGES_BPM_ONLY),
+          exact_energy_(exact_energy),
           fs_((int)std::min<uint64_t>(cfg.frame_size, STFT_GEN_MAX)),
           nb_(fs_ / 2 + 1),
           s2_(base_stride(fs_)),
@@ -821,6 +852,9 @@ class Pipeline {
     // SDSP_STAGES_BPM_ONLY: the tempo path alone (src/lib.rs:86-910); the key
     // stream and the beat grid are not run, their result fields keep their defaults
     bool bpm_only_ = false;
+    // the key path with the reference's sequential frame-energy fold (k_mask_r / k_hpcp) even where
+    // the band-limited mask applies: run_locked's rerun of tracks whose key vote was near a decision
+    bool exact_energy_ = false;
     // the tempo path's STFT: frame size (AnalysisConfig::frame_size), bins, row stride
     const int fs_, nb_, s2_;
     // the key path's STFT: frame size, hop, row stride (key_fft / key_hop)
@@ -1129,6 +1163,7 @@ void Pipeline::tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPa
     if (in.mags_in || in.reuse == 0) rm = RowMap{o.mags, o.mags, o.fmax, o.fmax, o.d_fpfx, nullptr, 1, 2, 2};
     tm.mark(1);
     o.stft_launch = stft_frames ? 1 : 0;
+    o.stft_frames = stft_frames;
     if (stft_frames) {
         double inb = 0;
         for (int t = 0; t < P_T; t++) inb += 4.0 * (double)in.n_trim[(size_t)t];
@@ -1407,6 +1442,7 @@ void Pipeline::finish_key(std::vector<TrackRes>& res) {
         r.key_tonic = ko.tonic;
         r.key_conf = ko.conf;
         r.key_clarity = ko.clarity;
+        r.key_near = ko.near != 0;
     }
     times_.stft8192_ms += kp->kt->ms(0, 1);
     times_.key_ms += kp->kt->ms(1, 2);
@@ -1639,21 +1675,12 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         HpcpParams hp{};
         hp.B = B8;
         hp.stride = ks_;
-        hp.pk_lo = 1;
-        hp.pk_hi = 0;
-        band_bins(B8, fres8, sd_maxf(100.0f, 20.0f), sd_minf(5000.0f, (float)sr_ / 2.0f), &hp.pk_lo, &hp.pk_hi);
+        key_peak_band(cfg_, sr_, &hp.pk_lo, &hp.pk_hi);
         hp.K = (int)std::max<uint64_t>(cfg_.key_hpcp_peaks_per_frame, 1);
         hp.hmax = (int)std::max<uint64_t>(cfg_.key_hpcp_num_harmonics, 1);
         hp.p = sd_clampf(cfg_.key_hpcp_mag_power, 0.05f, 1.0f);
-#ifdef SDSP_KEY_EXACT_ENERGY
-        constexpr bool band_ok = false;
-#else
-        constexpr bool band_ok = true;
-#endif
-        const bool plain_hpcp = !use_log && cfg_.enable_key_hpcp && !tuned && !whiten && !cfg_.enable_key_hpcp_bass_blend;
-        const bool band = band_ok && plain_hpcp && !cfg_.enable_key_hpss_harmonic && cfg_.enable_key_harmonic_mask &&
-                          mask_band_ok((int)cfg_.key_spectrogram_smooth_margin, cfg_.key_harmonic_mask_power) &&
-                          !(cfg_.enable_key_beat_synchronous && !cfg_.enable_key_log_frequency) && hp.pk_lo <= hp.pk_hi;
+        // sdsp_debug_key_energy_blocked answers the same; exact_energy_: the rerun of near-decision tracks
+        const bool band = key_energy_blocked(cfg_, sr_) && !exact_energy_;
         float* d_part = band ? c_.dev<float>("E.kpart", total8 * (uint64_t)((B8 + 63) / 64)) : nullptr;
         if (band) {
             launch_mask_band(mags8, ks_, B8, d_kpfx, d_kid, NK, cfg_.key_harmonic_mask_power, hp.pk_lo - 1, hp.pk_hi + 1,
@@ -1723,6 +1750,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         std::vector<float> tpl(576);
         key_templates(tpl.data());
         d_tpl = c_.up(EP + "tpl", tpl);
+        kp.near_check = band ? 1 : 0;
         kp.weighting = cfg_.enable_key_frame_weighting;
         kp.min_tonal = cfg_.key_min_tonalness;
         kp.tonal_pow = cfg_.key_tonalness_power;
@@ -1766,12 +1794,14 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         kt.mark(2, st3);
         SDSP_HIP_CHECK(hipEventRecord(d_.vote_done, st3));
         times_.stft8192_launches += 1;
+        times_.stft8192_frames += total8;
         times_.stft8192_bytes += key_in_bytes + 4.0 * (double)total8 * (double)B8;
     }
     TempoPassOut bo;
     tempo_pass("B.", bin, bo);
     times_.stft2048_ms += bo.stft_ms;
     times_.stft2048_launches += bo.stft_launch;
+    times_.stft2048_frames += bo.stft_frames;
     times_.stft2048_bytes += bo.stft_bytes;
     times_.features_ms += bo.feat_ms;
     times_.tempogram_ms += bo.tempo_ms;
@@ -1974,6 +2004,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         for (TempoPassOut* o : mr_passes) {
             times_.stft2048_ms += o->stft_ms;
             times_.stft2048_launches += o->stft_launch;
+            times_.stft2048_frames += o->stft_frames;
             times_.stft2048_bytes += o->stft_bytes;
             times_.features_ms += o->feat_ms;
             times_.tempogram_ms += o->tempo_ms;
@@ -2329,6 +2360,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         r.key_tonic = ko.tonic;
         r.key_conf = ko.conf;
         r.key_clarity = ko.clarity;
+        r.key_near = ko.near != 0;
     }
     if (dbg_on) {
         if (NK > 0) {  // src/lib.rs:1471-1538 (the beat-synchronous re-vote keeps the frame-level record)
@@ -2440,6 +2472,29 @@ int32_t run_locked(DeviceCtx& d, const float* d_samples, const uint64_t* offsets
     Pipeline p(d, *cfg, sr, stages);
     try {
         p.run(d_samples, off, ln, res);
+        // Certified block energies: a track whose key vote had an energy-dependent
+        // decision within its margin (KeyOut::near) is analysed again with the reference's sequential
+        // frame-energy fold, and that result replaces its own (the tempo fields are the same bits;
+        // the key fields are then the exact ones).
+        std::vector<size_t> near;
+        d.last_near.assign(res.size(), 0);
+        for (size_t i = 0; i < res.size(); i++)
+            if (res[i].key_near) near.push_back(i), d.last_near[i] = 1;
+        if (!near.empty()) {
+            const sdsp_stage_times first = d.last;
+            std::vector<uint64_t> o2, l2;
+            for (size_t i : near) o2.push_back(off[i]), l2.push_back(ln[i]);
+            std::vector<TrackRes> r2;
+            Pipeline px(d, *cfg, sr, stages, true);
+            px.run(d_samples, o2, l2, r2);
+            for (size_t j = 0; j < near.size(); j++) res[near[j]] = std::move(r2[j]);
+            // the call's stage times stay the main pass's; the rerun is reported beside them
+            const double rerun_ms = d.last.total_ms;
+            d.last = first;
+            d.last.key_reruns = near.size();
+            d.last.rerun_ms = rerun_ms;
+            d.last.total_ms += rerun_ms;
+        }
     } catch (...) {
         // a sub-batch may have queued key-stream work (the late join) before a later one threw:
         // nothing of this call may still run on the engine's streams once the context lock is
@@ -2507,10 +2562,13 @@ void stage_release(DeviceStage* ds) {
 }
 // test hook (sdsp_debug_set_test_hooks): the worker devices of sdsp_analyze_batch, repeats
 // allowed (two workers on device 0 exercise the multi-device chunk path on a one-GPU box)
+// (compiled only into the test build, -DSDSP_TEST_HOOKS: the shipping library cannot be re-routed)
 std::vector<int> device_list_override(int ndev) {
     std::vector<int> devs;
+#ifdef SDSP_TEST_HOOKS
     for (int v : test_hooks_devices())
         if (v >= 0 && v < ndev) devs.push_back(v);
+#endif
     return devs;
 }
 }  // namespace
@@ -2542,6 +2600,27 @@ int32_t sdsp_analyze_batch_device_ex(const float* d_samples, const uint64_t* off
     }
 }
 
+// Whether `cfg` at `sample_rate` takes the default key path's block-folded HPCP frame energies
+// (include/stratum_hip_debug.h): the parity tests then compare key_confidence / key_clarity with
+// the oracle within the north star's tolerance, and every other configuration bit for bit.
+int32_t sdsp_debug_key_energy_blocked(const sdsp_config* cfg, uint32_t sample_rate) {
+    if (!cfg || sample_rate == 0) return -1;
+    return key_energy_blocked(*cfg, sample_rate) ? 1 : 0;
+}
+
+// Per track of the last sdsp_analyze_batch_device / sdsp_analyze_audio call on `device`: 1 where
+// its key vote was near an energy-dependent decision and the track was analysed again exactly.
+int32_t sdsp_debug_last_key_near(int32_t device, uint8_t* out, uint64_t n) {
+    try {
+        DeviceCtx& d = device_ctx(device);
+        std::lock_guard<std::mutex> lk(d.mu);
+        for (uint64_t i = 0; i < n; i++) out[i] = i < d.last_near.size() ? d.last_near[(size_t)i] : 0;
+        return SDSP_OK;
+    } catch (const std::exception&) {
+        return SDSP_ERR_PROCESSING;
+    }
+}
+
 // Host buffers: chunks of whole tracks (up to SDSP_BATCH_CHUNK_TRACKS tracks, default
 // 512, and about 8 GB) pulled from a shared counter by one worker per device; per device a copier
 // thread stages the next chunk into the second of two HBM slots (its own stream, completion
@@ -2568,7 +2647,9 @@ int32_t sdsp_analyze_batch(const float* const* tracks, const uint64_t* lens, uin
     if (const uint64_t t = test_hooks().batch_chunk_tracks.load()) max_tracks = t;  // sdsp_debug_set_schedule
     const std::vector<uint64_t> cb = plan_chunks(lens, n_tracks, max_tracks, (uint64_t)2 << 30 /* 8 GB of f32 */);
     // test hook (sdsp_debug_set_test_hooks): the chunk whose analysis throws (the per-chunk failure path)
+#ifdef SDSP_TEST_HOOKS
     const long fail_chunk = test_hooks().fail_chunk.load();
+#endif
     const size_t n_chunks = cb.size() - 1;
     // every result starts as an error; run_device overwrites the tracks it analyses
     auto mark_failed = [&](size_t c, const std::string& what) {
@@ -2610,8 +2691,12 @@ int32_t sdsp_analyze_batch(const float* const* tracks, const uint64_t* lens, uin
             }
             SDSP_HIP_CHECK(hipEventRecord(sl.ready, ds->copy));
         };
+#ifdef SDSP_TEST_HOOKS
         cd.analyze = [ds, &cb, lens, sample_rate, cfg, outs, fail_chunk](int s, size_t c) {
             if ((long)c == fail_chunk) throw HipError("injected chunk failure (test hook)");
+#else
+        cd.analyze = [ds, &cb, lens, sample_rate, cfg, outs](int s, size_t c) {  // (no failure injection)
+#endif
             const uint64_t a = cb[c], b = cb[c + 1];
             std::vector<uint64_t> off(b - a), ln(b - a);
             uint64_t tot = 0;

@@ -270,6 +270,12 @@ int32_t sdsp_last_stage_times(int32_t device, sdsp_stage_times* out) {
 // environment; a test sets these explicitly and resets them with (-1, NULL, 0, 0).
 int32_t sdsp_debug_set_test_hooks(int64_t fail_chunk, const int32_t* devices, uint32_t n_devices,
                                   int32_t stft_frame_parallel) {
+#ifndef SDSP_TEST_HOOKS
+    // the shipping library: failure injection and the device override are compiled only into the
+    // test build (lib/libstratum_hip_testhooks.so, -DSDSP_TEST_HOOKS), so nothing can make this
+    // library fail a chunk or re-route work; the frame-parallel STFT switch (same results) stays
+    if (fail_chunk >= 0 || n_devices > 0) return SDSP_ERR_NOT_IMPLEMENTED;
+#endif
     TestHooks& h = test_hooks();
     h.fail_chunk.store((long)fail_chunk);
     h.stft_frame_parallel.store(stft_frame_parallel != 0);
@@ -301,6 +307,13 @@ int32_t sdsp_debug_mem_info(int32_t device, uint64_t* free_bytes, uint64_t* tota
     } catch (const std::exception&) {
         return SDSP_ERR_PROCESSING;
     }
+}
+
+// the PCI bus id of a HIP device ("0000:c1:00.0"): the benchmark reads that card's shader clock
+// from sysfs (HIP device numbers are not the driver's card numbers under HIP_VISIBLE_DEVICES)
+int32_t sdsp_debug_device_pci_bus_id(int32_t device, char* out, uint32_t len) {
+    if (!out || len < 13) return SDSP_ERR_INVALID_INPUT;
+    return hipDeviceGetPCIBusId(out, (int)len, device) == hipSuccess ? SDSP_OK : SDSP_ERR_PROCESSING;
 }
 
 // test probe: device allocations the engine has made so far (count, bytes)

@@ -86,6 +86,7 @@ struct DeviceCtx {
     std::map<int, std::unique_ptr<FftTables>> fft;  // keyed by real FFT size N
     std::map<std::string, std::unique_ptr<DevBuf>> bufs;
     sdsp_stage_times last{};
+    std::vector<uint8_t> last_near;  // per track of the last call: its key vote was near a decision (rerun)
     DevBuf& buf(const std::string& name) {
         auto& b = bufs[name];
         if (!b) {

@@ -18,7 +18,11 @@ from sdsp_abi import ERROR_NAMES, FLAG_NAMES, SdspConfidence, SdspConfig, SdspRe
 
 PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("SDSP_LIB_PATH") or os.path.join(PKG, "lib", "libstratum_hip.so")  # override: layout/ablation builds
+# the test build (-DSDSP_TEST_HOOKS): the same library with failure injection and the device
+# override compiled in; only test_hooks(fail_chunk=..., devices=...) switches to it
+TESTHOOKS_LIB_PATH = os.path.join(PKG, "lib", "libstratum_hip_testhooks.so")
 _lib = None
+_lib_th = None
 
 
 class AnalysisError(Exception):
@@ -37,9 +41,16 @@ def build():
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise RuntimeError(f"libstratum_hip.so not built ({LIB_PATH}); run __graft_entry__.build()")
-        L = C.CDLL(LIB_PATH)
+        _lib = _load(LIB_PATH)
+    return _lib
+
+
+def _load(path):
+    """ctypes handle of one build of the engine, with the ABI's argument types declared."""
+    if True:
+        if not os.path.exists(path):
+            raise RuntimeError(f"{os.path.basename(path)} not built ({path}); run __graft_entry__.build()")
+        L = C.CDLL(path)
         fp = C.POINTER(C.c_float)
         u64p = C.POINTER(C.c_uint64)
         L.sdsp_config_default.argtypes = [C.POINTER(SdspConfig)]
@@ -84,8 +95,11 @@ def lib():
         for f in ("sdsp_device_malloc", "sdsp_device_free", "sdsp_memcpy_h2d", "sdsp_memcpy_d2h",
                   "sdsp_device_synchronize", "sdsp_compute_confidence", "sdsp_key_name", "sdsp_decode_audio_file"):
             getattr(L, f).restype = C.c_int32
-        _lib = L
-    return _lib
+        L.sdsp_debug_key_energy_blocked.argtypes = [C.POINTER(SdspConfig), C.c_uint32]
+        L.sdsp_debug_key_energy_blocked.restype = C.c_int32
+        L.sdsp_debug_set_test_hooks.argtypes = [C.c_int64, C.POINTER(C.c_int32), C.c_uint32, C.c_int32]
+        L.sdsp_debug_set_test_hooks.restype = C.c_int32
+        return L
 
 
 def _fp(a):
@@ -108,17 +122,47 @@ def device_mem_info(device=0):
 def test_hooks(fail_chunk=-1, devices=(), stft_frame_parallel=False):
     """Sets the library's test hooks (include/stratum_hip_debug.h, sdsp_debug_set_test_hooks)
     for the duration of the block, then resets them.  The library reads none of them from the
-    environment."""
-    L = lib()
-    f = L.sdsp_debug_set_test_hooks
-    f.argtypes = [C.c_int64, C.POINTER(C.c_int32), C.c_uint32, C.c_int32]
-    f.restype = C.c_int32
+    environment.  Failure injection and the device override exist only in the test build
+    (libstratum_hip_testhooks.so): with either set, every call inside the block goes to it."""
+    global _lib, _lib_th, _schedule_set
+    test_build = fail_chunk >= 0 or len(devices) > 0
+    prev = lib()
+    if test_build:
+        if _lib_th is None:
+            _lib_th = _load(TESTHOOKS_LIB_PATH)
+        _lib, _schedule_set = _lib_th, None
+    f = _lib.sdsp_debug_set_test_hooks
     dev = (C.c_int32 * max(len(devices), 1))(*devices)
     assert f(fail_chunk, dev if devices else None, len(devices), int(bool(stft_frame_parallel))) == 0
     try:
         yield
     finally:
         f(-1, None, 0, 0)
+        if test_build:
+            _lib, _schedule_set = prev, None
+
+
+def last_key_near(n, device=0):
+    """sdsp_debug_last_key_near: per track of the last analysis call on `device`, whether its key
+    vote was near an energy-dependent decision (and the track was analysed again exactly)."""
+    out = np.zeros(max(int(n), 1), np.uint8)
+    f = lib().sdsp_debug_last_key_near
+    f.argtypes = [C.c_int32, C.c_void_p, C.c_uint64]
+    f.restype = C.c_int32
+    if f(device, out.ctypes.data, int(n)) != 0:
+        raise RuntimeError("sdsp_debug_last_key_near failed")
+    return out[: int(n)].astype(bool)
+
+
+def key_energy_blocked(config=None, sample_rate=44100):
+    """sdsp_debug_key_energy_blocked: True when `config` at `sample_rate` takes the default key
+    path's block-folded HPCP frame energies (key_confidence / key_clarity re-associated, DESIGN.md
+    §2); no device is touched."""
+    cfg = config if config is not None else default_config()
+    v = lib().sdsp_debug_key_energy_blocked(C.byref(cfg), sample_rate)
+    if v < 0:
+        raise ValueError("sdsp_debug_key_energy_blocked: bad arguments")
+    return bool(v)
 
 
 _SCHEDULE_ENV = ("SDSP_SERIAL_STREAMS", "SDSP_NO_KEY_DEFER", "SDSP_NO_ROW_REUSE", "SDSP_HOST_TRACE",

@@ -199,6 +199,10 @@ class SdspStageTimes(C.Structure):
         ("stft8192_launches", u64),
         ("stft2048_bytes", C.c_double),
         ("stft8192_bytes", C.c_double),
+        ("stft2048_frames", u64),
+        ("stft8192_frames", u64),
+        ("key_reruns", u64),
+        ("rerun_ms", C.c_double),
     ]
 
 

@@ -54,18 +54,32 @@ def diff_results(got, ref, tol=TOL):
 
 # The default key path folds each frame's HPCP energy in 64-bin blocks (k_mask_rp / k_hpcp_band,
 # DESIGN.md §2): a GPU-only re-association of one f32 sum (extractor.rs:1133) that the north star's
-# tolerance allows (key exact, confidences within 1e-4).  Against the oracle, key_confidence and
-# key_clarity are then compared within TOL (diff_results) instead of bit for bit; every other field
-# stays bit-identical.  GPU-against-GPU comparisons pass strict=True.
+# tolerance allows (key exact, confidences within 1e-4).  Only configurations that take that path
+# (the library answers: sdsp_debug_key_energy_blocked) have key_confidence and key_clarity compared
+# with the oracle within TOL; every other field, and both fields under every other configuration,
+# stay bit for bit.  strict=True forces bit-for-bit (GPU against GPU).
 KEY_ENERGY_FIELDS = ("key_confidence", "key_clarity")
-KEY_ENERGY_REASSOCIATED = True
 
 
-def exact_fraction(got, ref, strict=False):
+def relaxed_fields(strict=None, cfg=None, sample_rate=44100):
+    """The fields compared within TOL instead of bit for bit: KEY_ENERGY_FIELDS when `cfg` (None =
+    AnalysisConfig::default()) at `sample_rate` takes the block-folded energies, else none."""
+    if strict:
+        return ()
+    import sdsp
+
+    return KEY_ENERGY_FIELDS if sdsp.key_energy_blocked(cfg, int(sample_rate)) else ()
+
+
+def _sr(r):
+    return (r.get("metadata") or {}).get("sample_rate", 44100) if isinstance(r, dict) else 44100
+
+
+def exact_fraction(got, ref, strict=None, cfg=None):
     """1.0 when every float field is bit-identical (the design target), else the share that is.
-    strict=False leaves out KEY_ENERGY_FIELDS when KEY_ENERGY_REASSOCIATED (diff_results checks
-    them within TOL)."""
-    skip = () if strict or not KEY_ENERGY_REASSOCIATED else KEY_ENERGY_FIELDS
+    The block-folded key energies (relaxed_fields) are left out here; diff_results checks them
+    within TOL."""
+    skip = relaxed_fields(strict, cfg, _sr(got))
     pairs = [(got[k], ref[k]) for k in ("bpm", "bpm_confidence", "key_confidence", "key_clarity", "grid_stability")
              if k not in skip]
     same = sum(1 for a, b in pairs if np.float32(a).tobytes() == np.float32(b).tobytes())
@@ -101,20 +115,20 @@ def result_digest(r):
     }
 
 
-def digests_match(got, ref, strict=False):
-    """result_digest equality; with the re-associated key energies (strict=False) the
+def digests_match(got, ref, strict=None, cfg=None, sample_rate=44100):
+    """result_digest equality; where `cfg` takes the block-folded key energies (relaxed_fields) the
     KEY_ENERGY_FIELDS compare within TOL, as f32 values from their bits."""
-    skip = () if strict or not KEY_ENERGY_REASSOCIATED else KEY_ENERGY_FIELDS
+    skip = relaxed_fields(strict, cfg, sample_rate)
     if any(got[k] != ref[k] for k in got if k not in skip):
         return False
     f = lambda b: float(np.uint32(b).view(np.float32))
     return all(abs(f(got[k]) - f(ref[k])) <= TOL for k in skip)
 
 
-def dicts_match(got, ref, strict=False):
-    """Equality of two result dicts as JSON-plain data (the committed golden vectors); with the
-    re-associated key energies (strict=False) the KEY_ENERGY_FIELDS compare within TOL."""
-    skip = () if strict or not KEY_ENERGY_REASSOCIATED else KEY_ENERGY_FIELDS
+def dicts_match(got, ref, strict=None, cfg=None):
+    """Equality of two result dicts as JSON-plain data (the committed golden vectors); where `cfg`
+    takes the block-folded key energies (relaxed_fields) the KEY_ENERGY_FIELDS compare within TOL."""
+    skip = relaxed_fields(strict, cfg, _sr(got))
     if {k: v for k, v in got.items() if k not in skip} != {k: v for k, v in ref.items() if k not in skip}:
         return False
     return all(abs(float(got[k]) - float(ref[k])) <= TOL for k in skip)

@@ -62,6 +62,36 @@ def test_no_test_switch_read_from_environment():
         assert name not in data, name
 
 
+def test_shipping_library_refuses_failure_injection():
+    """Failure injection and the device override are compiled only into the test build
+    (libstratum_hip_testhooks.so, -DSDSP_TEST_HOOKS): the shipping library refuses both (Not
+    implemented) and keeps the frame-parallel STFT switch, which changes no result; the test build
+    accepts all three.  No device is touched."""
+    f = sdsp.lib().sdsp_debug_set_test_hooks
+    dev = (C.c_int32 * 2)(0, 0)
+    assert f(0, None, 0, 0) == 4
+    assert f(-1, dev, 2, 0) == 4
+    assert f(-1, None, 0, 1) == 0 and f(-1, None, 0, 0) == 0
+    th = sdsp._load(sdsp.TESTHOOKS_LIB_PATH)
+    assert th.sdsp_debug_set_test_hooks(0, dev, 2, 1) == 0
+    assert th.sdsp_debug_set_test_hooks(-1, None, 0, 0) == 0
+    data = open(sdsp.lib()._name, "rb").read()
+    assert b"injected chunk failure" not in data and b"injected chunk failure" in open(th._name, "rb").read()
+
+
+def test_key_energy_blocked_query():
+    """sdsp_debug_key_energy_blocked names the configurations whose key_confidence / key_clarity
+    are block-folded: the default path yes; tuning, log-frequency chroma, whitening,
+    bass blend, key HPSS, another mask margin or power, no mask: no."""
+    assert sdsp.key_energy_blocked() and sdsp.key_energy_blocked(sample_rate=22050)
+    for k, v in (("enable_key_tuning_compensation", 1), ("enable_key_log_frequency", 1),
+                 ("enable_key_hpss_harmonic", 1), ("enable_key_harmonic_mask", 0), ("key_spectrogram_smooth_margin", 8),
+                 ("key_harmonic_mask_power", 1.0), ("enable_key_hpcp_bass_blend", 1), ("enable_key_hpcp", 0)):
+        c = sdsp.default_config()
+        setattr(c, k, v)
+        assert not sdsp.key_energy_blocked(c), k
+
+
 def test_library_reads_no_environment():
     """The schedule switches reach the library only through sdsp_debug_set_schedule (the Python
     layer maps the SDSP_* variables onto it): no source of the shipping library calls getenv."""

@@ -152,7 +152,7 @@ def test_unnormalised_int_scale_input():
         assert st == 0
         assert np.isfinite(got["bpm"]) and np.isfinite(got["key_confidence"])
         assert not parity.diff_results(got, ref), parity.diff_results(got, ref)
-        assert parity.exact_fraction(got, ref) == 1.0
+        assert parity.exact_fraction(got, ref, cfg=cfg) == 1.0
 
 
 def test_unnormalised_overflowing_magnitudes():

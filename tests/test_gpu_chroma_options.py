@@ -94,7 +94,7 @@ def _run(case, xs, sr=SR):
         assert not isinstance(got[i], Exception), (case, i, got[i])
         bad = parity.diff_results(got[i], ref)
         assert not bad, f"{case} track {i}: {bad}"
-        assert parity.exact_fraction(got[i], ref) == 1.0, (case, i)
+        assert parity.exact_fraction(got[i], ref, cfg=cfg) == 1.0, (case, i)
         refs.append(ref)
     return got, refs
 

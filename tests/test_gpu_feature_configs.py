@@ -59,4 +59,4 @@ def test_feature_config_parity(case):
         st, ref = oracle.analyze(x, 44100, ocfg)
         assert st == 0
         assert not parity.diff_results(g, ref), case
-        assert parity.exact_fraction(g, ref) == 1.0, case
+        assert parity.exact_fraction(g, ref, cfg=cfg) == 1.0, case

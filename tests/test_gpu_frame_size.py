@@ -65,7 +65,7 @@ def test_frame_size_parity(case):
         assert not isinstance(got[i], Exception), (case, i, got[i])
         bad = parity.diff_results(got[i], ref)
         assert not bad, f"{case} track {i}: {bad}"
-        assert parity.exact_fraction(got[i], ref) == 1.0, (case, i)
+        assert parity.exact_fraction(got[i], ref, cfg=cfg) == 1.0, (case, i)
 
 
 def test_key_stft_size_changes_results():

@@ -99,7 +99,7 @@ def test_hpss_parity(case):
         assert not isinstance(got[i], Exception), (case, i, got[i])
         bad = parity.diff_results(got[i], ref)
         assert not bad, f"{case} track {i}: {bad}"
-        assert parity.exact_fraction(got[i], ref) == 1.0, (case, i)
+        assert parity.exact_fraction(got[i], ref, cfg=cfg) == 1.0, (case, i)
         m, rm = got[i]["metadata"], ref["metadata"]
         for k in ("tempogram_multi_res_triggered", "tempogram_multi_res_used", "tempogram_percussive_triggered",
                   "tempogram_percussive_used"):

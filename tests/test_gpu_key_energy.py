@@ -54,3 +54,4 @@ def test_exact_energy_configs_stay_bitexact():
     for i, x in enumerate(xs):
         st, ref = oracle.analyze(x, 44100, config=cfg)
         assert st == 0 and parity.exact_fraction(got[i], ref, strict=True) == 1.0, i
+

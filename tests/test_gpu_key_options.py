@@ -92,7 +92,7 @@ def test_key_option_parity(case):
         assert not isinstance(got[i], Exception), (case, i, got[i])
         bad = parity.diff_results(got[i], ref)
         assert not bad, f"{case} track {i}: {bad}"
-        assert parity.exact_fraction(got[i], ref) == 1.0, (case, i)
+        assert parity.exact_fraction(got[i], ref, cfg=cfg) == 1.0, (case, i)
     # single-track API through the same path
     g1 = sdsp.analyze_audio(xs[0], 44100, cfg)
     assert not parity.diff_results(g1, oracle.analyze(xs[0], 44100, ocfg)[1])

@@ -81,7 +81,7 @@ def test_legacy_parity(case):
         assert not isinstance(got[i], Exception), (case, i, got[i])
         bad = parity.diff_results(got[i], ref)
         assert not bad, f"{case} track {i}: {bad}"
-        assert parity.exact_fraction(got[i], ref) == 1.0, (case, i)
+        assert parity.exact_fraction(got[i], ref, cfg=cfg) == 1.0, (case, i)
         assert got[i]["bpm"] == ref["bpm"] and got[i]["bpm_confidence"] == ref["bpm_confidence"], (case, i)
 
 

@@ -141,7 +141,7 @@ def test_key_peak_list_capacities(peaks):
     got = sdsp.analyze_batch_device(buf.ptr, offs, lens, config=cfg)
     for i in range(len(lens)):
         st, ref = oracle.analyze(buf.to_host(int(offs[i]), int(lens[i])), 44100, config=cfg)
-        assert st == 0 and parity.exact_fraction(got[i], ref) == 1.0, i
+        assert st == 0 and parity.exact_fraction(got[i], ref, cfg=cfg) == 1.0, i
 
 
 @pytest.mark.parametrize("late_join", [True, False])

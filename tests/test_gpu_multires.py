@@ -61,7 +61,7 @@ def test_multires_config_parity(case):
         assert not isinstance(got[i], Exception), (case, i, got[i])
         bad = parity.diff_results(got[i], ref)
         assert not bad, f"{case} track {i}: {bad}"
-        assert parity.exact_fraction(got[i], ref) == 1.0, (case, i)
+        assert parity.exact_fraction(got[i], ref, cfg=cfg) == 1.0, (case, i)
         trig += ref["metadata"].get("tempogram_multi_res_triggered") is True
     assert trig >= 2, (case, trig)  # the escalation path is exercised
 

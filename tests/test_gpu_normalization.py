@@ -54,7 +54,7 @@ def test_batch_parity(method):
         assert not isinstance(got[i], Exception), (method, i, got[i])
         bad = parity.diff_results(got[i], ref)
         assert not bad, f"{method} track {i}: {bad}"
-        assert parity.exact_fraction(got[i], ref) == 1.0, (method, i)
+        assert parity.exact_fraction(got[i], ref, cfg=cfg) == 1.0, (method, i)
 
 
 @pytest.mark.parametrize("method", sorted(METHODS))
