@@ -370,7 +370,7 @@ def main():
                "not a scaling measurement]" if args.rank_shard >= 0 else ""),
             "config": {
                 "workload": wl,
-                "baseline_config": cfg_no if world == 1 or cfg_no != 2 else 3,
+                "baseline_config": 3 if (cfg_no == 2 and (world > 1 or args.rank_shard >= 0)) else cfg_no,
                 "tracks_per_gpu": n,
                 "seconds_per_track": args.seconds if args.workload != "mixed" else "30-600",
                 "sample_rate": sr,

@@ -161,6 +161,49 @@ __device__ __forceinline__ void radix16(c2 v[16], const c2 w[15]) {
                      v[ja + 4], v[ja + 8], v[ja + 12]);
 }
 
+// radix16 with scheduling fences between its eight butterflies: the same operations in the same
+// order per element, evaluated butterfly by butterfly (at most 16 + 8 live complex values), for a
+// caller whose register budget is at its limit (k_stft_slide8w3's pass 1 beside the register ring)
+template <bool LAST>
+__device__ __forceinline__ void radix16_fenced(c2 v[16], const c2 w[15]) {
+    c2 u[16];
+#pragma unroll
+    for (int jp = 0; jp < 4; jp++) {
+        if (LAST && jp == 0)
+            bfly4<false>(v[0], v[4], v[8], v[12], w[0], w[0], w[0], u[0], u[1], u[2], u[3]);
+        else
+            bfly4<true>(v[jp], v[jp + 4], v[jp + 8], v[jp + 12], w[3 * jp + 0], w[3 * jp + 1], w[3 * jp + 2],
+                        u[jp * 4 + 0], u[jp * 4 + 1], u[jp * 4 + 2], u[jp * 4 + 3]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int ja = 0; ja < 4; ja++) {
+        bfly4<!LAST>(u[0 * 4 + ja], u[1 * 4 + ja], u[2 * 4 + ja], u[3 * 4 + ja], w[12], w[13], w[14], v[ja + 0],
+                     v[ja + 4], v[ja + 8], v[ja + 12]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// radix16 whose 15 twiddles come from a loader (tw(j) = w[j] of radix16) fetched per butterfly:
+// stage A's butterfly j' takes tw(3 j' .. 3 j' + 2) just before it runs and stage B's three are
+// fetched after stage A, so at most 3 twiddles are live instead of 15 (k_stft_slide8w3's pass 2,
+// whose LDS twiddles otherwise need 30 VGPRs beside the register ring at the 168-VGPR limit)
+template <typename TW>
+__device__ __forceinline__ void radix16_tw(c2 v[16], TW tw) {
+    c2 u[16];
+#pragma unroll
+    for (int jp = 0; jp < 4; jp++) {
+        const c2 w1 = tw(3 * jp + 0), w2 = tw(3 * jp + 1), w3 = tw(3 * jp + 2);
+        bfly4<true>(v[jp], v[jp + 4], v[jp + 8], v[jp + 12], w1, w2, w3, u[jp * 4 + 0], u[jp * 4 + 1],
+                    u[jp * 4 + 2], u[jp * 4 + 3]);
+    }
+    const c2 b1 = tw(12), b2 = tw(13), b3 = tw(14);
+#pragma unroll
+    for (int ja = 0; ja < 4; ja++)
+        bfly4<true>(u[0 * 4 + ja], u[1 * 4 + ja], u[2 * 4 + ja], u[3 * 4 + ja], b1, b2, b3, v[ja + 0], v[ja + 4],
+                    v[ja + 8], v[ja + 12]);
+}
+
 template <int M>
 struct StftShape {
     static constexpr int TPF = M / 16;                                   // threads per frame
@@ -855,12 +898,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
         // pass 2 (n = M/16 = 64, s = 16), in place
 #pragma unroll
         for (int k = 0; k < 16; k++) v[k] = buf[rb2 + 68 * k];
-        {
-            c2 tw2[15];
-#pragma unroll
-            for (int j = 0; j < 15; j++) tw2[j] = tw2s[pp2 * 16 + j];
-            radix16<false>(v, tw2);
-        }
+        radix16_tw(v, [&](int j) { return tw2s[pp2 * 16 + j]; });
 #pragma unroll
         for (int k = 0; k < 16; k++) buf[rb2 + 68 * k] = v[k];
         frame_sync<TPF>();
@@ -1220,12 +1258,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
         // pass 2 (n = M/16, s = 16), in place
 #pragma unroll
         for (int k = 0; k < 16; k++) v[k] = buf[rb2 + P272 * k];
-        {
-            c2 tw2[15];
-#pragma unroll
-            for (int j = 0; j < 15; j++) tw2[j] = tw2s[pp2 * 16 + j];
-            radix16<false>(v, tw2);
-        }
+        radix16_tw(v, [&](int j) { return tw2s[pp2 * 16 + j]; });
 #pragma unroll
         for (int k = 0; k < 16; k++) buf[rb2 + P272 * k] = v[k];
         __syncthreads();

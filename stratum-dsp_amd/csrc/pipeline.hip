@@ -827,13 +827,15 @@ void print_debug(const sdsp_config& c, const TrackDbg& d) {
 // ---------------------------------------------------------------------------------------
 class Pipeline {
    public:
-    Pipeline(DeviceCtx& d, const sdsp_config& cfg, uint32_t sr, int stages = SDSP_STAGES_FULL, bool exact_energy = false)
+    Pipeline(DeviceCtx& d, const sdsp_config& cfg, uint32_t sr, int stages = SDSP_STAGES_FULL, bool exact_energy = false,
+             bool key_only = false)
         : c_(d),
           d_(d),
           cfg_(cfg),
           sr_(sr),
           bpm_only_(stages == SDSP_STAGES_BPM_ONLY),
           exact_energy_(exact_energy),
+          key_only_(key_only),
           fs_((int)std::min<uint64_t>(cfg.frame_size, STFT_GEN_MAX)),
           nb_(fs_ / 2 + 1),
           s2_(base_stride(fs_)),
@@ -855,6 +857,8 @@ class Pipeline {
     // the key path with the reference's sequential frame-energy fold (k_mask_r / k_hpcp) even where
     // the band-limited mask applies: run_locked's rerun of tracks whose key vote was near a decision
     bool exact_energy_ = false;
+    // the key path alone (with exact_energy_: the rerun): front end, key stream, key fields only
+    bool key_only_ = false;
     // the tempo path's STFT: frame size (AnalysisConfig::frame_size), bins, row stride
     const int fs_, nb_, s2_;
     // the key path's STFT: frame size, hop, row stride (key_fft / key_hop)
@@ -1797,6 +1801,22 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         times_.stft8192_frames += total8;
         times_.stft8192_bytes += key_in_bytes + 4.0 * (double)total8 * (double)B8;
     }
+    if (key_only_) {  // run_locked's exact key rerun: the key fields only (the tempo path is not run)
+        if (NK > 0) {
+            SDSP_HIP_CHECK(hipStreamWaitEvent(st, kt.ev[2], 0));
+            const std::vector<KeyOut> ko = c_.down(d_kout, (size_t)NK);
+            for (int k = 0; k < NK; k++) {
+                TrackRes& r = res[(size_t)idx[(size_t)R[(size_t)K[(size_t)k]]]];
+                if (!ko[(size_t)k].ok) continue;
+                r.key_mode = ko[(size_t)k].mode;
+                r.key_tonic = ko[(size_t)k].tonic;
+                r.key_conf = ko[(size_t)k].conf;
+                r.key_clarity = ko[(size_t)k].clarity;
+            }
+        }
+        htr("E key only");
+        return;
+    }
     TempoPassOut bo;
     tempo_pass("B.", bin, bo);
     times_.stft2048_ms += bo.stft_ms;
@@ -2473,9 +2493,9 @@ int32_t run_locked(DeviceCtx& d, const float* d_samples, const uint64_t* offsets
     try {
         p.run(d_samples, off, ln, res);
         // Certified block energies: a track whose key vote had an energy-dependent
-        // decision within its margin (KeyOut::near) is analysed again with the reference's sequential
-        // frame-energy fold, and that result replaces its own (the tempo fields are the same bits;
-        // the key fields are then the exact ones).
+        // decision within its margin (KeyOut::near) has its key path run again with the reference's
+        // sequential frame-energy fold, and those key fields replace its own (everything else is
+        // independent of the key energies).
         std::vector<size_t> near;
         d.last_near.assign(res.size(), 0);
         for (size_t i = 0; i < res.size(); i++)
@@ -2485,9 +2505,16 @@ int32_t run_locked(DeviceCtx& d, const float* d_samples, const uint64_t* offsets
             std::vector<uint64_t> o2, l2;
             for (size_t i : near) o2.push_back(off[i]), l2.push_back(ln[i]);
             std::vector<TrackRes> r2;
-            Pipeline px(d, *cfg, sr, stages, true);
+            Pipeline px(d, *cfg, sr, stages, true, true);
             px.run(d_samples, o2, l2, r2);
-            for (size_t j = 0; j < near.size(); j++) res[near[j]] = std::move(r2[j]);
+            for (size_t j = 0; j < near.size(); j++) {
+                TrackRes& r = res[near[j]];
+                if (r2[j].status != SDSP_OK) continue;  // (the same front end as the main pass)
+                r.key_mode = r2[j].key_mode;
+                r.key_tonic = r2[j].key_tonic;
+                r.key_conf = r2[j].key_conf;
+                r.key_clarity = r2[j].key_clarity;
+            }
             // the call's stage times stay the main pass's; the rerun is reported beside them
             const double rerun_ms = d.last.total_ms;
             d.last = first;

@@ -55,3 +55,22 @@ def test_exact_energy_configs_stay_bitexact():
         st, ref = oracle.analyze(x, 44100, config=cfg)
         assert st == 0 and parity.exact_fraction(got[i], ref, strict=True) == 1.0, i
 
+
+
+def test_near_decision_track_rerun_exact():
+    """Track 538 of BASELINE config 5's mix (bench.py's generator, bpm_mode 1; the mix picks the
+    BPM range by the track's index in the call, so it is generated as the second of two tracks from
+    seed 537).  Under the block-folded energies one segment's within-mode argmax flips (a top-two
+    gap of 6.6e-7, tools/key_near_study.py) and key_confidence came out 0.0058 against the
+    oracle's 0.0086 (profiles/r05_key_scale_block_energies.jsonl).  k_key_vote flags it
+    (KeyOut::near) and the library analyses it again with the sequential fold: every field
+    bit-exact, the rerun reported in the stage times and by sdsp_debug_last_key_near."""
+    n = 180 * 44100
+    buf = sdsp.DeviceBuffer(2 * n)
+    sdsp.generate_synthetic(buf.ptr, 2, n, 44100, seed0=537, bpm_mode=1)
+    got = sdsp.analyze_batch_device(buf.ptr, [n], [n], 44100)
+    st = sdsp.stage_times()
+    assert st["key_reruns"] == 1 and bool(sdsp.last_key_near(1)[0])
+    rc, ref = oracle.analyze(buf.to_host(n, n), 44100)
+    assert rc == 0
+    assert parity.exact_fraction(got[0], ref, strict=True) == 1.0 and not parity.diff_results(got[0], ref)

@@ -155,3 +155,15 @@ def test_bench_share_device_rehearsal_is_labelled():
     d = _bench_json([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0",
                      "--tracks", "2", "--seconds", "1", "--dry-run", "--share-device"])
     assert d["n_gpus"] == 2 and "REHEARSAL: 2 ranks sharing device 0" in d["data"]
+
+
+def test_bench_rank_shard_is_labelled_config3():
+    """--rank-shard R (config 3 on a one-GPU box): one process runs rank R's seed range of the
+    8-rank job on device 0; the line says baseline config 3, names the shard and is labelled as
+    not a scaling measurement."""
+    d = _bench_json([sys.executable, os.path.join(ROOT, "bench.py"), "--rank-shard", "5", "--steps", "1", "--warmup",
+                     "0", "--tracks", "4", "--seconds", "1", "--dry-run"])
+    c = d["config"]
+    assert d["n_gpus"] == 1 and c["baseline_config"] == 3
+    assert c["shards"] == [{"rank": 5, "tracks": 4, "seed0": 20}]
+    assert "CONFIG-3 SHARD: rank 5" in d["data"]
