@@ -51,9 +51,11 @@ int32_t sdsp_debug_set_schedule(int32_t serial_streams, int32_t no_key_defer, in
 int32_t sdsp_debug_key_energy_blocked(const sdsp_config* cfg, uint32_t sample_rate);
 
 /*
- * Per track of the last analysis call on `device` (n entries): 1 where the block-folded key
- * energies left a key decision within its margin, so the track was analysed again with the
- * sequential energy fold (sdsp_stage_times.key_reruns counts them), else 0.
+ * Per track of the last analysis call on `device` (n entries): non-zero where the block-folded
+ * key energies left a key decision within its margin, so the track's key path ran again with the
+ * sequential energy fold (sdsp_stage_times.key_reruns counts them), else 0.  Bits: 1 a segment's
+ * (or the slice's) within-mode argmax, 2 a segment clarity gate, 4 the final key gap, 8 the
+ * weight-sum fallback.
  */
 int32_t sdsp_debug_last_key_near(int32_t device, uint8_t* out, uint64_t n);
 

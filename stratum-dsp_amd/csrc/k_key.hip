@@ -893,7 +893,7 @@ __global__ __launch_bounds__(KV_THREADS) void k_key_vote(const int* __restrict__
         if (threadIdx.x == 0) {
             use_w_s = !(sw <= 1e-12f || used < 10);
             // the unweighted fallback (src/lib.rs:1278-1285) is decided by a sum of energy-derived weights
-            if (P.near_check && sd_absf(sw - 1e-12f) <= KV_NEAR_REL * 1e-12f) near_s = 1;
+            if (P.near_check && sd_absf(sw - 1e-12f) <= KV_NEAR_REL * 1e-12f) atomicOr(&near_s, KV_NEAR_WSUM);
         }
     } else if (threadIdx.x == 0) {
         use_w_s = 0;
@@ -982,7 +982,7 @@ __global__ __launch_bounds__(KV_THREADS) void k_key_vote(const int* __restrict__
         r.weights_used = use_w;
         // the key is the argmax of the accumulated scores: a relative gap in (0, margin] could flip
         // it (an exact tie of winners is structural and stays exact, key_raw_near)
-        r.near = P.near_check && (near_s || (conf > 0.0f && !(conf > KV_NEAR_CONF)));
+        r.near = P.near_check ? (near_s | ((conf > 0.0f && !(conf > KV_NEAR_CONF)) ? KV_NEAR_FINAL : 0)) : 0;
         out[trk] = r;
     };
     // full-slice detection: detect_key_weighted (+ the mode heuristic)
@@ -995,7 +995,7 @@ __global__ __launch_bounds__(KV_THREADS) void k_key_vote(const int* __restrict__
             float raw[24], sorted[24];
             int order[24];
             for (int k = 0; k < 24; k++) raw[k] = acc[k];
-            if (P.near_check && key_raw_near(raw)) near_s = 1;
+            if (P.near_check && key_raw_near(raw)) atomicOr(&near_s, KV_NEAR_ARGMAX);
             key_from_raw(raw, sorted, order);
             int key = order[0];
             float conf = sorted[0] > 0.0f ? sd_clampf((sorted[0] - sorted[1]) / sorted[0], 0.0f, 1.0f) : 0.0f;
@@ -1086,7 +1086,7 @@ __global__ __launch_bounds__(KV_THREADS) void k_key_vote(const int* __restrict__
         float raw[24], sorted[24];
         int order[24];
         for (int k = 0; k < 24; k++) raw[k] = row[k];
-        if (P.near_check && key_raw_near(raw)) near_s = 1;
+        if (P.near_check && key_raw_near(raw)) atomicOr(&near_s, KV_NEAR_ARGMAX);
         key_from_raw(raw, sorted, order);
         if (P.mh_on) {
             int key;
@@ -1105,7 +1105,7 @@ __global__ __launch_bounds__(KV_THREADS) void k_key_vote(const int* __restrict__
         row[48] = cl;
         const float gate = mode == 1 ? P.ms_min_cl : P.min_clarity;
         row[49] = cl >= gate ? 1.0f : 0.0f;
-        if (P.near_check && sd_absf(cl - gate) <= KV_NEAR_CLARITY) near_s = 1;  // the segment gate (src/lib.rs:1380)
+        if (P.near_check && sd_absf(cl - gate) <= KV_NEAR_CLARITY) atomicOr(&near_s, KV_NEAR_GATE);  // the segment gate (src/lib.rs:1380)
         row[50] = cl * sw;
     }
     __syncthreads();

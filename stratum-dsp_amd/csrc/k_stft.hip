@@ -1203,11 +1203,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
         const int pp = lt / 15, j = lt % 15;
         tw2s[pp * 16 + j] = ld_c2(rtw, 8 * (15 * TPF + j * (TPF / 16) + pp), 0);
     }
-    // per-strip register constants: window, pass-1 twiddles, the sample ring; pass 3 wave-uniform
-    c2 win[16], tw1[15], tw3[15], ring[16];
+    // per-strip register constants: window, pass-1 twiddles, the sample ring; pass 3 wave-uniform.
+    // At hop 512 (S = 1) the frame loop is unrolled by U = 2 frames, so the ring holds 16 + S
+    // entries and shifts by 2 S once per two frames (16 - S moves of a complex value per two frames
+    // instead of per frame); at S = 2 the two-frame ring would spill, so U = 1.
+    // ring[k] = x[TPF ((f + 1) S + k) + lt] * gain at the top of an iteration starting at frame f.
+    constexpr int U = S == 1 ? 2 : 1, RN = 16 + (U - 1) * S;
+    c2 win[16], tw1[15], tw3[15], ring[RN];
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const c2 x = ld_c2(rx, vo, 8 * TPF * k);
+    for (int k = 0; k < RN; k++) {
+        const c2 x = ld_c2(rx, vo, 8 * TPF * (S + k));
         ring[k] = {x.x * gn, x.y * gn};
     }
 #pragma unroll
@@ -1229,28 +1234,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     // pass reads (c % 16) + 272 (c / 16) + 17 m for its column c
     const int rb2 = q2 + 17 * pp2, rb3 = (colA & 15) + P272 * (colA >> 4);
     const int vown = 4 * colA, vpart = 4 * (M - colA - 256 * 7), vmid = 4 * (M / 2);
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the per-strip loads have landed
 
-    // prologue: pass 1 of frame 0 in registers, the ring advanced to frame 1
+    // prologue: pass 1 of frame 0 in registers (its samples x[TPF k + lt], k < 16)
     c2 v[16];
 #pragma unroll
-    for (int k = 0; k < 16; k++) v[k] = {ring[k].x * win[k].x, ring[k].y * win[k].y};
-    radix16<false>(v, tw1);
-    {
-        c2 nx[S];
-#pragma unroll
-        for (int s2 = 0; s2 < S; s2++) nx[s2] = ld_c2(rx, vo, 8 * ((hop / 2) + TPF * (16 - S + s2)));
-#pragma unroll
-        for (int k = 0; k < 16 - S; k++) ring[k] = ring[k + S];
-#pragma unroll
-        for (int s2 = 0; s2 < S; s2++) ring[16 - S + s2] = {nx[s2].x * gn, nx[s2].y * gn};
+    for (int k = 0; k < 16; k++) {
+        const c2 x = ld_c2(rx, vo, 8 * TPF * k);
+        v[k] = {(x.x * gn) * win[k].x, (x.y * gn) * win[k].y};
     }
+    radix16<false>(v, tw1);
 
     uint64_t miss = 0;  // wave-uniform: bit i = frame f0 + i met the sqrt's inexact range
-    for (int i = 0;; i++) {
-        c2 nx[S];  // the ring's new values for frame i + 2 (zeros past the strip: outside rx)
-#pragma unroll
-        for (int s2 = 0; s2 < S; s2++) nx[s2] = ld_c2(rx, vo, 8 * ((i + 2) * (hop / 2) + TPF * (16 - S + s2)));
+    // frame i from v (its pass-1 output): LDS passes 2 and 3, the exchange, the post-processing
+    auto frame = [&](int i) {
         if (i > 0) __syncthreads();  // every last-pass read of frame i - 1 is done
 #pragma unroll
         for (int k = 0; k < 16; k++) buf[P17 * lt + k] = v[k];
@@ -1275,41 +1271,54 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
             P[k] = v[k];
         }
         const c2 Pm = v[8];
-        {
-            // post-processing of frame i (sdsp_fft_spec.h STFT section; see k_stft_slide)
-            const __amdgpu_buffer_rsrc_t ro = rsrc_of(row0 + (int64_t)i * stride, 4u * (M + 1));
-            uint32_t lo = 0xFFFFFFFFu, hi = 0u;
-            auto sq = [&](float yx, float yy) { return 0x1p-33f * sqrt_fast(__builtin_fmaf(yx, yx, yy * yy), lo, hi); };
-            auto st = [&](float mag, int voff, int soff) {
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mag), ro, voff, soff, 0);
-            };
+        // post-processing of frame i (sdsp_fft_spec.h STFT section; see k_stft_slide)
+        const __amdgpu_buffer_rsrc_t ro = rsrc_of(row0 + (int64_t)i * stride, 4u * (M + 1));
+        uint32_t lo = 0xFFFFFFFFu, hi = 0u;
+        auto sq = [&](float yx, float yy) { return 0x1p-33f * sqrt_fast(__builtin_fmaf(yx, yx, yy * yy), lo, hi); };
+        auto st = [&](float mag, int voff, int soff) {
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mag), ro, voff, soff, 0);
+        };
 #pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const c2 Zk = P[j], Zr = P[15 - j], w = wks[j * TPF + lt];
-                const float sx = Zk.x + Zr.x, sy = Zk.y - Zr.y, dx = Zk.y + Zr.y, dy = -(Zk.x - Zr.x);
-                st(sq(__builtin_fmaf(w.x, dx, __builtin_fmaf(-w.y, dy, sx)), __builtin_fmaf(w.x, dy, __builtin_fmaf(w.y, dx, sy))),
-                   vown, 1024 * j);
-                st(sq(__builtin_fmaf(-w.x, dx, __builtin_fmaf(w.y, dy, sx)), __builtin_fmaf(w.x, dy, __builtin_fmaf(w.y, dx, -sy))),
-                   vpart, 1024 * (7 - j));
-            }
-            if (self0) {  // bin M/2, self-paired
-                const c2 Z = Pm, w = rtH;
-                const float sx = Z.x + Z.x, sy = Z.y - Z.y, dx = Z.y + Z.y, dy = -(Z.x - Z.x);
-                st(sq(__builtin_fmaf(w.x, dx, __builtin_fmaf(-w.y, dy, sx)), __builtin_fmaf(w.x, dy, __builtin_fmaf(w.y, dx, sy))),
-                   vmid, 0);
-            }
-            const bool missed = __builtin_amdgcn_ballot_w64(sqrt_fast_missed(lo, hi)) != 0;
-            miss |= (uint64_t)missed << (i & 63);
+        for (int j = 0; j < 8; j++) {
+            const c2 Zk = P[j], Zr = P[15 - j], w = wks[j * TPF + lt];
+            const float sx = Zk.x + Zr.x, sy = Zk.y - Zr.y, dx = Zk.y + Zr.y, dy = -(Zk.x - Zr.x);
+            st(sq(__builtin_fmaf(w.x, dx, __builtin_fmaf(-w.y, dy, sx)), __builtin_fmaf(w.x, dy, __builtin_fmaf(w.y, dx, sy))),
+               vown, 1024 * j);
+            st(sq(__builtin_fmaf(-w.x, dx, __builtin_fmaf(w.y, dy, sx)), __builtin_fmaf(w.x, dy, __builtin_fmaf(w.y, dx, -sy))),
+               vpart, 1024 * (7 - j));
         }
-        if (i + 1 == nf) break;
-        // pass 1 of frame i + 1 from the ring (stored after the next barrier)
+        if (self0) {  // bin M/2, self-paired
+            const c2 Z = Pm, w = rtH;
+            const float sx = Z.x + Z.x, sy = Z.y - Z.y, dx = Z.y + Z.y, dy = -(Z.x - Z.x);
+            st(sq(__builtin_fmaf(w.x, dx, __builtin_fmaf(-w.y, dy, sx)), __builtin_fmaf(w.x, dy, __builtin_fmaf(w.y, dx, sy))),
+               vmid, 0);
+        }
+        const bool missed = __builtin_amdgcn_ballot_w64(sqrt_fast_missed(lo, hi)) != 0;
+        miss |= (uint64_t)missed << (i & 63);
+    };
+    // pass 1 of the next frame from ring[o .. o + 15] (stored after the next barrier)
+    auto pass1 = [&](int o) {
 #pragma unroll
-        for (int k = 0; k < 16; k++) v[k] = {ring[k].x * win[k].x, ring[k].y * win[k].y};
+        for (int k = 0; k < 16; k++) v[k] = {ring[o + k].x * win[k].x, ring[o + k].y * win[k].y};
         radix16<false>(v, tw1);
+    };
+    for (int i = 0;; i += U) {
+        // the ring's U S new values for the next iteration (zeros past the strip: outside rx)
+        c2 nx[U * S];
 #pragma unroll
-        for (int k = 0; k < 16 - S; k++) ring[k] = ring[k + S];
+        for (int s2 = 0; s2 < U * S; s2++) nx[s2] = ld_c2(rx, vo, 8 * TPF * ((i + U + 1) * S + 16 - S + s2));
+        frame(i);
+        if (i + 1 == nf) break;
+        pass1(0);
+        if constexpr (U == 2) {
+            frame(i + 1);
+            if (i + 2 == nf) break;
+            pass1(S);
+        }
 #pragma unroll
-        for (int s2 = 0; s2 < S; s2++) ring[16 - S + s2] = {nx[s2].x * gn, nx[s2].y * gn};
+        for (int k = 0; k < 16 - S; k++) ring[k] = ring[k + U * S];
+#pragma unroll
+        for (int s2 = 0; s2 < U * S; s2++) ring[16 - S + s2] = {nx[s2].x * gn, nx[s2].y * gn};
     }
     // list the strip's missed frames once (k_stft_mag recomputes them right after this kernel)
     if ((lt & 63) == 0) miss_mask[lt >> 6] = miss;

@@ -183,13 +183,15 @@ struct KeyParams {
 // <= 1e-6 and relative score gaps by <= 1e-6 on every track measured (profiles/r05_key_scale.jsonl),
 // so the margins hold a factor of 100.
 constexpr float KV_NEAR_CLARITY = 1e-4f, KV_NEAR_CONF = 1e-4f, KV_NEAR_REL = 1e-3f;
+// KeyOut::near bits: which decision was within its margin
+constexpr int KV_NEAR_ARGMAX = 1, KV_NEAR_GATE = 2, KV_NEAR_FINAL = 4, KV_NEAR_WSUM = 8;
 struct KeyOut {
     int mode, tonic;
     float conf, clarity;
     int ok;
     int used_segments;
     int weights_used;
-    int near;  // near_check only: some energy-dependent decision within its margin (rerun exactly)
+    int near;  // near_check only: KV_NEAR_* bits of the energy-dependent decisions within their margin (rerun exactly)
 };
 
 // ---- k_chroma (opt-in chroma front-ends) ----

@@ -553,7 +553,7 @@ struct TrackRes {
     int8_t mr_trig = -1, mr_used = -1, perc_trig = -1, perc_used = -1;
     bool has_cands = false;
     std::vector<sdsp_tempo_candidate> cands;
-    bool key_near = false;  // block-folded key energies near a decision: rerun with the sequential fold
+    int key_near = 0;  // block-folded key energies near a decision (KV_NEAR_* bits): rerun with the sequential fold
 };
 
 // Configuration support (everything the default path and its numeric knobs need).
@@ -1446,7 +1446,7 @@ void Pipeline::finish_key(std::vector<TrackRes>& res) {
         r.key_tonic = ko.tonic;
         r.key_conf = ko.conf;
         r.key_clarity = ko.clarity;
-        r.key_near = ko.near != 0;
+        r.key_near = ko.near;
     }
     times_.stft8192_ms += kp->kt->ms(0, 1);
     times_.key_ms += kp->kt->ms(1, 2);
@@ -2380,7 +2380,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         r.key_tonic = ko.tonic;
         r.key_conf = ko.conf;
         r.key_clarity = ko.clarity;
-        r.key_near = ko.near != 0;
+        r.key_near = ko.near;
     }
     if (dbg_on) {
         if (NK > 0) {  // src/lib.rs:1471-1538 (the beat-synchronous re-vote keeps the frame-level record)
@@ -2499,7 +2499,7 @@ int32_t run_locked(DeviceCtx& d, const float* d_samples, const uint64_t* offsets
         std::vector<size_t> near;
         d.last_near.assign(res.size(), 0);
         for (size_t i = 0; i < res.size(); i++)
-            if (res[i].key_near) near.push_back(i), d.last_near[i] = 1;
+            if (res[i].key_near) near.push_back(i), d.last_near[i] = (uint8_t)res[i].key_near;
         if (!near.empty()) {
             const sdsp_stage_times first = d.last;
             std::vector<uint64_t> o2, l2;

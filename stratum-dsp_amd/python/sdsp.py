@@ -144,14 +144,15 @@ def test_hooks(fail_chunk=-1, devices=(), stft_frame_parallel=False):
 
 def last_key_near(n, device=0):
     """sdsp_debug_last_key_near: per track of the last analysis call on `device`, whether its key
-    vote was near an energy-dependent decision (and the track was analysed again exactly)."""
+    vote was near an energy-dependent decision (and the track was analysed again exactly): 0, or
+    the reason bits (1 within-mode argmax, 2 segment gate, 4 final key gap, 8 weight-sum fallback)."""
     out = np.zeros(max(int(n), 1), np.uint8)
     f = lib().sdsp_debug_last_key_near
     f.argtypes = [C.c_int32, C.c_void_p, C.c_uint64]
     f.restype = C.c_int32
     if f(device, out.ctypes.data, int(n)) != 0:
         raise RuntimeError("sdsp_debug_last_key_near failed")
-    return out[: int(n)].astype(bool)
+    return out[: int(n)]
 
 
 def key_energy_blocked(config=None, sample_rate=44100):

@@ -70,7 +70,7 @@ def test_near_decision_track_rerun_exact():
     sdsp.generate_synthetic(buf.ptr, 2, n, 44100, seed0=537, bpm_mode=1)
     got = sdsp.analyze_batch_device(buf.ptr, [n], [n], 44100)
     st = sdsp.stage_times()
-    assert st["key_reruns"] == 1 and bool(sdsp.last_key_near(1)[0])
+    assert st["key_reruns"] == 1 and sdsp.last_key_near(1)[0] & 1  # the within-mode argmax margin
     rc, ref = oracle.analyze(buf.to_host(n, n), 44100)
     assert rc == 0
     assert parity.exact_fraction(got[0], ref, strict=True) == 1.0 and not parity.diff_results(got[0], ref)

@@ -5,7 +5,8 @@
 
 Compiles one source of stratum-dsp_amd with the Makefile's flags to device assembly, finds each
 matching kernel's outermost loop with the most instructions (the frame loop of the STFT kernels) and
-counts its instructions per wave and iteration by class:
+counts its instructions per wave and iteration by class (the per-frame VALU figure divides by the
+frames one iteration runs):
   valu (split into f32 add/sub, mul, fma, transcendental, move, select, integer), lds (ds_*), vmem
   (buffer_/global_ loads and stores), scratch (spill traffic), smem, salu, waitcnt, barrier.
 It also reports the kernel's VGPR / LDS / spill figures (-Rpass-analysis=kernel-resource-usage).
@@ -26,11 +27,11 @@ FLAGS = ("--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast
          "-fhip-fp32-correctly-rounded-divide-sqrt -fno-slp-vectorize")
 TRANS = ("v_rsq_", "v_sqrt_", "v_rcp_", "v_exp_", "v_log_", "v_sin_", "v_cos_")
 
-# kernel (mangled-name regex) -> waves per frame of one loop iteration (the census is per frame)
+# kernel (mangled-name regex) -> (waves per frame, frames per loop iteration); the census is per frame
 DEFAULT_KERNELS = {
-    r"k_stft_slide8w3ILi1E": 4,        # 256 threads work on one frame per iteration
-    r"k_stft_slide2sILi4ELb1E": 1,     # one wave per frame per iteration (4 strips per workgroup)
-    r"k_stft_slide2sILi4ELb0E": 1,
+    r"k_stft_slide8w3ILi1E": (4, 2),     # 256 threads per frame; the loop body runs two frames (hop 512)
+    r"k_stft_slide2sILi4ELb1E": (1, 1),  # one wave per frame per iteration (4 strips per workgroup)
+    r"k_stft_slide2sILi4ELb0E": (1, 1),
 }
 
 
@@ -136,11 +137,12 @@ def main():
     ap.add_argument("--src", default=os.path.join(PKG, "csrc", "k_stft.hip"))
     ap.add_argument("--kernel", action="append", help="mangled-name regex (default: the STFT frame loops)")
     ap.add_argument("--waves-per-frame", type=int, default=1)
+    ap.add_argument("--frames-per-iteration", type=int, default=1)
     ap.add_argument("--flags", default=FLAGS)
     ap.add_argument("--extra", default="", help="extra hipcc flags (variants)")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
-    kernels = {k: a.waves_per_frame for k in a.kernel} if a.kernel else DEFAULT_KERNELS
+    kernels = {k: (a.waves_per_frame, a.frames_per_iteration) for k in a.kernel} if a.kernel else DEFAULT_KERNELS
     flags = a.flags + " " + a.extra
     with tempfile.TemporaryDirectory() as td:
         s = os.path.join(td, "k.s")
@@ -150,7 +152,7 @@ def main():
     fns = functions(asm)
     res = resources(a.src, flags)
     out = {"source": os.path.relpath(a.src, ROOT), "flags": flags.strip(), "kernels": {}}
-    for pat, wpf in kernels.items():
+    for pat, (wpf, fpi) in kernels.items():
         for name, body in fns.items():
             if not re.search(pat, name):
                 continue
@@ -161,8 +163,8 @@ def main():
                 cnt[c] = cnt.get(c, 0) + 1
             valu = sum(v for k, v in cnt.items() if k.startswith("valu"))
             out["kernels"][name] = {
-                "waves_per_frame": wpf, "loop_instructions_per_wave": len(loop), "valu_per_wave": valu,
-                "valu_per_frame": valu * wpf, "classes_per_wave": dict(sorted(cnt.items())),
+                "waves_per_frame": wpf, "frames_per_iteration": fpi, "loop_instructions_per_wave": len(loop),
+                "valu_per_wave": valu, "valu_per_frame": valu * wpf / fpi, "classes_per_wave": dict(sorted(cnt.items())),
                 "resources": res.get(name, {}),
             }
     js = json.dumps(out, indent=1)

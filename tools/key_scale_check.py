@@ -42,13 +42,15 @@ def run_set(name, n, threads, sr=44100, seconds=180.0):
     res = sdsp.analyze_batch_device(buf.ptr, offs, lens, sr, raw=True)
     gpu_s = time.time() - t0
     st = sdsp.stage_times()
-    near = [int(i) for i in np.nonzero(sdsp.last_key_near(n))[0]]
+    nb = sdsp.last_key_near(n)
+    near = [int(i) for i in np.nonzero(nb)[0]]
+    why = {name: int(((nb & bit) != 0).sum()) for name, bit in (("argmax", 1), ("gate", 2), ("final", 4), ("wsum", 8))}
     out = {"set": name, "tracks": n, "bpm_mode": SETS[name], "seeds": [0, n - 1], "gpu_s": round(gpu_s, 2),
            "gpu_errors": sum(1 for s in res.status if s != 0), "key_equal": 0, "within_tol": 0,
            "bit_exact_except_key_energy": 0, "bit_exact_strict": 0, "max_key_confidence_diff": 0.0,
            "max_key_clarity_diff": 0.0, "escalated": res.count("tempogram_multi_res_triggered"),
            "key_reruns": int(st.get("key_reruns", 0)), "rerun_ms": round(float(st.get("rerun_ms", 0.0)), 1),
-           "near_tracks": near, "key_mismatch": [], "tolerance_fail": []}
+           "near_reasons": why, "near_tracks": near, "key_mismatch": [], "tolerance_fail": []}
 
     def one(i):
         x = buf.to_host(int(offs[i]), length)
