@@ -482,10 +482,11 @@ std::string fmt2(float v) {
 struct Ctx {
     DeviceCtx& d;
     std::deque<std::vector<uint8_t>> keep;  // host staging kept alive until the next sync
+    std::string pre;  // buffer-name prefix: a nested pipeline's buffers are its own
     explicit Ctx(DeviceCtx& dc) : d(dc) {}
     template <class T>
     T* up(const std::string& name, const std::vector<T>& v) {
-        DevBuf& b = d.buf(name);
+        DevBuf& b = d.buf(pre + name);
         const size_t bytes = std::max<size_t>(v.size() * sizeof(T), 16);
         b.ensure(bytes);
         if (!v.empty()) {
@@ -504,7 +505,7 @@ struct Ctx {
     }
     template <class T>
     T* dev(const std::string& name, size_t n) {
-        DevBuf& b = d.buf(name);
+        DevBuf& b = d.buf(pre + name);
         b.ensure(std::max<size_t>(n * sizeof(T), 16));
         return b.as<T>();
     }
@@ -554,6 +555,7 @@ struct TrackRes {
     bool has_cands = false;
     std::vector<sdsp_tempo_candidate> cands;
     int key_near = 0;  // block-folded key energies near a decision (KV_NEAR_* bits): rerun with the sequential fold
+    bool key_rerun = false;  // that rerun has replaced the key fields
 };
 
 // Configuration support (everything the default path and its numeric knobs need).
@@ -828,7 +830,7 @@ void print_debug(const sdsp_config& c, const TrackDbg& d) {
 class Pipeline {
    public:
     Pipeline(DeviceCtx& d, const sdsp_config& cfg, uint32_t sr, int stages = SDSP_STAGES_FULL, bool exact_energy = false,
-             bool key_only = false)
+             bool key_only = false, bool nested = false)
         : c_(d),
           d_(d),
           cfg_(cfg),
@@ -836,12 +838,15 @@ class Pipeline {
           bpm_only_(stages == SDSP_STAGES_BPM_ONLY),
           exact_energy_(exact_energy),
           key_only_(key_only),
+          nested_(nested),
           fs_((int)std::min<uint64_t>(cfg.frame_size, STFT_GEN_MAX)),
           nb_(fs_ / 2 + 1),
           s2_(base_stride(fs_)),
           kfs_((int)std::min<uint64_t>(key_fft(cfg), STFT_GEN_MAX)),
           khop_((int)std::min<uint64_t>(std::max<uint64_t>(key_hop(cfg), 1), INT32_MAX)),
-          ks_(base_stride(kfs_)) {}
+          ks_(base_stride(kfs_)) {
+        if (nested_) c_.pre = "X.";
+    }
 
     void run(const float* d_samples, const std::vector<uint64_t>& in_off, const std::vector<uint64_t>& n_raw,
              std::vector<TrackRes>& res);
@@ -859,6 +864,13 @@ class Pipeline {
     bool exact_energy_ = false;
     // the key path alone (with exact_energy_: the rerun): front end, key stream, key fields only
     bool key_only_ = false;
+    // a rerun started from inside the main pass (rerun_near): its buffers carry the prefix "X."
+    // and its key path runs on the main stream, in that stream's slack beside the key stream
+    bool nested_ = false;
+    uint64_t reruns_ = 0;
+    double rerun_ms_ = 0.0;
+    void rerun_near(const float* d_samples, const std::vector<uint64_t>& in_off, const std::vector<uint64_t>& n_raw,
+                    const std::vector<size_t>& near, std::vector<TrackRes>& res);
     // the tempo path's STFT: frame size (AnalysisConfig::frame_size), bins, row stride
     const int fs_, nb_, s2_;
     // the key path's STFT: frame size, hop, row stride (key_fft / key_hop)
@@ -886,7 +898,7 @@ class Pipeline {
     };
     std::unique_ptr<KeyPending> key_pending_;
     int sb_parity_ = 0;
-    void finish_key(std::vector<TrackRes>& res);
+    std::vector<size_t> finish_key(std::vector<TrackRes>& res);
     void tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPassOut& out);
     void legacy_select(const TempoPassIn& bin, const uint32_t* d_onsets, const uint64_t* d_on_off, const int* d_on_n,
                        const std::vector<int>& R, const std::vector<int>& idx, std::vector<TrackRes>& res,
@@ -918,8 +930,10 @@ void Pipeline::run(const float* d_samples, const std::vector<uint64_t>& in_off, 
     {
         size_t fr = 0, tot = 0;
         if (hipMemGetInfo(&fr, &tot) == hipSuccess) {
-            double held = 0;
-            for (auto& kv : d_.bufs) held += (double)kv.second->bytes;
+            double held = 0;  // (a nested rerun's "X." buffers are not this pipeline's to reuse)
+            for (auto& kv : d_.bufs)
+                if (kv.first.compare(0, c_.pre.size(), c_.pre) == 0 && (!c_.pre.empty() || kv.first.compare(0, 2, "X.") != 0))
+                    held += (double)kv.second->bytes;
             budget = std::max(4e9, ((double)fr + held) * 0.80 / 1.125);
         }
         // schedule knob (sdsp_debug_set_schedule): the tests' several-sub-batch paths
@@ -967,8 +981,10 @@ void Pipeline::run(const float* d_samples, const std::vector<uint64_t>& in_off, 
         cum += need[i];
     }
     flush();
-    finish_key(res);
+    finish_key(res);  // the last sub-batch's near tracks are rerun by run_locked
     times_.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    times_.key_reruns = reruns_;  // in-flight reruns (rerun_near), their time inside total_ms
+    times_.rerun_ms = rerun_ms_;
     d_.last = times_;
 }
 
@@ -1433,8 +1449,9 @@ void Pipeline::tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPa
 namespace sdsp {
 
 // SDSP_HOST_TRACE=1: host wall time between the sub-batch's synchronisation points (stderr)
-void Pipeline::finish_key(std::vector<TrackRes>& res) {
-    if (!key_pending_) return;
+std::vector<size_t> Pipeline::finish_key(std::vector<TrackRes>& res) {
+    std::vector<size_t> near;
+    if (!key_pending_) return near;
     std::unique_ptr<KeyPending> kp = std::move(key_pending_);
     SDSP_HIP_CHECK(hipStreamWaitEvent(d_.stream, kp->kt->ev[2], 0));
     const std::vector<KeyOut> kout = c_.down(kp->d_kout, kp->at.size());
@@ -1447,9 +1464,36 @@ void Pipeline::finish_key(std::vector<TrackRes>& res) {
         r.key_conf = ko.conf;
         r.key_clarity = ko.clarity;
         r.key_near = ko.near;
+        if (ko.near) near.push_back(kp->at[k]);
     }
     times_.stft8192_ms += kp->kt->ms(0, 1);
     times_.key_ms += kp->kt->ms(1, 2);
+    return near;
+}
+
+// The exact key rerun of near-decision tracks for a finished sub-batch, from inside
+// the main pass: a nested key-only pipeline with the sequential energy fold, its buffers prefixed
+// ("X.") and its key path on the main stream, whose queue then runs it in the slack the tempo path
+// leaves beside the key stream.  The tracks of the last sub-batch are rerun by run_locked.
+void Pipeline::rerun_near(const float* d_samples, const std::vector<uint64_t>& in_off, const std::vector<uint64_t>& n_raw,
+                          const std::vector<size_t>& near, std::vector<TrackRes>& res) {
+    if (near.empty() || exact_energy_ || nested_) return;
+    std::vector<uint64_t> o2, l2;
+    for (size_t i : near) o2.push_back(in_off[i]), l2.push_back(n_raw[i]);
+    std::vector<TrackRes> r2;
+    Pipeline px(d_, cfg_, sr_, SDSP_STAGES_FULL, true, true, true);
+    px.run(d_samples, o2, l2, r2);
+    for (size_t j = 0; j < near.size(); j++) {
+        TrackRes& r = res[near[j]];
+        if (r2[j].status != SDSP_OK) continue;
+        r.key_mode = r2[j].key_mode;
+        r.key_tonic = r2[j].key_tonic;
+        r.key_conf = r2[j].key_conf;
+        r.key_clarity = r2[j].key_clarity;
+        r.key_rerun = true;
+    }
+    reruns_ += near.size();
+    rerun_ms_ += d_.last.total_ms;  // px.run's
 }
 
 struct HostTrace {
@@ -1632,7 +1676,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     sb_parity_ ^= 1;
     const std::string EP = sb_parity_ ? "E1." : "E0.";
     // schedule knob (sdsp_debug_set_schedule): the key path on the main stream (per-kernel profiling)
-    const bool serial_streams = test_hooks().serial_streams.load() != 0;
+    const bool serial_streams = nested_ || test_hooks().serial_streams.load() != 0;
     hipStream_t st2 = serial_streams ? st : d_.stream2;
     hipStream_t st3 = serial_streams ? st : d_.stream3;  // the key vote
     float* d_tune = nullptr;  // per key track tuning offset (tuning compensation)
@@ -1727,7 +1771,8 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         float* d_energy = c_.dev<float>("E.energy", total8);
         // the previous sub-batch's key vote (stream3) reads E.chroma / E.energy: the producers
         // below wait for it (an event never recorded counts as complete)
-        SDSP_HIP_CHECK(hipStreamWaitEvent(st2, d_.vote_done, 0));
+        // (a nested rerun has its own "X." buffers and runs in order on the main stream)
+        if (!nested_) SDSP_HIP_CHECK(hipStreamWaitEvent(st2, d_.vote_done, 0));
         if (use_log) {  // :1120-1131
             const ChromaParams cp = chroma_params(cfg_, sr_, 1, B8, fres8, ks_);
             launch_chroma(1, mags8, d_kpfx, d_ktile, d_kid, NK, ktile.back(), cp, nullptr, d_chroma, d_energy, st2);
@@ -1796,7 +1841,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         launch_key_vote(d_kid, NK, d_kpfx, d_chroma, d_energy, d_cs, d_w, d_sscr, d_kseg, d_tpl, kp, d_kout, st3, d_kdbg);
         SDSP_HIP_CHECK(hipGetLastError());
         kt.mark(2, st3);
-        SDSP_HIP_CHECK(hipEventRecord(d_.vote_done, st3));
+        if (!nested_) SDSP_HIP_CHECK(hipEventRecord(d_.vote_done, st3));
         times_.stft8192_launches += 1;
         times_.stft8192_frames += total8;
         times_.stft8192_bytes += key_in_bytes + 4.0 * (double)total8 * (double)B8;
@@ -2251,8 +2296,9 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     tm.mark(5);
     tm.mark(6);
     const bool beat_sync = cfg_.enable_key_beat_synchronous && !cfg_.enable_key_log_frequency;
-    // the previous sub-batch's key results (its key work ran ahead of this one's on the key stream)
-    finish_key(res);
+    // the previous sub-batch's key results (its key work ran ahead of this one's on the key stream),
+    // and the exact rerun of its near-decision tracks on the main stream
+    rerun_near(d_samples, in_off, n_raw, finish_key(res), res);
     // late join by default (+2 % in alternating bench runs on one box, 2,350 vs 2,301 tracks/s:
     // the main stream otherwise idles ~45 ms per sub-batch waiting for the key tail);
     // no_key_defer (sdsp_debug_set_schedule) joins at the end of each sub-batch (the tests' control)
@@ -2498,8 +2544,10 @@ int32_t run_locked(DeviceCtx& d, const float* d_samples, const uint64_t* offsets
         // independent of the key energies).
         std::vector<size_t> near;
         d.last_near.assign(res.size(), 0);
-        for (size_t i = 0; i < res.size(); i++)
-            if (res[i].key_near) near.push_back(i), d.last_near[i] = (uint8_t)res[i].key_near;
+        for (size_t i = 0; i < res.size(); i++) {
+            if (res[i].key_near) d.last_near[i] = (uint8_t)res[i].key_near;
+            if (res[i].key_near && !res[i].key_rerun) near.push_back(i);  // the last sub-batch's
+        }
         if (!near.empty()) {
             const sdsp_stage_times first = d.last;
             std::vector<uint64_t> o2, l2;
@@ -2518,8 +2566,8 @@ int32_t run_locked(DeviceCtx& d, const float* d_samples, const uint64_t* offsets
             // the call's stage times stay the main pass's; the rerun is reported beside them
             const double rerun_ms = d.last.total_ms;
             d.last = first;
-            d.last.key_reruns = near.size();
-            d.last.rerun_ms = rerun_ms;
+            d.last.key_reruns += near.size();
+            d.last.rerun_ms += rerun_ms;
             d.last.total_ms += rerun_ms;
         }
     } catch (...) {
