@@ -243,18 +243,19 @@ __global__ __launch_bounds__(MASK_T) void k_mask_rp(float* __restrict__ mags, in
     float prev = 0.0f;
     auto finish = [&](float v, int64_t t, int u) {
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), row_rsrc(t, (uint32_t)B * 4u), svo, 0, 2 /* nt */);
-        tile[u][lane] = live ? v * v : 0.0f;
+        tile[u][lane] = v * v;  // lanes past the last bin load x = 0, so v = 0 * (0 / 1e-12) = +0
     };
     // interior element: the full window's quotient by the product + FMA correction, exact on
     // {0} U [2^-90, 2^120] (mask_elem); a wave with a lane outside that range (tiny non-zero or huge
-    // window sums) redoes that lane by the IEEE division, behind a wave-uniform branch
-    auto emit_full = [&](float a, float xr, int64_t t, int u) {
+    // window sums) redoes that lane by the IEEE division, behind a wave-uniform branch.  chk =
+    // false: the block's range test (below) already holds for every lane of the wave
+    auto emit_full = [&](float a, float xr, int64_t t, int u, bool chk = true) {
         const float q0 = a * inv_w;
         float hm = __builtin_fmaf(__builtin_fmaf(-q0, (float)(2 * M + 1), a), inv_w, q0);
         // outside {+-0} U [2^-90, 2^120] (negative, NaN: sign or exponent bits above the range)
         const uint32_t ab = __float_as_uint(a);
         const bool bad = ((ab << 1) != 0u) & (ab - 0x12800000u > 0x7B800000u - 0x12800000u);
-        if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0))
+        if (chk && __builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0))
             if (bad) hm = a / (float)(2 * M + 1);
         const float x = max0_quiet(xr);
         const float h = max0_quiet(hm);
@@ -299,6 +300,24 @@ __global__ __launch_bounds__(MASK_T) void k_mask_rp(float* __restrict__ mags, in
     for (int64_t base = 0; base < F + M; base += R) {
         if (base >= 2 * M && base + R <= F) {
             // interior block: every step has a full window; no edge conditions
+            // the per-element range check once per block: the block's window sums a = P1 - P0 (P
+            // non-decreasing, P1 in [P[base + 1], P[base + R]]) are 0 or >= 2^-90 when P[base + 1]
+            // >= 2^-66 (a nonzero difference is at least half an ulp of P1, or P1 / 2), all 0 when
+            // the block and its past are 0, and <= 2^120 when prev + R max(x) <= 2^118 (the
+            // sequential prefix rounds up by at most (1 + 2^-24)^R); NaN or inf fail the tests
+            float mx = xv[0];
+#pragma unroll
+            for (int u = 1; u < R; u++) mx = __builtin_fmaxf(mx, xv[u]);
+            const bool ok = (prev + xv[0] >= 0x1p-66f || prev + mx == 0.0f) && prev + (float)R * mx <= 0x1p118f;
+            if (__builtin_expect(__builtin_amdgcn_ballot_w64(!ok) == 0, 1)) {
+#pragma unroll
+                for (int u = 0; u < R; u++) {
+                    prev = prev + xv[u];
+                    P[(u + 1) % R] = prev;
+                    X[u % RX] = xv[u];
+                    emit_full(P[(u + 1) % R] - P[(u + R - 2 * M) % R], X[(u + 1) % RX], base + u - M, u, false);
+                }
+            } else
 #pragma unroll
             for (int u = 0; u < R; u++) {
                 prev = prev + xv[u];
