@@ -203,8 +203,10 @@ __device__ __forceinline__ float max0_quiet(float v) {
     return r;
 }
 
+// 4 waves per SIMD (at most 128 VGPRs): with the D1 quotient the compiler otherwise settles at
+// 130 VGPRs and 3 waves, 2-3 % slower (profiles/r05_kernel_ab_mask_d1.txt)
 template <int M, int PW>
-__global__ __launch_bounds__(MASK_T) void k_mask_rp(float* __restrict__ mags, int stride, int B,
+__global__ __launch_bounds__(MASK_T) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_mask_rp(float* __restrict__ mags, int stride, int B,
                                                      const uint64_t* __restrict__ frame_pfx,
                                                      const int* __restrict__ tracks, int blocks_per_track,
                                                      float power, int st_lo, int st_hi, float* __restrict__ part,
@@ -262,7 +264,15 @@ __global__ __launch_bounds__(MASK_T) void k_mask_rp(float* __restrict__ mags, in
         const float r = max_bnn(x - h, 0.0f);
         const float hp = mask_pow<PW>(h, p);
         const float rp = mask_pow<PW>(r, p);
-        finish(x * (hp / (hp + rp + 1e-12f)), t, u);
+        const float den = hp + rp + 1e-12f;
+        if (!chk) {  // the block's range test holds (below)
+            const float y = __builtin_amdgcn_rcpf(den);
+            const float y1 = __builtin_fmaf(__builtin_fmaf(-den, y, 1.0f), y, y);
+            const float q0 = hp * y1;
+            finish(x * __builtin_fmaf(__builtin_fmaf(-den, q0, hp), y1, q0), t, u);
+            return;
+        }
+        finish(x * (hp / den), t, u);
     };
     // the block's partial sums: lane u folds the 64 squares of frame base + u - M in bin order
     auto fold = [&](int64_t base) {
@@ -300,15 +310,26 @@ __global__ __launch_bounds__(MASK_T) void k_mask_rp(float* __restrict__ mags, in
     for (int64_t base = 0; base < F + M; base += R) {
         if (base >= 2 * M && base + R <= F) {
             // interior block: every step has a full window; no edge conditions
-            // the per-element range check once per block: the block's window sums a = P1 - P0 (P
-            // non-decreasing, P1 in [P[base + 1], P[base + R]]) are 0 or >= 2^-90 when P[base + 1]
-            // >= 2^-66 (a nonzero difference is at least half an ulp of P1, or P1 / 2), all 0 when
-            // the block and its past are 0, and <= 2^120 when prev + R max(x) <= 2^118 (the
-            // sequential prefix rounds up by at most (1 + 2^-24)^R); NaN or inf fail the tests
+            // the per-element range checks once per block.  P is non-decreasing and every window
+            // sum a = P1 - P0 has P1 in [P[base + 1], P[base + R]]; a nonzero difference is at
+            // least half an ulp of P1 (or P1 / 2), so a = 0 or a >= P[base + 1] 2^-25, and the
+            // sequential prefix rounds up by at most (1 + 2^-24)^R, so a <= 2^60.01 when prev +
+            // R max(x) <= 2^60.  With P[base + 1] >= 2^-21: a is 0 or in [2^-46, 2^61] (the window
+            // quotient's exact range), hp = h^2 is 0 or >= 2^-103 (the mask quotient's residual is
+            // exact), and with P[base + 1] >= max(x) 2^-31, hp / den >= 2^-124 (r <= x), hp, rp and
+            // den stay below 2^112: the reciprocal + Newton + FMA-residual quotient is then the
+            // correctly rounded one (tools/check_div_fast.hip, D1, every mantissa pair).  max(x)
+            // covers the block's samples and the raw ring (the centres x of the block's first
+            // elements are the previous block's).  A block and past of zeros is exact on either
+            // path.  NaN and inf fail the tests.
             float mx = xv[0];
 #pragma unroll
             for (int u = 1; u < R; u++) mx = __builtin_fmaxf(mx, xv[u]);
-            const bool ok = (prev + xv[0] >= 0x1p-66f || prev + mx == 0.0f) && prev + (float)R * mx <= 0x1p118f;
+#pragma unroll
+            for (int j = 0; j < RX; j++) mx = __builtin_fmaxf(mx, X[j]);
+            const float pf = prev + xv[0];
+            const bool ok = prev + mx == 0.0f ||
+                            (pf >= 0x1p-21f && pf >= mx * 0x1p-31f && prev + (float)R * mx <= 0x1p60f);
             if (__builtin_expect(__builtin_amdgcn_ballot_w64(!ok) == 0, 1)) {
 #pragma unroll
                 for (int u = 0; u < R; u++) {
