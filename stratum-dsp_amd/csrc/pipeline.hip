@@ -1728,11 +1728,15 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         hp.hmax = (int)std::max<uint64_t>(cfg_.key_hpcp_num_harmonics, 1);
         hp.p = sd_clampf(cfg_.key_hpcp_mag_power, 0.05f, 1.0f);
         // sdsp_debug_key_energy_blocked answers the same; exact_energy_: the rerun of near-decision tracks
-        const bool band = key_energy_blocked(cfg_, sr_) && !exact_energy_;
-        float* d_part = band ? c_.dev<float>("E.kpart", total8 * (uint64_t)((B8 + 63) / 64)) : nullptr;
-        if (band) {
-            launch_mask_band(mags8, ks_, B8, d_kpfx, d_kid, NK, cfg_.key_harmonic_mask_power, hp.pk_lo - 1, hp.pk_hi + 1,
-                             d_part, total8, st2);
+        // exact_energy_ on the same configurations (the rerun): the band path's mask storing every
+        // bin (its masked values are k_mask_r's, bit for bit, at less cost), then k_hpcp's one
+        // sequential energy sum; the block sums it also writes go unused
+        const bool blocked = key_energy_blocked(cfg_, sr_);
+        const bool band = blocked && !exact_energy_;
+        float* d_part = blocked ? c_.dev<float>("E.kpart", total8 * (uint64_t)((B8 + 63) / 64)) : nullptr;
+        if (blocked) {
+            launch_mask_band(mags8, ks_, B8, d_kpfx, d_kid, NK, cfg_.key_harmonic_mask_power, band ? hp.pk_lo - 1 : 0,
+                             band ? hp.pk_hi + 1 : B8 - 1, d_part, total8, st2);
         } else if (cfg_.enable_key_hpss_harmonic) {
             const KeyHpssParams kh = key_hpss_params(cfg_, sr_, B8, fres8, ks_);
             if (kh.nb > 0) {  // an empty band returns the spectrogram unchanged (extractor.rs:1408-1410)
