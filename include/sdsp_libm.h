@@ -290,8 +290,10 @@ SD_HD float sd_logf_ge1_t2(float x, const sd_logtab2_t* tab) {
  * of a branch: x = 1 + max(v, 0) is never NaN, and +inf runs the finite arithmetic harmlessly.
  * For i >= 53, k = mant - ((i + 1) << 16) = low16 - 2^16, i.e. low16 with the high half set.
  * The double arithmetic is unchanged; bit-identical on all 2^32 inputs (tools/check_logf_ge1.c). */
-SD_HD float sd_ln1p_max0_t2(float v, const sd_logtab2_t* tab) {
-    const float x = 1.0f + (v > 0.0f ? v : 0.0f);
+SD_HD float sd_ln1p_x_t2(float x, const sd_logtab2_t* tab);
+SD_HD float sd_ln1p_max0_t2(float v, const sd_logtab2_t* tab) { return sd_ln1p_x_t2(1.0f + (v > 0.0f ? v : 0.0f), tab); }
+/* its arithmetic from x = 1 + max(v, 0) (the device caller takes the max without canonicalising) */
+SD_HD float sd_ln1p_x_t2(float x, const sd_logtab2_t* tab) {
     const uint32_t b = sd_bits_f(x);
     const uint32_t off = (b >> 16) & 0x7fu;
     const int hi = off >= 53u;

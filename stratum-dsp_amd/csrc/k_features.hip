@@ -202,6 +202,9 @@ __global__ __launch_bounds__(FT_FRAMES) __attribute__((amdgpu_waves_per_eu(KK > 
     };
     auto fix = [&](int b0) {  // zeros for columns past B and rows outside the track
         const bool col_ok = b0 + jj < B;
+        // only a track's last tile has rows outside it, and only the last chunks columns past B:
+        // a wave with neither skips the selects
+        if (__builtin_amdgcn_ballot_w64(!col_ok || row_ok != (1u << NLD) - 1u) == 0) return;
 #pragma unroll
         for (int u = 0; u < NLD; u++) nx[u] = (col_ok && ((row_ok >> u) & 1)) ? nx[u] : 0.0f;
     };
@@ -211,7 +214,9 @@ __global__ __launch_bounds__(FT_FRAMES) __attribute__((amdgpu_waves_per_eu(KK > 
 #pragma unroll
         for (int u = 0; u < NLD; u++) {
             const int r = wrow + sub + u * RSTEP;
-            ML[r][slot] = make_float2(nx[u], sd_ln1p_max0_t2(nx[u], ltab));
+            // sd_ln1p_max0_t2 with the max taken by max0_quiet: the staged magnitudes are
+            // arithmetic results or zeros, never signalling NaNs
+            ML[r][slot] = make_float2(nx[u], sd_ln1p_x_t2(1.0f + max0_quiet(nx[u]), ltab));
         }
     };
     __syncthreads();  // ltab; from here on each wave works on its own rows

@@ -193,18 +193,6 @@ __global__ __launch_bounds__(MASK_T) void k_mask_r(float* __restrict__ mags, int
 // association differs from the reference's one sequential sum over 4,097 bins (a GPU-only
 // re-association of the key energies); every masked value is bit-identical.
 // Lanes past the last bin stay in the wave and contribute +0 (exact: the sums are >= +0).
-// max_bnn(v, 0) for a v that is never a signalling NaN (the spectrogram and everything computed
-// from it are results of arithmetic, whose NaNs are quiet): the IEEE-mode v_max_f32 already returns
-// 0 for a quiet NaN and +0 for -0, so the canonicalising max the compiler adds in front of a value
-// it cannot see the origin of (a load, a phi) is left out
-__device__ __forceinline__ float max0_quiet(float v) {
-    float r;
-    asm("v_max_f32 %0, 0, %1" : "=v"(r) : "v"(v));
-    return r;
-}
-
-// 4 waves per SIMD (at most 128 VGPRs): with the D1 quotient the compiler otherwise settles at
-// 130 VGPRs and 3 waves, 2-3 % slower (profiles/r05_kernel_ab_mask_d1.txt)
 template <int M, int PW>
 __global__ __launch_bounds__(MASK_T) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_mask_rp(float* __restrict__ mags, int stride, int B,
                                                      const uint64_t* __restrict__ frame_pfx,

@@ -50,6 +50,19 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
 // the NaN tests (sd_maxf(NaN, b) = b = (NaN > b ? NaN : b)).
 __device__ __forceinline__ float max_bnn(float a, float b) { return a > b ? a : b; }
 
+// max_bnn(v, 0) for a v that is never a signalling NaN (the spectrogram and everything computed
+// from it are results of arithmetic, whose NaNs are quiet): the IEEE-mode v_max_f32 already returns
+// 0 for a quiet NaN and +0 for -0, so the canonicalising max the compiler adds in front of a value
+// it cannot see the origin of (a load, a phi) is left out
+__device__ __forceinline__ float max0_quiet(float v) {
+    float r;
+    asm("v_max_f32 %0, 0, %1" : "=v"(r) : "v"(v));
+    return r;
+}
+
+// 4 waves per SIMD (at most 128 VGPRs): with the D1 quotient the compiler otherwise settles at
+// 130 VGPRs and 3 waves, 2-3 % slower (profiles/r05_kernel_ab_mask_d1.txt)
+
 // ---- wave / block reductions (order-free ops only: max, min, integer sums) ----
 __device__ __forceinline__ float wave_max(float v) {
     for (int o = 32; o > 0; o >>= 1) v = sd_maxf(v, __shfl_xor(v, o, 64));
