@@ -357,6 +357,7 @@ __global__ __launch_bounds__(MASK_T) __attribute__((amdgpu_waves_per_eu(4, 4))) 
 
 // ----------------------------------------------------------------------------------------
 constexpr int HP_CW = 16;  // bins per staged chunk (LDS row stride 17: conflict-free)
+constexpr int HPB_CW = HP_CW;  // k_hpcp_band's chunk (32: 164 VGPRs, 3 waves, 15 % slower in round 5)
 
 // The per-frame HPCP state of one thread (extractor.rs:529-680 for one frame): the energy fold,
 // the last two magnitudes for the local-maximum test, and a register-resident top-KCAP list
@@ -523,7 +524,7 @@ __global__ __launch_bounds__(HP_FRAMES) SDSP_HPCP_ATTR void k_hpcp_band(const fl
                                                          const HarmEntry* __restrict__ harm,
                                                          const float* __restrict__ part, int n_blocks, uint64_t total,
                                                          float* __restrict__ chroma, float* __restrict__ energy) {
-    __shared__ float tile[HP_FRAMES][HP_CW + 1];
+    __shared__ float tile[HP_FRAMES][HPB_CW + 1];
     __shared__ float pcs[12][HP_FRAMES];  // pitch-class accumulators (a column per thread)
     const uint64_t gb = blockIdx.x;
     const int it = find_track(tile_pfx, n_items, gb);
@@ -546,9 +547,9 @@ __global__ __launch_bounds__(HP_FRAMES) SDSP_HPCP_ATTR void k_hpcp_band(const fl
         hf.e = e;
     }
     // lane (sub, jj) stages column jj of rows wrow + sub + RSTEP u of its own wave
-    constexpr int RSTEP = 64 / HP_CW;
+    constexpr int RSTEP = 64 / HPB_CW;
     constexpr int NLD = 64 / RSTEP;
-    const int sub = lane / HP_CW, jj = lane % HP_CW;
+    const int sub = lane / HPB_CW, jj = lane % HPB_CW;
     const float* rowp = mags + (g0 + (uint64_t)f0 + (uint64_t)(wrow + sub)) * (uint64_t)P.stride + jj;
     const uint64_t rstride = (uint64_t)RSTEP * (uint64_t)P.stride;
     const int w_lo = P.pk_lo - 1 > 0 ? P.pk_lo - 1 : 0, w_hi = P.pk_hi + 1 < P.B - 1 ? P.pk_hi + 1 : P.B - 1;
@@ -564,15 +565,20 @@ __global__ __launch_bounds__(HP_FRAMES) SDSP_HPCP_ATTR void k_hpcp_band(const fl
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
-    if (w_lo <= w_hi) load_chunk(w_lo);
-    for (int c0 = w_lo; c0 <= w_hi; c0 += HP_CW) {
+    // chunks on HPB_CW-bin boundaries, so every 64-byte row segment is one aligned sector (rows
+    // are 64-byte aligned); the bins below w_lo this adds are no candidates (c < pk_lo), they only
+    // pass through the walk's two-bin history.  (From w_lo itself: 2.2-2.5 % slower; the chunk after
+    // next in flight too: 20-25 % slower, at 4 waves with spills or at 3; round 5.)
+    const int c_start = w_lo & ~(HPB_CW - 1);
+    if (w_lo <= w_hi) load_chunk(c_start);
+    for (int c0 = c_start; c0 <= w_hi; c0 += HPB_CW) {
         wave_sync();  // the previous chunk's walk has read its rows
 #pragma unroll
         for (int u = 0; u < NLD; u++) tile[wrow + sub + u * RSTEP][jj] = nx[u];
         wave_sync();
-        if (c0 + HP_CW <= w_hi) load_chunk(c0 + HP_CW);
+        if (c0 + HPB_CW <= w_hi) load_chunk(c0 + HPB_CW);
         if (!valid) continue;
-        hf.template walk<false>(tile[i], c0, w_hi + 1 - c0 < HP_CW ? w_hi + 1 - c0 : HP_CW, P);
+        hf.template walk<false>(tile[i], c0, w_hi + 1 - c0 < HPB_CW ? w_hi + 1 - c0 : HPB_CW, P);
     }
     if (!valid) return;
     hf.finish(pcs, i, P, harm, chroma, energy, g0 + (uint64_t)f);
