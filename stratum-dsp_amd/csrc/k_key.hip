@@ -358,6 +358,7 @@ __global__ __launch_bounds__(MASK_T) __attribute__((amdgpu_waves_per_eu(4, 4))) 
 // ----------------------------------------------------------------------------------------
 constexpr int HP_CW = 16;  // bins per staged chunk (LDS row stride 17: conflict-free)
 constexpr int HPB_CW = HP_CW;  // k_hpcp_band's chunk (32: 164 VGPRs, 3 waves, 15 % slower in round 5)
+static_assert(HPB_CW == 16, "k_hpcp_band stages a chunk as four 16-byte groups per row");
 
 // The per-frame HPCP state of one thread (extractor.rs:529-680 for one frame): the energy fold,
 // the last two magnitudes for the local-maximum test, and a register-resident top-KCAP list
@@ -546,19 +547,24 @@ __global__ __launch_bounds__(HP_FRAMES) SDSP_HPCP_ATTR void k_hpcp_band(const fl
         for (int g = 0; g < n_blocks; g++) e += pp[(uint64_t)g * total];
         hf.e = e;
     }
-    // lane (sub, jj) stages column jj of rows wrow + sub + RSTEP u of its own wave
-    constexpr int RSTEP = 64 / HPB_CW;
-    constexpr int NLD = 64 / RSTEP;
-    const int sub = lane / HPB_CW, jj = lane % HPB_CW;
-    const float* rowp = mags + (g0 + (uint64_t)f0 + (uint64_t)(wrow + sub)) * (uint64_t)P.stride + jj;
-    const uint64_t rstride = (uint64_t)RSTEP * (uint64_t)P.stride;
     const int w_lo = P.pk_lo - 1 > 0 ? P.pk_lo - 1 : 0, w_hi = P.pk_hi + 1 < P.B - 1 ? P.pk_hi + 1 : P.B - 1;
-    float nx[NLD];
+    // lane (r4, q4) stages bins 4 q4 .. 4 q4 + 3 of rows wrow + r4 + 16 u (u < 4), one 16-byte load
+    // per row: a wave load covers 16 rows' 64-byte segments (4 with 4-byte loads: 8.8 % slower per
+    // launch, round 5)
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const int r4 = lane >> 2, q4 = lane & 3;
+    const f4v* rowp4 = reinterpret_cast<const f4v*>(mags + (g0 + (uint64_t)f0 + (uint64_t)(wrow + r4)) * (uint64_t)P.stride + 4 * q4);
+    const uint64_t rstride4 = 4 * (uint64_t)P.stride;  // 16 rows, in f4v units
+    f4v n4[4];
     auto load_chunk = [&](int c0) {
-        const bool col_ok = c0 + jj <= w_hi;
 #pragma unroll
-        for (int u = 0; u < NLD; u++)
-            nx[u] = (wrow + sub + u * RSTEP < rows && col_ok) ? rowp[(uint64_t)u * rstride + c0] : 0.0f;
+        for (int u = 0; u < 4; u++) {
+            f4v v = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (wrow + r4 + 16 * u < rows) v = rowp4[(uint64_t)u * rstride4 + (uint64_t)(c0 >> 2)];
+            const int b = c0 + 4 * q4;
+            n4[u] = f4v{b <= w_hi ? v.x : 0.0f, b + 1 <= w_hi ? v.y : 0.0f, b + 2 <= w_hi ? v.z : 0.0f,
+                        b + 3 <= w_hi ? v.w : 0.0f};
+        }
     };
     auto wave_sync = [] {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -574,7 +580,13 @@ __global__ __launch_bounds__(HP_FRAMES) SDSP_HPCP_ATTR void k_hpcp_band(const fl
     for (int c0 = c_start; c0 <= w_hi; c0 += HPB_CW) {
         wave_sync();  // the previous chunk's walk has read its rows
 #pragma unroll
-        for (int u = 0; u < NLD; u++) tile[wrow + sub + u * RSTEP][jj] = nx[u];
+        for (int u = 0; u < 4; u++) {
+            float* tr = tile[wrow + r4 + 16 * u] + 4 * q4;
+            tr[0] = n4[u].x;
+            tr[1] = n4[u].y;
+            tr[2] = n4[u].z;
+            tr[3] = n4[u].w;
+        }
         wave_sync();
         if (c0 + HPB_CW <= w_hi) load_chunk(c0 + HPB_CW);
         if (!valid) continue;
