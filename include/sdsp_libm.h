@@ -313,6 +313,47 @@ SD_HD float sd_ln1p_x_t2(float x, const sd_logtab2_t* tab) {
     return x < SD_INF_F ? y : x;
 }
 
+/* sd_ln1p_x_t2 from a 9-bit table and a degree-4 polynomial (round 5): x = 2^e m, i = the top 9
+ * mantissa bits, c = 1 + i/512 (i < 212) or (1 + (i+1)/512) / 2 with m/2 and e + 1 (i >= 212); r = k s
+ * with k the mantissa's offset from c's (14 bits, or negative for i >= 212) and s = (1/c) 2^-23 or
+ * 2^-24 from include/sdsp_logtab9.h; ln(1 + r) by its degree-4 Taylor polynomial (|r| < 2^-9); and
+ * e ln 2 from a per-exponent pair {e LN2_HI (exact: LN2_HI has 21 trailing zero bits), RN(e LN2_LO)},
+ * so the sum is three double additions: 10 double operations instead of 13.  Bit-identical to
+ * sd_logf_ge1 on every finite f32 >= 1 (tools/check_logf_ge1.c, exhaustive; the same check finds 634
+ * differences with a degree-3 polynomial, 22 with an 8-bit table).  x = +inf is the caller's select. */
+#include "sdsp_logtab9.h"
+#define SD_LOGTAB9_PIV 212
+typedef struct {
+    double hi, lo;
+} sd_ln2tab_t;
+#if defined(__HIPCC__) || defined(__HIP__)
+static __constant__ const sd_logtab2_t SD_LOGTAB9_D[512] = SDSP_LOGTAB9_INIT;
+#endif
+static const sd_logtab2_t SD_LOGTAB9_H[512] = SDSP_LOGTAB9_INIT;
+/* e ln 2 for e = 0 .. 128 (every exponent of x in [1, +inf], the pivot's e + 1 included) */
+SD_HD sd_ln2tab_t sd_ln2tab_from(int e) {
+    sd_ln2tab_t t;
+    t.hi = (double)e * SD_LN2_HI;
+    t.lo = (double)e * SD_LN2_LO;
+    return t;
+}
+SD_HD float sd_ln1p_x_t9_finite(float x, const sd_logtab2_t* tab, const sd_ln2tab_t* et) {
+    const uint32_t b = sd_bits_f(x);
+    const uint32_t off = (b >> 14) & 0x1ffu;
+    const int hi = off >= (uint32_t)SD_LOGTAB9_PIV;
+    const int k = (int)((b & 0x3fffu) | (hi ? 0xffffc000u : 0u)); /* low 14 bits, minus 2^14 for hi */
+    const int e = (int)(b >> 23) - (hi ? 126 : 127);
+    const sd_logtab2_t t = tab[off];
+    const double r = (double)k * t.s;
+    double p = -0.25;
+    p = __builtin_fma(p, r, 1.0 / 3.0);
+    p = __builtin_fma(p, r, -0.5);
+    p = __builtin_fma(p, r, 1.0);
+    p = p * r;
+    const sd_ln2tab_t E = et[e];
+    return (float)(E.hi + (E.lo + (t.lg + p)));
+}
+
 /* f32::log10 */
 SD_HD float sd_log10f(float x) {
     if (x != x) return x;

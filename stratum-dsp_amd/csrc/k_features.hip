@@ -62,9 +62,13 @@ __global__ __launch_bounds__(FT_FRAMES) __attribute__((amdgpu_waves_per_eu(KK > 
     // with one ds_read_b64 at a per-chunk base plus an immediate offset (the chunk's 8 slots never
     // wrap: CW divides W), and the staging writes both with one ds_write_b64
     __shared__ float2 ML[ROWS][LS];
-    __shared__ sd_logtab2_t ltab[128];  // sd_logf's table {s, ln c}, read per element by the staging
+    // the staging's log tables (sd_ln1p_x_t9_finite): {s, ln c} per 9-bit mantissa index and
+    // {e LN2_HI, RN(e LN2_LO)} per exponent, read per element
+    __shared__ sd_logtab2_t ltab[512];
+    __shared__ sd_ln2tab_t etab[129];
     static_assert(KK == 0 || CW + 2 * KK <= W, "window halo must fit the ring");
-    for (int q = threadIdx.x; q < 128; q += FT_FRAMES) ltab[q] = sd_logtab2_from(SD_LOGTAB_D, q);
+    for (int q = threadIdx.x; q < 512; q += FT_FRAMES) ltab[q] = SD_LOGTAB9_D[q];
+    for (int q = threadIdx.x; q < 129; q += FT_FRAMES) etab[q] = sd_ln2tab_from(q);
 
     const uint64_t gb = blockIdx.x;
     const int trk = find_track(tile_pfx, T, gb);
@@ -214,9 +218,12 @@ __global__ __launch_bounds__(FT_FRAMES) __attribute__((amdgpu_waves_per_eu(KK > 
 #pragma unroll
         for (int u = 0; u < NLD; u++) {
             const int r = wrow + sub + u * RSTEP;
-            // sd_ln1p_max0_t2 with the max taken by max0_quiet: the staged magnitudes are
-            // arithmetic results or zeros, never signalling NaNs
-            ML[r][slot] = make_float2(nx[u], sd_ln1p_x_t2(1.0f + max0_quiet(nx[u]), ltab));
+            // sd_ln1p_max0_t2 with the max taken by max0_quiet (the staged magnitudes are
+            // arithmetic results or zeros, never signalling NaNs) and the 9-bit-table, degree-4
+            // evaluation, bit-identical to sd_logf on every finite f32 >= 1 (sdsp_libm.h)
+            const float xx = 1.0f + max0_quiet(nx[u]);
+            const float lv = sd_ln1p_x_t9_finite(xx, ltab, etab);
+            ML[r][slot] = make_float2(nx[u], xx < SD_INF_F ? lv : xx);
         }
     };
     __syncthreads();  // ltab; from here on each wave works on its own rows

@@ -1,6 +1,7 @@
 /* Exhaustive checks: sd_logf_ge1_t2 (two-column table, no m / c formed) against sd_logf_ge1 on
  * every f32 >= 1 (finite, +inf) and a NaN; sd_ln1p_max0_t2(v) against
- * sd_logf_ge1_t2(1 + sd_maxf(v, 0)) on all 2^32 bit patterns of v.
+ * sd_logf_ge1_t2(1 + sd_maxf(v, 0)) on all 2^32 bit patterns of v; and (round 5) the 9-bit-table,
+ * degree-4 sd_ln1p_x_t9_finite against sd_logf_ge1 on every finite f32 >= 1.
  * gcc -O2 -ffp-contract=off -march=x86-64-v3 -fopenmp */
 #include <stdio.h>
 #include <stdint.h>
@@ -35,5 +36,20 @@ int main(void) {
         }
     }
     printf("ln(1 + max(v, 0)), all v: %lld inputs, %lld differ (last 0x%08x)\n", n2, diff2, first2);
-    return diff != 0 || diff2 != 0;
+    sd_ln2tab_t et[129];
+    for (int e = 0; e < 129; e++) et[e] = sd_ln2tab_from(e);
+    long long diff3 = 0, n3 = 0;
+    uint32_t first3 = 0;
+#pragma omp parallel for reduction(+ : diff3, n3) schedule(static, 1 << 20)
+    for (long long u = 0x3f800000LL; u < 0x7f800000LL; u++) {
+        const float x = sd_from_bits_f((uint32_t)u);
+        const float a = sd_logf_ge1(x, SD_LOGTAB_H), b = sd_ln1p_x_t9_finite(x, SD_LOGTAB9_H, et);
+        n3++;
+        if (sd_bits_f(a) != sd_bits_f(b)) {
+            diff3++;
+            first3 = (uint32_t)u;
+        }
+    }
+    printf("9-bit table, degree 4, finite f32 >= 1: %lld inputs, %lld differ (last 0x%08x)\n", n3, diff3, first3);
+    return diff != 0 || diff2 != 0 || diff3 != 0;
 }
