@@ -161,29 +161,6 @@ __device__ __forceinline__ void radix16(c2 v[16], const c2 w[15]) {
                      v[ja + 4], v[ja + 8], v[ja + 12]);
 }
 
-// radix16 with scheduling fences between its eight butterflies: the same operations in the same
-// order per element, evaluated butterfly by butterfly (at most 16 + 8 live complex values), for a
-// caller whose register budget is at its limit (k_stft_slide8w3's pass 1 beside the register ring)
-template <bool LAST>
-__device__ __forceinline__ void radix16_fenced(c2 v[16], const c2 w[15]) {
-    c2 u[16];
-#pragma unroll
-    for (int jp = 0; jp < 4; jp++) {
-        if (LAST && jp == 0)
-            bfly4<false>(v[0], v[4], v[8], v[12], w[0], w[0], w[0], u[0], u[1], u[2], u[3]);
-        else
-            bfly4<true>(v[jp], v[jp + 4], v[jp + 8], v[jp + 12], w[3 * jp + 0], w[3 * jp + 1], w[3 * jp + 2],
-                        u[jp * 4 + 0], u[jp * 4 + 1], u[jp * 4 + 2], u[jp * 4 + 3]);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-#pragma unroll
-    for (int ja = 0; ja < 4; ja++) {
-        bfly4<!LAST>(u[0 * 4 + ja], u[1 * 4 + ja], u[2 * 4 + ja], u[3 * 4 + ja], w[12], w[13], w[14], v[ja + 0],
-                     v[ja + 4], v[ja + 8], v[ja + 12]);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-}
-
 // radix16 whose 15 twiddles come from a loader (tw(j) = w[j] of radix16) fetched per butterfly:
 // stage A's butterfly j' takes tw(3 j' .. 3 j' + 2) just before it runs and stage B's three are
 // fetched after stage A, so at most 3 twiddles are live instead of 15 (k_stft_slide8w3's pass 2,
