@@ -559,9 +559,11 @@ __global__ __launch_bounds__(HP_FRAMES) SDSP_HPCP_ATTR void k_hpcp_band(const fl
     auto load_chunk = [&](int c0) {
 #pragma unroll
         for (int u = 0; u < 4; u++) {
-            f4v v = {0.0f, 0.0f, 0.0f, 0.0f};
-            if (wrow + r4 + 16 * u < rows) v = rowp4[(uint64_t)u * rstride4 + (uint64_t)(c0 >> 2)];
+            // a group wholly past w_hi is not read; one that starts at a bin b <= w_hi < B ends
+            // inside the row (strides are multiples of 4 floats, at least B: b + 4 <= stride)
             const int b = c0 + 4 * q4;
+            f4v v = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (wrow + r4 + 16 * u < rows && b <= w_hi) v = rowp4[(uint64_t)u * rstride4 + (uint64_t)(c0 >> 2)];
             n4[u] = f4v{b <= w_hi ? v.x : 0.0f, b + 1 <= w_hi ? v.y : 0.0f, b + 2 <= w_hi ? v.z : 0.0f,
                         b + 3 <= w_hi ? v.w : 0.0f};
         }
