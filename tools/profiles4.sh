@@ -11,7 +11,7 @@ timeout -k 10 600 python3 $R/bench.py > $O/bench.json 2> $O/bench.err &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/conc -o $tag -- python3 $R/bench.py --tracks 1024 --steps 2 --warmup 1 --no-cpu-baseline --no-probe > $O/conc.json 2> $O/conc.err &&
 python3 $R/tools/kdur.py $O/conc/${tag}_kernel_trace.csv 3000 > $O/conc_kdur.txt &&
 SDSP_SERIAL_STREAMS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/serial -o $tag -- python3 $R/bench.py --tracks 1024 --steps 2 --warmup 1 --no-cpu-baseline --no-probe > $O/serial.json 2> $O/serial.err &&
-python3 $R/tools/step_kernels.py $O/serial/${tag}_kernel_trace.csv > $O/serial_step.txt &&
+python3 $R/tools/step_kernels.py $O/serial/${tag}_kernel_trace.csv 4 > $O/serial_step.txt &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/probe -o $tag -- python3 $R/tools/stft_probe.py > $O/probe.jsonl 2> $O/probe.err &&
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_stft --output-format csv -d $O/fetch -o $tag -- python3 $R/bench.py --tracks 64 --steps 1 --warmup 0 --no-cpu-baseline --no-probe > $O/fetch.log 2>&1 &&
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_stft --output-format csv -d $O/write -o $tag -- python3 $R/bench.py --tracks 64 --steps 1 --warmup 0 --no-cpu-baseline --no-probe > $O/write.log 2>&1 &&
