@@ -80,6 +80,27 @@ __device__ __forceinline__ void bfly4(c2 a, c2 b, c2 c, c2 d, c2 w1, c2 w2, c2 w
     }
 }
 
+// 16 LDS elements p[17 k], k < 16, read as 16 single ds_read_b64 (the compiler pairs them into
+// ds_read2_b64, 8 LDS cycles per pair against 2 per single read), then waited for
+__device__ __forceinline__ void lds_ld16_s17(const c2* p, c2 v[16]) {
+    typedef __attribute__((address_space(3))) const c2 lds_c2;
+    const uint32_t a = (uint32_t)(uintptr_t)(lds_c2*)p;
+    uint64_t r[16];
+    asm volatile(
+        "ds_read_b64 %0, %16\n ds_read_b64 %1, %16 offset:136\n ds_read_b64 %2, %16 offset:272\n"
+        "ds_read_b64 %3, %16 offset:408\n ds_read_b64 %4, %16 offset:544\n ds_read_b64 %5, %16 offset:680\n"
+        "ds_read_b64 %6, %16 offset:816\n ds_read_b64 %7, %16 offset:952\n ds_read_b64 %8, %16 offset:1088\n"
+        "ds_read_b64 %9, %16 offset:1224\n ds_read_b64 %10, %16 offset:1360\n ds_read_b64 %11, %16 offset:1496\n"
+        "ds_read_b64 %12, %16 offset:1632\n ds_read_b64 %13, %16 offset:1768\n ds_read_b64 %14, %16 offset:1904\n"
+        "ds_read_b64 %15, %16 offset:2040\n s_waitcnt lgkmcnt(0)"
+        : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]), "=&v"(r[7]),
+          "=&v"(r[8]), "=&v"(r[9]), "=&v"(r[10]), "=&v"(r[11]), "=&v"(r[12]), "=&v"(r[13]), "=&v"(r[14]), "=&v"(r[15])
+        : "v"(a)
+        : "memory");
+#pragma unroll
+    for (int k = 0; k < 16; k++) v[k] = __builtin_bit_cast(c2, r[k]);
+}
+
 __device__ __forceinline__ int lpad(int i) { return i + (i >> 4); }
 #define P17 17
 #define P272 272
@@ -1226,7 +1247,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     auto frame = [&](int i) {
         if (i > 0) __syncthreads();  // every last-pass read of frame i - 1 is done
 #pragma unroll
-        for (int k = 0; k < 16; k++) buf[P17 * lt + k] = v[k];
+        for (int k = 0; k < 16; k++) {
+            buf[P17 * lt + k] = v[k];
+        }
         __syncthreads();
         // pass 2 (n = M/16, s = 16), in place
 #pragma unroll
@@ -1237,8 +1260,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
         __syncthreads();
         // last pass (n = 16, s = 256, p' = 0) on column colA, then the (k, M-k) exchange between
         // lanes l and l^32: every lane sends its elements 8..15; the column-0 lane sends itself 9..15, 0
+#ifndef SDSP_STFT8_PAIRED
+        lds_ld16_s17(&buf[rb3], v);
+#else
 #pragma unroll
         for (int k = 0; k < 16; k++) v[k] = buf[rb3 + P17 * k];
+#endif
         radix16<true>(v, tw3);
         c2 P[16];
 #pragma unroll

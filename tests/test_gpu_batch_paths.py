@@ -108,6 +108,35 @@ def test_config2_shaped_sub_batches(monkeypatch):
         assert stt == 0 and parity.exact_fraction(res[i], ref) == 1.0, i
 
 
+def test_config3_shards_through_eight_workers(monkeypatch):
+    """BASELINE config 3 (8192 3-min tracks sharded across 8 GPUs, 1024 per rank: bench.py's
+    shard_seed0, seeds 1024 r ..): three tracks from each of the eight shard seed ranges (first,
+    middle, last) through sdsp_analyze_batch with an 8-entry device list.  The test build maps
+    every entry to device 0, so eight workers, eight copier threads and their copy streams deal
+    the 24 tracks out of the shared chunk counter (3-track chunks: one per worker) as the
+    reference's caller-side fan-out does (examples/analyze_batch.rs:239-268).  Every result is
+    checked against the oracle."""
+    L = 180 * 44100
+    seeds = [1024 * r + k for r in range(8) for k in (0, 511, 1023)]
+    buf = sdsp.DeviceBuffer(L)
+    tracks = []
+    for s in seeds:
+        sdsp.generate_synthetic(buf.ptr, 1, L, seed0=s)
+        tracks.append(buf.to_host(0, L))
+    monkeypatch.setenv("SDSP_BATCH_CHUNK_TRACKS", "3")
+    monkeypatch.delenv("SDSP_SERIAL_STREAMS", raising=False)
+    with sdsp.test_hooks(devices=(0,) * 8):
+        res = sdsp.analyze_batch(tracks)
+    assert len(res) == len(seeds)
+    with cf.ThreadPoolExecutor(8) as ex:
+        refs = list(ex.map(lambda x: oracle.analyze(x, 44100), tracks))
+    for i, ((st, ref), r) in enumerate(zip(refs, res)):
+        assert st == 0, (seeds[i], ref)
+        assert not isinstance(r, sdsp.AnalysisError), (seeds[i], r)
+        assert not parity.diff_results(r, ref), (seeds[i], parity.diff_results(r, ref))
+        assert parity.exact_fraction(r, ref) == 1.0, seeds[i]
+
+
 def test_concurrent_callers():
     tracks = [synth.make_track(5400 + k, seconds=12.0 + 3 * k)[0] for k in range(8)]
     with cf.ThreadPoolExecutor(4) as ex:
