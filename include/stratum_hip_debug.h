@@ -55,9 +55,18 @@ int32_t sdsp_debug_key_energy_blocked(const sdsp_config* cfg, uint32_t sample_ra
  * key energies left a key decision within its margin, so the track's key path ran again with the
  * sequential energy fold (sdsp_stage_times.key_reruns counts them), else 0.  Bits: 1 a segment's
  * (or the slice's) within-mode argmax, 2 a segment clarity gate, 4 the final key gap, 8 the
- * weight-sum fallback.
+ * weight-sum fallback, 16 a weight, energy or mode top outside the certificate's range (underflow,
+ * no usable bound, near the 1e-9 normalisation guard).
  */
 int32_t sdsp_debug_last_key_near(int32_t device, uint8_t* out, uint64_t n);
+
+/*
+ * The key vote's near-decision certificate on the default key path: 0 (default) the
+ * rigorous bounds (per-frame energy bounds carried through the weights, raw scores, clarities and
+ * the vote, with the fixed margins as floors); non-zero the fixed round-5 margins alone (A/B of the
+ * flagged sets).  Process-wide; applies to the next analysis calls.
+ */
+int32_t sdsp_debug_set_key_cert(int32_t fixed_margins);
 
 /* Free and total HBM bytes of `device` (the benchmark sizes its kernel probe by them). */
 int32_t sdsp_debug_mem_info(int32_t device, uint64_t* free_bytes, uint64_t* total_bytes);

@@ -510,6 +510,40 @@ __global__ __launch_bounds__(HP_FRAMES) SDSP_HPCP_ATTR void k_hpcp(const float* 
     hf.finish(pcs, i, P, harm, chroma, energy, g0 + (uint64_t)f);
 }
 
+// A rigorous bound on |e_blk - e_ref| / e_blk for one frame ("Certification"): e_blk
+// is this engine's fold of the 65 block sums Bt_b (each the sequential f32 fold of its 64 squares
+// t_k = RN(x_k^2) from 0, k_mask_rp), e_ref the reference's one sequential f32 fold of the same
+// 4,097 squares (extractor.rs:1133).  With u = 2^-24, T = sum t_k (exact), B_b the exact block sums:
+//   |Bt_b - B_b| <= g63 B_b, so B_b <= Bt_b / (1 - g63) =: Bu_b;
+//   |e_blk - sum Bt_b| <= u (1 + g64) sum_b (Bt_0 + .. + Bt_b)   (one rounding per block fold step);
+//   |sum Bt_b - T| <= g63 sum_b Bu_b;
+//   |e_ref - T| <= sum_k |d_k|, d_k the rounding of the reference's step k: |d_k| <= t_k (its
+//   partial sum S_{k-1} is a float next to S_{k-1} + t_k) and |d_k| <= u (1 + u) U_b for k in block
+//   b, U_b = (Bu_0 + .. + Bu_b)(1 + gN) bounding every partial sum there (the terms are >= 0), so
+//   block b adds at most min(Bu_b, n_b u (1 + u) U_b).
+// Evaluated in double (relative error ~1e-14, covered by a 1e-9 factor) and rounded up to f32.
+// e_blk = 0 means every square is +0, so both folds are +0 (bound 0).
+__device__ float energy_delta(const float* __restrict__ pp, uint64_t total, int n_blocks, int B, float e_blk) {
+    if (!(e_blk > 0.0f)) return 0.0f;
+    const double u = 0x1p-24, g63 = 63.0 * u / (1.0 - 63.0 * u), g64 = 64.0 * u / (1.0 - 64.0 * u);
+    const double gN = (double)B * u / (1.0 - (double)B * u), iu = 1.0 / (1.0 - g63);
+    double pu = 0.0, pt = 0.0, eref = 0.0, eo = 0.0;
+    for (int g = 0; g < n_blocks; g++) {
+        const double bt = (double)pp[(uint64_t)g * total], bu = bt * iu;
+        pu += bu;
+        pt += bt;
+        const int nb = B - 64 * g < 64 ? B - 64 * g : 64;
+        eref += __builtin_fmin(bu, (double)nb * u * (1.0 + u) * pu * (1.0 + gN));
+        eo += pt;
+    }
+    const double D = (eref + u * (1.0 + u) * (1.0 + g64) * eo + g63 * pu) * (1.0 + 1e-9);
+    const double r = D / (double)e_blk;
+    if (!(r < 1.0)) return 1.0f;  // no usable bound (cannot happen for finite sums); the vote flags it
+    float d = (float)r;
+    if ((double)d < r) d = __uint_as_float(__float_as_uint(d) + 1u);
+    return d;
+}
+
 // k_hpcp_band: k_hpcp after k_mask_rp.  The frame energy folds the 65 block sums part[g][frame] in
 // block order; the bin walk covers only the band k_mask_rp stored, [pk_lo - 1, pk_hi + 1] (the
 // local-maximum test of candidate c reads bins c - 1 .. c + 1; starting the walk at pk_lo - 1 with
@@ -524,7 +558,8 @@ __global__ __launch_bounds__(HP_FRAMES) SDSP_HPCP_ATTR void k_hpcp_band(const fl
                                                          const int* __restrict__ tracks, int n_items, HpcpParams P,
                                                          const HarmEntry* __restrict__ harm,
                                                          const float* __restrict__ part, int n_blocks, uint64_t total,
-                                                         float* __restrict__ chroma, float* __restrict__ energy) {
+                                                         float* __restrict__ chroma, float* __restrict__ energy,
+                                                         float* __restrict__ edel) {
     __shared__ float tile[HP_FRAMES][HPB_CW + 1];
     __shared__ float pcs[12][HP_FRAMES];  // pitch-class accumulators (a column per thread)
     const uint64_t gb = blockIdx.x;
@@ -546,6 +581,8 @@ __global__ __launch_bounds__(HP_FRAMES) SDSP_HPCP_ATTR void k_hpcp_band(const fl
         float e = 0.0f;
         for (int g = 0; g < n_blocks; g++) e += pp[(uint64_t)g * total];
         hf.e = e;
+        // the certificate's per-frame energy bound (k_key_vote, KeyParams::near_check)
+        if (edel) edel[g0 + (uint64_t)f] = energy_delta(pp, total, n_blocks, P.B, e);
     }
     const int w_lo = P.pk_lo - 1 > 0 ? P.pk_lo - 1 : 0, w_hi = P.pk_hi + 1 < P.B - 1 ? P.pk_hi + 1 : P.B - 1;
     // lane (r4, q4) stages bins 4 q4 .. 4 q4 + 3 of rows wrow + r4 + 16 u (u < 4), one 16-byte load
@@ -789,8 +826,126 @@ __device__ void mode_heuristic(float sorted[24], int order[24], const float* avg
     *conf = cs > 0.0f ? sd_clampf((cs - other) / cs, 0.0f, 1.0f) : 0.0f;
 }
 
-constexpr int KV_ROW = 64;  // segment scratch row: 24 sorted, 24 order, clarity, used, cw, wsum, avg[12]
 constexpr int KV_MAXSCALE = 8;
+
+// ---- the rigorous near-decision certificate (KeyParams::near_check, cert_fixed = 0) ----
+// k_hpcp_band bounds each frame's energy by |e_ref - e| <= d_f e (energy_delta).  With p the energy
+// power, the reference's frame weight is w'_f = c w_f (1 + eps_f), |eps_f| <= eta_f (kc_eta), c the
+// factor (med / med')^p its median carries for every frame alike: every decision below is invariant
+// under a common factor of the weights, so only eta_f and the roundings matter.  Every raw score is
+// R_x = sequential sum over frames of RN(w_f D_fx) (D_fx the frame's template dot, identical on both
+// sides), so |R'_x - c R_x| <= c (V_x (1 + 2u) + N_x) with V_x = sum_f eta_f w_f D_fx and
+// N_x = u (2.0001 R_x + (1 + K) SS_x), SS_x the sum of the fold's partial sums (both sides' roundings;
+// K bounds the reference's partial sums against c times ours).
+constexpr double KC_U = 0x1p-24;
+constexpr int KC_CAP = 32;
+struct KcCand {
+    int64_t st;     // the table's frames [st, st + len) of the slice
+    int len, w, k;  // the mode's argmax W and a competitor k (key indices)
+    float slack;    // G - N_W - N_k - 1.01 u R_W: what E_Wk must stay below
+};
+// a non-negative double rounded up to f32
+__device__ __forceinline__ float kc_up(double x) {
+    float d = (float)x;
+    if ((double)d < x) d = __uint_as_float(__float_as_uint(d) + 1u);
+    return d;
+}
+__device__ __forceinline__ double kc_noise(double R, double SS, double K) { return KC_U * (2.0001 * R + (1.0 + K) * SS); }
+// eta_f for an energy bound d and energy power p: the weight ratio w'/(c w) lies in [e^-L, e^L] with
+// L = p d / (1 - d) (the energy) + 2.0001 u p (the two e / med roundings) + 2.0001 (u + 2^-40) (the
+// two powf evaluations: double exp / log, then one rounding) + 2.0001 u (the two tonal products);
+// e^L - 1 <= L / (1 - L)
+__device__ __forceinline__ double kc_eta(double d, double p) {
+    const double L = p * d / (1.0 - d) + 2.0001 * KC_U * p + 2.0001 * (KC_U + 0x1p-40) + 2.0001 * KC_U;
+    return L / (1.0 - L);
+}
+// The within-mode argmaxes (key_from_raw's last maximum W) of the reference equal this table's when,
+// for every other key k of the mode, G = R_W - R_k > N_W + N_k + E_Wk + 1.01 u R_W (the margin keeps
+// RN(R'_k / R'_W) below 1, so the normalised scores cannot tie), where E_Wk = sum_f eta_f w_f
+// |D_fW - D_fk| <= V_W + V_k.  Pairs that fail even with E_Wk = 0 are flagged; pairs that only the
+// loose V_W + V_k fails are queued for the pair pass (kc_pair_pass), which computes E_Wk.
+__device__ __noinline__ int kc_argmax(const float* raw, const float* SS, const float* V, double sf, double K, int64_t st, int len,
+                         KcCand* list, int* nlist) {
+    int bits = 0;
+    for (int m = 0; m < 2; m++) {
+        int W = 0;
+        for (int k = 1; k < 12; k++)
+            if (!(raw[12 * m + k] < raw[12 * m + W])) W = k;
+        const double RW = raw[12 * m + W];
+        if (!(RW > 0.0)) continue;  // an all-zero mode: every product is +0 on both sides
+        const double NW = kc_noise(RW, SS[12 * m + W] * sf, K), VW = V[12 * m + W] * sf;
+        for (int k = 0; k < 12; k++) {
+            if (k == W) continue;
+            const double Rk = raw[12 * m + k], G = RW - Rk;
+            const double need0 = NW + kc_noise(Rk, SS[12 * m + k] * sf, K) + 1.01 * KC_U * RW;
+            if (G > need0 + (VW + V[12 * m + k] * sf) * (1.0 + 2.0001 * KC_U)) continue;
+            const int q = G > need0 ? atomicAdd(nlist, 1) : KC_CAP;
+            if (q < KC_CAP) {
+                float sl = (float)(G - need0);
+                if ((double)sl > G - need0) sl = __uint_as_float(__float_as_uint(sl) - 1u);  // round down
+                list[q] = KcCand{st, len, 12 * m + W, 12 * m + k, sl};
+            } else {
+                bits |= KV_NEAR_ARGMAX;
+            }
+        }
+    }
+    return bits;
+}
+// The clarity gate of one segment (src/lib.rs:1379-1380, key_clarity.rs:51-93), given that both
+// within-mode argmaxes hold (kc_argmax): each mode's top is normalised to exactly 1 and gets the
+// same bonus on both sides, so best = RN(1 + 0.2f) exactly, and every other post-bonus score rs_x
+// moves by at most beta_x = B_x + 2.0001 u (sc_x + rs_x), B_x = (A_x + sc_x A_W) / (R_W - A_W)
+// bounding |R'_x / R'_W - R_x / R_W| (A_x = V_x (1 + 2u) + N_x).  The sum over the sorted table
+// (whose order may differ) moves by sum beta + 2 * 23 u sum rs, the minimum by max beta, and
+// clarity = (best - avg) / (best - min) by the returned bound.  beta_x is written per key.
+__device__ __noinline__ double kc_clarity(const float* raw, const float* SS, const float* V, double sf, double K, const float* sorted,
+                             const int* order, float* beta, int* bits) {
+    auto Ax = [&](int x) { return V[x] * sf * (1.0 + 2.0001 * KC_U) + kc_noise(raw[x], SS[x] * sf, K); };
+    int Wm[2];
+    double AW[2];
+    for (int m = 0; m < 2; m++) {
+        int W = 0;
+        for (int k = 1; k < 12; k++)
+            if (!(raw[12 * m + k] < raw[12 * m + W])) W = k;
+        Wm[m] = 12 * m + W;
+        AW[m] = Ax(Wm[m]);
+        // the normalisation guard (max > 1e-9, detector.rs:165) with the common factor's range is
+        // checked by the caller; here an unnormalised table is simply not certified
+        if (!(raw[Wm[m]] > 1e-9f) || !((double)raw[Wm[m]] - AW[m] > 0.0)) {
+            *bits |= KV_NEAR_RANGE;
+            return 1.0;
+        }
+    }
+    double sb = 0.0, bmax = 0.0;
+    for (int i = 0; i < 24; i++) {
+        const int x = order[i];
+        const int W = Wm[x / 12];
+        double b = 0.0;
+        if (x != W) {
+            const double M = raw[W], sc = (double)raw[x] / M, aw = AW[x / 12];
+            b = (Ax(x) + sc * aw) / (M - aw) + 2.0001 * KC_U * (sc + (double)sorted[i]);
+        }
+        beta[x] = kc_up(b);
+        sb += b;
+        bmax = b > bmax ? b : bmax;
+    }
+    double srs = 0.0, mn = sorted[0];
+    for (int i = 0; i < 24; i++) {
+        srs += (double)sorted[i];
+        mn = (double)sorted[i] < mn ? (double)sorted[i] : mn;
+    }
+    const double best = sorted[0], range = best - mn, avg = srs / 24.0, num = best - avg;
+    const double dsum = sb + 2.0 * 23.0 * KC_U * srs * 1.01;
+    const double davg = dsum / 24.0 + 2.0 * KC_U * __builtin_fabs(avg) * 1.01;
+    const double dnum = davg + 2.0 * KC_U * __builtin_fabs(num) * 1.01;
+    const double drange = bmax + 2.0 * KC_U * range * 1.01;
+    if (!(range - drange > 1e-6)) {
+        *bits |= KV_NEAR_RANGE;
+        return 1.0;
+    }
+    const double cl0 = __builtin_fabs(num / range);
+    return (dnum + cl0 * drange) / (range - drange) + 2.0 * KC_U * cl0 * 1.01 + 1e-15;
+}
 
 // threads per track in k_key_vote.  1024 halves the kernel's serial time (its frame loops are
 // latency-bound) but triples it in the two-stream pipeline (16.9 vs 5.5 ms per launch): a
@@ -799,12 +954,13 @@ constexpr int KV_MAXSCALE = 8;
 #ifndef KV_THREADS
 #define KV_THREADS 256
 #endif
-__global__ __launch_bounds__(KV_THREADS) void k_key_vote(const int* __restrict__ tracks, int n_items,
+__global__ __launch_bounds__(KV_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_key_vote(const int* __restrict__ tracks, int n_items,
                                                   const uint64_t* __restrict__ frame_pfx, float* __restrict__ chroma_raw,
                                                   const float* __restrict__ energy, float* __restrict__ chroma_s,
                                                   float* __restrict__ weights, float* __restrict__ seg_scratch,
                                                   const uint64_t* __restrict__ seg_off, const float* __restrict__ tmpl,
-                                                  KeyParams P, KeyOut* __restrict__ out, KeyDbg* __restrict__ dbg) {
+                                                  KeyParams P, KeyOut* __restrict__ out, KeyDbg* __restrict__ dbg,
+                                                  const float* __restrict__ edel, float* __restrict__ wdel) {
     __shared__ int hist[256];
     __shared__ int misc[4];
     __shared__ int redi[KV_THREADS / 64];
@@ -814,13 +970,28 @@ __global__ __launch_bounds__(KV_THREADS) void k_key_vote(const int* __restrict__
     __shared__ float tpl[48][12];
     __shared__ int sc_len[KV_MAXSCALE], sc_pfx[KV_MAXSCALE + 1];
     __shared__ float sc_w[KV_MAXSCALE];
+    // the certificate (cert): argmax pairs for the pair pass, the slice's largest energy bound and
+    // eta, per-key vote bounds, the full slice's partial-sum totals and sensitivities
+    __shared__ KcCand kc_list[KC_CAP];
+    __shared__ int kc_n;
+    __shared__ unsigned int kc_dmax, kc_emax;
+    __shared__ float kc_pa[24], kc_ss[24], kc_v[24];
+    __shared__ int kc_w;
+    __shared__ double kc_red[KV_THREADS / 64];
+    __shared__ float kc_crs;  // the common factor's relative range (the median's), for absolute thresholds
+    const bool cert = P.near_check && !P.cert_fixed && edel && wdel;
     const int it = blockIdx.x;
     const int trk = tracks[it];
     const int64_t F_all = (int64_t)(frame_pfx[trk + 1] - frame_pfx[trk]);
     const uint64_t g0 = frame_pfx[trk];
     float* cr = chroma_raw + g0 * 12;
     for (int k = threadIdx.x; k < 576; k += blockDim.x) tpl[k / 12][k % 12] = tmpl[k];
-    if (threadIdx.x == 0) near_s = 0;  // published by the barriers below before any reader
+    if (threadIdx.x == 0) {  // published by the barriers below before any reader
+        near_s = 0;
+        kc_n = 0;
+        kc_dmax = 0u;
+        kc_emax = 0u;
+    }
     if (F_all <= 0) {
         if (threadIdx.x == 0) out[trk] = KeyOut{0, 0, 0.0f, 0.0f, 0, 0, 0, 0};
         return;
@@ -908,6 +1079,8 @@ __global__ __launch_bounds__(KV_THREADS) void k_key_vote(const int* __restrict__
     const float* cs = cs_all + t0 * 12;
     const float* en = energy + g0 + t0;
     float* w = weights + g0 + t0;
+    const float* ed = cert ? edel + g0 + t0 : nullptr;
+    float* wd = cert ? wdel + g0 + t0 : nullptr;
     // frame weights over the slice (src/lib.rs:1236-1287)
     if (P.weighting) {
         const float med = sd_maxf(block_select_kth(en, (int)F, (int)(F / 2), hist, misc), 1e-12f);
@@ -933,6 +1106,17 @@ __global__ __launch_bounds__(KV_THREADS) void k_key_vote(const int* __restrict__
             const float ww = sd_maxf(wt * we, 0.0f);
             w[f] = ww;
             used_local += ww > 0.0f;
+            if (cert) {  // eta_f w_f, and the range the certificate assumes
+                const double d = ed[f];
+                const double eta = d < 0.25 ? kc_eta(d, sd_maxf(P.energy_pow, 0.0f)) : 1.0;
+                wd[f] = ww > 0.0f ? kc_up(eta * (double)ww) : 0.0f;
+                // an energy whose quotient or weight could underflow on one side only, or no bound
+                if (!(d < 0.25) || (en[f] > 0.0f && !(e_norm >= 0x1p-100f) && we != 1.0f) ||
+                    (ww > 0.0f && !(ww >= 0x1p-100f)) || !(ww < 0x1p100f))
+                    atomicOr(&near_s, KV_NEAR_RANGE);
+                atomicMax(&kc_dmax, __float_as_uint((float)d));
+                atomicMax(&kc_emax, __float_as_uint(kc_up(eta)));
+            }
         }
         const int used = block_sum_i(used_local, redi);
         __syncthreads();
@@ -940,8 +1124,17 @@ __global__ __launch_bounds__(KV_THREADS) void k_key_vote(const int* __restrict__
         const float sw = block_seq_sum(w, F, sbuf);  // weights.iter().sum(), in order
         if (threadIdx.x == 0) {
             use_w_s = !(sw <= 1e-12f || used < 10);
-            // the unweighted fallback (src/lib.rs:1278-1285) is decided by a sum of energy-derived weights
-            if (P.near_check && sd_absf(sw - 1e-12f) <= KV_NEAR_REL * 1e-12f) atomicOr(&near_s, KV_NEAR_WSUM);
+            // the unweighted fallback (src/lib.rs:1278-1285) is decided by a sum of energy-derived weights:
+            // sw' = c sw (1 +- eta_max) +- both folds' roundings, c in [(1 + d_max)^-p, (1 - d_max)^-p]
+            float mrel = KV_NEAR_REL;
+            if (cert) {
+                const double dm = __uint_as_float(kc_dmax), em = __uint_as_float(kc_emax);
+                const double L = sd_maxf(P.energy_pow, 0.0f) * dm / (1.0 - dm);
+                const double cr = (L < 0.5 ? L / (1.0 - L) : 1.0);
+                kc_crs = kc_up(cr);
+                mrel = sd_maxf(mrel, kc_up(((1.0 + cr) * (1.0 + em) * (1.0 + 3.0 * (double)F * KC_U) - 1.0) * 1.01));
+            }
+            if (P.near_check && sd_absf(sw - 1e-12f) <= mrel * 1e-12f) atomicOr(&near_s, KV_NEAR_WSUM);
         }
     } else if (threadIdx.x == 0) {
         use_w_s = 0;
@@ -1007,6 +1200,81 @@ __global__ __launch_bounds__(KV_THREADS) void k_key_vote(const int* __restrict__
         }
         return a;
     };
+    // weighted_sum_dot with the certificate's companions: *ss = the sum of the fold's partial sums,
+    // *vv = sum_f eta_f w_f D_f (f32 sums of non-negative terms; the readers inflate them by (n + 1) u)
+    auto wsd3 = [&](int64_t f0, int64_t n, int row, float* ss, float* vv) {
+        float a = 0.0f, sa = 0.0f, v = 0.0f;
+        const float* t = tpl[row];
+        float tr[12];
+#pragma unroll
+        for (int k = 0; k < 12; k++) tr[k] = t[k];
+#pragma unroll 4
+        for (int64_t f = f0; f < f0 + n; f++) {
+            const float* c = cs + f * 12;
+            float d = 0.0f;
+#pragma unroll
+            for (int k = 0; k < 12; k++) d += c[k] * tr[k];
+            const float wt = w[f];
+            a += wt > 0.0f ? wt * d : 0.0f;
+            sa += a;
+            v = __builtin_fmaf(wd[f], d, v);
+        }
+        *ss = sa;
+        *vv = v;
+        return a;
+    };
+    // the certificate's inflation of those f32 sums, and K (kc_noise) for a table of n frames
+    auto kc_sf = [](int64_t n) { return 1.0 + 1.0001 * (double)(n + 1) * KC_U; };
+    auto kc_K = [&](int64_t n) { return (1.0 + (double)__uint_as_float(kc_emax)) * (1.0 + 3.0 * (double)n * KC_U); };
+    // the pair pass (kc_argmax's queue): E_Wk = sum_f eta_f w_f |D_fW - D_fk| over the pair's frames
+    // by the whole workgroup, in double; a pair is certified when E_Wk (1 + 1e-6) < its slack
+    auto kc_pair_pass = [&]() {
+        __syncthreads();
+        const int nc = kc_n < KC_CAP ? kc_n : KC_CAP;
+        for (int q = 0; q < nc; q++) {
+            const KcCand cd = kc_list[q];
+            const float* tW = tpl[toff + cd.w];
+            const float* tK = tpl[toff + cd.k];
+            double e = 0.0;
+            for (int64_t f = cd.st + threadIdx.x; f < cd.st + cd.len; f += blockDim.x) {
+                const float wf = wd[f];
+                if (!(wf > 0.0f)) continue;
+                const float* c = cs + f * 12;
+                float dW = 0.0f, dK = 0.0f;
+#pragma unroll
+                for (int k = 0; k < 12; k++) dW += c[k] * tW[k];
+#pragma unroll
+                for (int k = 0; k < 12; k++) dK += c[k] * tK[k];
+                e += (double)wf * __builtin_fabs((double)dW - (double)dK);
+            }
+            for (int o = 32; o > 0; o >>= 1) e += __shfl_xor(e, o, 64);
+            if ((threadIdx.x & 63) == 0) kc_red[threadIdx.x >> 6] = e;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                double tot = 0.0;
+                for (int r = 0; r < (int)(blockDim.x >> 6); r++) tot += kc_red[r];
+                if (!(tot * (1.0 + 1e-6) < (double)cd.slack)) atomicOr(&near_s, KV_NEAR_ARGMAX);
+            }
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) kc_n = 0;
+        __syncthreads();
+    };
+    // the normalisation guard (max > 1e-9, detector.rs:165) under the common factor: the reference's
+    // mode top lies in [(R_W - A_W) / (1 + cr), (R_W + A_W)(1 + cr)]
+    auto kc_guard = [&](const float* raw, const float* SS, const float* V, double sf, double K) {
+        int bits = 0;
+        for (int m = 0; m < 2; m++) {
+            int W = 0;
+            for (int k = 1; k < 12; k++)
+                if (!(raw[12 * m + k] < raw[12 * m + W])) W = k;
+            const double R = raw[12 * m + W];
+            const double A = V[12 * m + W] * sf * (1.0 + 2.0001 * KC_U) + kc_noise(R, SS[12 * m + W] * sf, K);
+            const double cr = kc_crs, t = (double)1e-9f, lo = (R - A) / (1.0 + cr), hi = (R + A) * (1.0 + cr);
+            if (!(lo > t) && !(hi <= t)) bits |= KV_NEAR_RANGE;
+        }
+        return bits;
+    };
     // the heuristic's weighted chroma sums (detector.rs:344-368): i < 12 -> avg[i], 12 -> wsum
     auto avg_sum = [&](int64_t f0, int64_t n, int i) {
         if (!use_w && i == 12) return (float)n;
@@ -1036,9 +1304,22 @@ __global__ __launch_bounds__(KV_THREADS) void k_key_vote(const int* __restrict__
     // full-slice detection: detect_key_weighted (+ the mode heuristic)
     auto detect_full = [&](int used_segments) {
         __syncthreads();
-        if (threadIdx.x < 24) acc[threadIdx.x] = wsd(0, F, toff + threadIdx.x);
+        const bool kc = cert && use_w;  // without weights nothing depends on the energies
+        if (threadIdx.x < 24)
+            acc[threadIdx.x] = kc ? wsd3(0, F, toff + threadIdx.x, &kc_ss[threadIdx.x], &kc_v[threadIdx.x])
+                                  : wsd(0, F, toff + threadIdx.x);
         if (P.mh_on && threadIdx.x >= 24 && threadIdx.x < 37) acc[threadIdx.x] = avg_sum(0, F, threadIdx.x - 24);
         __syncthreads();
+        if (kc) {  // the slice's within-mode argmaxes (its final key and confidence are structural)
+            if (threadIdx.x == 0) {
+                float raw[24];
+                for (int k = 0; k < 24; k++) raw[k] = acc[k];
+                const int b = kc_argmax(raw, kc_ss, kc_v, kc_sf(F), kc_K(F), 0, (int)F, kc_list, &kc_n) |
+                              kc_guard(raw, kc_ss, kc_v, kc_sf(F), kc_K(F));
+                if (b) atomicOr(&near_s, b);
+            }
+            kc_pair_pass();
+        }
         if (threadIdx.x == 0) {
             float raw[24], sorted[24];
             int order[24];
@@ -1112,12 +1393,17 @@ __global__ __launch_bounds__(KV_THREADS) void k_key_vote(const int* __restrict__
         *sw = sc_w[si];
     };
     float* S = seg_scratch + seg_off[it];
+    const bool kc2 = cert && use_w && mode == 2;  // segment voting under the certificate
     for (int q = threadIdx.x; q < nseg * 24; q += blockDim.x) {
         int64_t st;
         int len;
         float sw;
         seg_of(q / 24, &st, &len, &sw);
-        S[(size_t)(q / 24) * KV_ROW + q % 24] = wsd(st, len, toff + q % 24);  // raw score
+        float* row = S + (size_t)(q / 24) * KV_ROW;
+        if (kc2)
+            row[q % 24] = wsd3(st, len, toff + q % 24, &row[64 + q % 24], &row[88 + q % 24]);
+        else
+            row[q % 24] = wsd(st, len, toff + q % 24);  // raw score
     }
     if (P.mh_on)
         for (int q = threadIdx.x; q < nseg * 13; q += blockDim.x) {
@@ -1135,17 +1421,31 @@ __global__ __launch_bounds__(KV_THREADS) void k_key_vote(const int* __restrict__
         int order[24];
         for (int k = 0; k < 24; k++) raw[k] = row[k];
         if (P.near_check && key_raw_near(raw)) atomicOr(&near_s, KV_NEAR_ARGMAX);
+        int64_t st;
+        int len;
+        float sw;
+        seg_of(sg, &st, &len, &sw);
+        if (kc2) {
+            const int b = kc_argmax(raw, row + 64, row + 88, kc_sf(len), kc_K(len), st, len, kc_list, &kc_n) |
+                          kc_guard(raw, row + 64, row + 88, kc_sf(len), kc_K(len));
+            if (b) atomicOr(&near_s, b);
+        }
         key_from_raw(raw, sorted, order);
         if (P.mh_on) {
             int key;
             float conf;
             mode_heuristic(sorted, order, row + 52, row[51], P, &key, &conf);
         }
-        int64_t st;
-        int len;
-        float sw;
-        seg_of(sg, &st, &len, &sw);
         const float cl = clarity_of(sorted);
+        float kc_dcl = 0.0f;
+        if (kc2) {  // the clarity bound; the per-key score bounds replace the partial-sum totals
+            float beta[24];
+            int b = 0;
+            kc_dcl = kc_up(kc_clarity(raw, row + 64, row + 88, kc_sf(len), kc_K(len), sorted, order, beta, &b));
+            if (b) atomicOr(&near_s, b);
+            for (int k = 0; k < 24; k++) row[64 + k] = beta[k];
+            row[112] = kc_dcl;
+        }
         for (int k = 0; k < 24; k++) {
             row[k] = sorted[k];
             row[24 + k] = (float)order[k];
@@ -1153,23 +1453,28 @@ __global__ __launch_bounds__(KV_THREADS) void k_key_vote(const int* __restrict__
         row[48] = cl;
         const float gate = mode == 1 ? P.ms_min_cl : P.min_clarity;
         row[49] = cl >= gate ? 1.0f : 0.0f;
-        if (P.near_check && sd_absf(cl - gate) <= KV_NEAR_CLARITY) atomicOr(&near_s, KV_NEAR_GATE);  // the segment gate (src/lib.rs:1380)
+        if (P.near_check && sd_absf(cl - gate) <= sd_maxf(KV_NEAR_CLARITY, kc_dcl))
+            atomicOr(&near_s, KV_NEAR_GATE);  // the segment gate (src/lib.rs:1380)
         row[50] = cl * sw;
     }
     __syncthreads();
+    if (kc2) kc_pair_pass();
     if (threadIdx.x < 24) {
         const int key = threadIdx.x;
         float a = 0.0f;
+        double pa = 0.0;  // the certificate: the sum of the fold's partial sums
         for (int sg = 0; sg < nseg; sg++) {
             const float* row = S + (size_t)sg * KV_ROW;
             if (row[49] == 0.0f) continue;
             for (int k = 0; k < 24; k++)
                 if ((int)row[24 + k] == key) {
                     a += row[k] * row[50];
+                    pa += (double)a;
                     break;
                 }
         }
         acc[key] = a;
+        if (kc2) kc_pa[key] = kc_up(pa);
     }
     if (threadIdx.x == 32) {
         int u = 0;
@@ -1188,6 +1493,45 @@ __global__ __launch_bounds__(KV_THREADS) void k_key_vote(const int* __restrict__
     if (used == 0 || (mode == 1 && totw <= 1e-12f)) {
         detect_full(used);
         return;
+    }
+    // the certificate's final key (src/lib.rs:1412-1424): acc_x = sum over the used segments of
+    // RN(rs_x cl), so for the leader W and a competitor k the reference's difference moves by at most
+    // sum (|rs_W - rs_k| dcl + (beta_W + beta_k)(cl + dcl))(1 + 4u) + 2.0001 u (rs_W + rs_k) cl (the
+    // products) + 2.0001 u 1.01 (its partial sums): the segment clarity's error enters scaled by the
+    // pair's score difference, not by the scores
+    if (kc2) {
+        if (threadIdx.x == 0) {
+            float sorted[24], conf;
+            int order[24];
+            from_table(acc, sorted, order, &conf);
+            kc_w = order[0];
+        }
+        __syncthreads();
+        const int W = kc_w, k = threadIdx.x;
+        if (k < 24 && k != W) {
+            double D = 0.0;
+            // a structural tie: in every used segment both keys hold a certified mode top (the same
+            // RN(1 + 0.2f), bound 0), so the reference forms the same products for both and ties too
+            bool tie = true;
+            for (int sg = 0; sg < nseg; sg++) {
+                const float* row = S + (size_t)sg * KV_ROW;
+                if (row[49] == 0.0f) continue;
+                double rW = 0.0, rK = 0.0;
+                for (int j = 0; j < 24; j++) {
+                    const int o = (int)row[24 + j];
+                    rW = o == W ? (double)row[j] : rW;
+                    rK = o == k ? (double)row[j] : rK;
+                }
+                const double cw = row[50], dc = row[112], bw = row[64 + W], bk = row[64 + k];
+                tie = tie && rW == rK && bw == 0.0 && bk == 0.0;
+                D += (__builtin_fabs(rW - rK) * dc + (bw + bk) * (cw + dc)) * (1.0 + 4.0001 * KC_U) +
+                     2.0001 * KC_U * (rW + rK) * cw;
+            }
+            D += 2.0001 * KC_U * 1.01 * ((double)kc_pa[W] + (double)kc_pa[k]);
+            if (!tie && !((double)acc[W] - (double)acc[k] > D + 1.01 * KC_U * (double)acc[W]))
+                atomicOr(&near_s, KV_NEAR_FINAL);
+        }
+        __syncthreads();
     }
     if (threadIdx.x == 0) {
         float tab[24], sorted[24];
@@ -1238,13 +1582,13 @@ void launch_mask_band(float* mags, int stride, int B, const uint64_t* frame_pfx,
 }
 void launch_hpcp_band(const float* mags, const uint64_t* frame_pfx, const uint64_t* tile_pfx, const int* tracks,
                       int n_items, uint64_t n_tiles, const HpcpParams& P, const HarmEntry* harm, const float* part,
-                      uint64_t total, float* chroma, float* energy, hipStream_t st) {
+                      uint64_t total, float* chroma, float* energy, float* edel, hipStream_t st) {
     if (n_tiles == 0) return;
     const int nblk = (P.B + MASK_T - 1) / MASK_T;
     const dim3 grid((unsigned)n_tiles), block(HP_FRAMES);
 #define SDSP_HB(K)                                                                                                   \
     hipLaunchKernelGGL(k_hpcp_band<K>, grid, block, 0, st, mags, frame_pfx, tile_pfx, tracks, n_items, P, harm, part, \
-                       nblk, total, chroma, energy)
+                       nblk, total, chroma, energy, edel)
     if (P.K <= 8)
         SDSP_HB(8);
     else if (P.K <= 16)
@@ -1275,10 +1619,11 @@ void launch_hpcp(const float* mags, const uint64_t* frame_pfx, const uint64_t* t
 }
 void launch_key_vote(const int* tracks, int n_items, const uint64_t* frame_pfx, float* chroma_raw,
                      const float* energy, float* chroma_s, float* weights, float* seg_scratch, const uint64_t* seg_off,
-                     const float* tmpl, const KeyParams& P, KeyOut* out, hipStream_t st, KeyDbg* dbg) {
+                     const float* tmpl, const KeyParams& P, KeyOut* out, hipStream_t st, KeyDbg* dbg,
+                     const float* edel, float* wdel) {
     if (n_items == 0) return;
     hipLaunchKernelGGL(k_key_vote, dim3(n_items), dim3(KV_THREADS), 0, st, tracks, n_items, frame_pfx, chroma_raw, energy,
-                       chroma_s, weights, seg_scratch, seg_off, tmpl, P, out, dbg);
+                       chroma_s, weights, seg_scratch, seg_off, tmpl, P, out, dbg, edel, wdel);
 }
 
 }  // namespace sdsp

@@ -176,6 +176,10 @@ struct KeyParams {
     // KeyOut::near whether a discrete decision downstream of the energies is within a margin the
     // re-association could cross, so the host reruns that track with the sequential fold
     int near_check;
+    // near_check margins: 0 the rigorous certificate (the per-frame energy bounds k_hpcp_band
+    // writes, carried through the weights, raw scores, clarities and the vote, with the fixed
+    // round-5 margins below as floors); 1 the fixed margins alone (sdsp_debug_set_key_cert, for A/B)
+    int cert_fixed;
 };
 // near-decision margins (k_key_vote, KeyParams::near_check): a segment clarity within
 // KV_NEAR_CLARITY of its gate, a final (best - second) / best below KV_NEAR_CONF, or a weight sum
@@ -183,8 +187,14 @@ struct KeyParams {
 // <= 1e-6 and relative score gaps by <= 1e-6 on every track measured (profiles/r05_key_scale.jsonl),
 // so the margins hold a factor of 100.
 constexpr float KV_NEAR_CLARITY = 1e-4f, KV_NEAR_CONF = 1e-4f, KV_NEAR_REL = 1e-3f;
+// k_key_vote's segment scratch row (floats): 24 sorted, 24 order, clarity, used, cw, wsum, avg[12];
+// then the certificate's per-key partial-sum totals [64, 88) and energy sensitivities [88, 112)
+// (the clarity stage replaces [64, 88) by the post-bonus score bounds), [112] the clarity bound
+constexpr int KV_ROW = 128;
 // KeyOut::near bits: which decision was within its margin
 constexpr int KV_NEAR_ARGMAX = 1, KV_NEAR_GATE = 2, KV_NEAR_FINAL = 4, KV_NEAR_WSUM = 8;
+// (16: a frame weight or energy outside the certificate's range: underflow, or no usable bound)
+constexpr int KV_NEAR_RANGE = 16;
 struct KeyOut {
     int mode, tonic;
     float conf, clarity;
@@ -353,13 +363,14 @@ void launch_mask_band(float* mags, int stride, int B, const uint64_t* frame_pfx,
                       float power, int st_lo, int st_hi, float* part, uint64_t total, hipStream_t st);
 void launch_hpcp_band(const float* mags, const uint64_t* frame_pfx, const uint64_t* tile_pfx, const int* tracks,
                       int n_items, uint64_t n_tiles, const HpcpParams& P, const HarmEntry* harm, const float* part,
-                      uint64_t total, float* chroma, float* energy, hipStream_t st);
+                      uint64_t total, float* chroma, float* energy, float* edel, hipStream_t st);
 void launch_hpcp(const float* mags, const uint64_t* frame_pfx, const uint64_t* tile_pfx, const int* tracks,
                  int n_items, uint64_t n_tiles, const HpcpParams& P, const HarmEntry* harm, float* chroma,
                  float* energy, hipStream_t st);
 void launch_key_vote(const int* tracks, int n_items, const uint64_t* frame_pfx, float* chroma_raw,
                      const float* energy, float* chroma_s, float* weights, float* seg_scratch, const uint64_t* seg_off,
-                     const float* tmpl, const KeyParams& P, KeyOut* out, hipStream_t st, KeyDbg* dbg = nullptr);
+                     const float* tmpl, const KeyParams& P, KeyOut* out, hipStream_t st, KeyDbg* dbg = nullptr,
+                     const float* edel = nullptr, float* wdel = nullptr);
 void launch_synth(float* out, uint64_t n_tracks, uint64_t len, uint32_t sr, const float* bpm, const int* key,
                   uint64_t seed0, hipStream_t st);
 void launch_synth_normalize(float* out, uint64_t n_tracks, uint64_t len, unsigned int* peak_bits, hipStream_t st);

@@ -1485,7 +1485,11 @@ void Pipeline::rerun_near(const float* d_samples, const std::vector<uint64_t>& i
     px.run(d_samples, o2, l2, r2);
     for (size_t j = 0; j < near.size(); j++) {
         TrackRes& r = res[near[j]];
-        if (r2[j].status != SDSP_OK) continue;
+        if (r2[j].status != SDSP_OK) {  // the key fields are not certified: the track fails
+            r.status = SDSP_ERR_PROCESSING;
+            r.err = "Processing error: key certification rerun failed (" + r2[j].err + ")";
+            continue;
+        }
         r.key_mode = r2[j].key_mode;
         r.key_tonic = r2[j].key_tonic;
         r.key_conf = r2[j].key_conf;
@@ -1660,7 +1664,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         K.push_back(i);
         kpfx.push_back(kpfx.back() + F8);
         ktile.push_back(ktile.back() + (F8 + HP_FRAMES - 1) / HP_FRAMES);
-        kseg.push_back(kseg.back() + 64 * seg_rows(F8));
+        kseg.push_back(kseg.back() + (uint64_t)KV_ROW * seg_rows(F8));
         ksrc.push_back(bin.src_off[(size_t)i]);
         kgain.push_back(bin.gain_h[(size_t)i]);
         key_in_bytes += 4.0 * (double)n;
@@ -1773,6 +1777,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         }
         float* d_chroma = c_.dev<float>("E.chroma", total8 * 12);
         float* d_energy = c_.dev<float>("E.energy", total8);
+        float* d_edel = nullptr;  // the band path's per-frame energy bounds (the vote's certificate)
         // the previous sub-batch's key vote (stream3) reads E.chroma / E.energy: the producers
         // below wait for it (an event never recorded counts as complete)
         // (a nested rerun has its own "X." buffers and runs in order on the main stream)
@@ -1790,9 +1795,11 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
             // the table upload is queued on the main stream: order the key stream after it
             kt.mark(10);
             SDSP_HIP_CHECK(hipStreamWaitEvent(st2, kt.ev[10], 0));
-            if (band)
+            if (band) {
+                d_edel = c_.dev<float>("E.edel", total8);
                 launch_hpcp_band(mags8, d_kpfx, d_ktile, d_kid, NK, ktile.back(), hp, d_ht, d_part, total8, d_chroma,
-                                 d_energy, st2);
+                                 d_energy, d_edel, st2);
+            }
             else
                 launch_hpcp(mags8, d_kpfx, d_ktile, d_kid, NK, ktile.back(), hp, d_ht, d_chroma, d_energy, st2);
         } else {  // :1169-1197 (the tuned variant only when |offset| > 1e-6)
@@ -1804,6 +1811,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         key_templates(tpl.data());
         d_tpl = c_.up(EP + "tpl", tpl);
         kp.near_check = band ? 1 : 0;
+        kp.cert_fixed = test_hooks().key_cert_fixed.load();  // sdsp_debug_set_key_cert
         kp.weighting = cfg_.enable_key_frame_weighting;
         kp.min_tonal = cfg_.key_min_tonalness;
         kp.tonal_pow = cfg_.key_tonalness_power;
@@ -1842,7 +1850,9 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         SDSP_HIP_CHECK(hipStreamWaitEvent(st3, kt.ev[8], 0));
         SDSP_HIP_CHECK(hipStreamWaitEvent(st3, kt.ev[11], 0));
         d_kdbg = dbg_on ? c_.dev<KeyDbg>(EP + "kdbg", (size_t)NK) : nullptr;
-        launch_key_vote(d_kid, NK, d_kpfx, d_chroma, d_energy, d_cs, d_w, d_sscr, d_kseg, d_tpl, kp, d_kout, st3, d_kdbg);
+        float* d_wdel = d_edel ? c_.dev<float>("E.wdel", total8) : nullptr;
+        launch_key_vote(d_kid, NK, d_kpfx, d_chroma, d_energy, d_cs, d_w, d_sscr, d_kseg, d_tpl, kp, d_kout, st3, d_kdbg,
+                        d_edel, d_wdel);
         SDSP_HIP_CHECK(hipGetLastError());
         kt.mark(2, st3);
         if (!nested_) SDSP_HIP_CHECK(hipEventRecord(d_.vote_done, st3));
@@ -2561,7 +2571,11 @@ int32_t run_locked(DeviceCtx& d, const float* d_samples, const uint64_t* offsets
             px.run(d_samples, o2, l2, r2);
             for (size_t j = 0; j < near.size(); j++) {
                 TrackRes& r = res[near[j]];
-                if (r2[j].status != SDSP_OK) continue;  // (the same front end as the main pass)
+                if (r2[j].status != SDSP_OK) {  // (the same front end as the main pass) uncertified: fail
+                    r.status = SDSP_ERR_PROCESSING;
+                    r.err = "Processing error: key certification rerun failed (" + r2[j].err + ")";
+                    continue;
+                }
                 r.key_mode = r2[j].key_mode;
                 r.key_tonic = r2[j].key_tonic;
                 r.key_conf = r2[j].key_conf;

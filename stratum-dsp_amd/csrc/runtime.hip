@@ -296,6 +296,11 @@ int32_t sdsp_debug_set_schedule(int32_t serial_streams, int32_t no_key_defer, in
     return SDSP_OK;
 }
 
+int32_t sdsp_debug_set_key_cert(int32_t fixed_margins) {
+    test_hooks().key_cert_fixed.store(fixed_margins != 0);
+    return SDSP_OK;
+}
+
 int32_t sdsp_debug_mem_info(int32_t device, uint64_t* free_bytes, uint64_t* total_bytes) {
     try {
         SDSP_HIP_CHECK(hipSetDevice(device));

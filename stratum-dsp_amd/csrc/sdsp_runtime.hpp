@@ -112,6 +112,8 @@ struct TestHooks {
     // sdsp_analyze_batch chunk size, and the sub-batch HBM budget in GB
     std::atomic<int> serial_streams{0}, no_key_defer{0}, no_row_reuse{0}, host_trace{0};
     std::atomic<uint64_t> batch_chunk_tracks{0};
+    // sdsp_debug_set_key_cert: 1 = the key vote's fixed round-5 near-decision margins alone
+    std::atomic<int> key_cert_fixed{0};
     std::atomic<double> hbm_budget_gb{0.0};
     std::mutex mu;
     std::vector<int> devices;

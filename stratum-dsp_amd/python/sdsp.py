@@ -142,6 +142,21 @@ def test_hooks(fail_chunk=-1, devices=(), stft_frame_parallel=False):
             _lib, _schedule_set = prev, None
 
 
+@contextlib.contextmanager
+def key_cert_fixed():
+    """sdsp_debug_set_key_cert(1) for the duration of the block: the key vote flags near-decision
+    tracks by the fixed round-5 margins alone instead of the rigorous certificate, for
+    comparing the two flagged sets."""
+    f = lib().sdsp_debug_set_key_cert
+    f.argtypes = [C.c_int32]
+    f.restype = C.c_int32
+    assert f(1) == 0
+    try:
+        yield
+    finally:
+        f(0)
+
+
 def last_key_near(n, device=0):
     """sdsp_debug_last_key_near: per track of the last analysis call on `device`, whether its key
     vote was near an energy-dependent decision (and the track was analysed again exactly): 0, or

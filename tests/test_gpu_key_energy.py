@@ -8,6 +8,8 @@ The north star's tolerance (key exact, confidences within 1e-4) is what the key 
 every other field stays bit-identical to the oracle.  The config-2 golden (64 x 3-min) is checked
 the same way in test_gpu_batch_paths.py.
 """
+import concurrent.futures as cf
+
 import numpy as np
 import pytest
 
@@ -74,3 +76,35 @@ def test_near_decision_track_rerun_exact():
     rc, ref = oracle.analyze(buf.to_host(n, n), 44100)
     assert rc == 0
     assert parity.exact_fraction(got[0], ref, strict=True) == 1.0 and not parity.diff_results(got[0], ref)
+
+
+def test_rigorous_certificate_covers_fixed_margins():
+    """The rigorous certificate (per-frame energy bounds from k_hpcp_band carried
+    through the weights, raw scores, clarities and the vote) flags every track the round-5 fixed
+    margins flag (they are its floors), and on this batch of 3-min tracks from the bench's generator
+    every result equals the oracle: key exact, every other field bit-exact, the two energy-weighted
+    fields within the tolerance (flagged tracks bit-exact: they were rerun with the sequential fold)."""
+    n, L = 48, 180 * 44100
+    buf = sdsp.DeviceBuffer(n * L)
+    sdsp.generate_synthetic(buf.ptr, n, L, 44100, seed0=3000)
+    offs, lens = np.arange(n) * L, np.full(n, L)
+    got = sdsp.analyze_batch_device(buf.ptr, offs, lens, 44100)
+    rig = sdsp.last_key_near(n).copy()
+    st = sdsp.stage_times()
+    with sdsp.key_cert_fixed():
+        got_f = sdsp.analyze_batch_device(buf.ptr, offs, lens, 44100)
+        fix = sdsp.last_key_near(n).copy()
+    assert all(rig[i] != 0 for i in range(n) if fix[i] != 0), (rig, fix)
+    assert st["key_reruns"] == int((rig != 0).sum())
+    print(f"rigorous certificate: {int((rig != 0).sum())} of {n} tracks rerun, fixed margins: {int((fix != 0).sum())}")
+    xs = [buf.to_host(int(offs[i]), L) for i in range(n)]
+    with cf.ThreadPoolExecutor(8) as ex:
+        refs = list(ex.map(lambda x: oracle.analyze(x, 44100), xs))
+    for i, (rc, ref) in enumerate(refs):
+        assert rc == 0, i
+        assert got[i]["key"] == ref["key"] and got_f[i]["key"] == ref["key"], i
+        assert not parity.diff_results(got[i], ref), (i, parity.diff_results(got[i], ref))
+        g, e = parity.result_digest(got[i]), parity.result_digest(ref)
+        assert all(g[k] == e[k] for k in g if k not in parity.KEY_ENERGY_FIELDS), i
+        if rig[i]:
+            assert parity.exact_fraction(got[i], ref, strict=True) == 1.0, i

@@ -44,7 +44,7 @@ def run_set(name, n, threads, sr=44100, seconds=180.0):
     st = sdsp.stage_times()
     nb = sdsp.last_key_near(n)
     near = [int(i) for i in np.nonzero(nb)[0]]
-    why = {name: int(((nb & bit) != 0).sum()) for name, bit in (("argmax", 1), ("gate", 2), ("final", 4), ("wsum", 8))}
+    why = {name: int(((nb & bit) != 0).sum()) for name, bit in (("argmax", 1), ("gate", 2), ("final", 4), ("wsum", 8), ("range", 16))}
     out = {"set": name, "tracks": n, "bpm_mode": SETS[name], "seeds": [0, n - 1], "gpu_s": round(gpu_s, 2),
            "gpu_errors": sum(1 for s in res.status if s != 0), "key_equal": 0, "within_tol": 0,
            "bit_exact_except_key_energy": 0, "bit_exact_strict": 0, "max_key_confidence_diff": 0.0,
