@@ -701,11 +701,90 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
                                                        int fs, int hop, float* __restrict__ rms) {
     typedef float f4 __attribute__((ext_vector_type(4)));
     constexpr int RUN = 4 * G;
+    // the wave-cooperative path's staging tile: per wave, 64 lane rows of 8 16-byte blocks, rows
+    // 144 B apart (ds_read_b128 of one block column by 16 lanes then covers all 64 banks)
+    __shared__ f4 tile[4][64][9];
     const uint64_t u0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * RUN;
-    if (u0 >= total) return;
     const uint64_t u1 = u0 + RUN < total ? u0 + RUN : total;
     uint64_t g = u0;
-    int trk = find_track(frame_pfx, T, g);
+    int trk = u0 < total ? find_track(frame_pfx, T, g) : 0;
+    // The wave-cooperative path: when every lane of the wave owns a whole run of RUN frames of one
+    // track, the runs 16-B aligned and their whole sample streams inside the track (every step is
+    // the plain step below), each step's 32 samples per lane come in by 8 loads per wave that each
+    // read the 128-byte segments of 8 lanes (8 cache lines per load instead of 64: a lane's own
+    // 16-B loads of its segment each hit a different line than the other lanes'), through a
+    // per-wave LDS tile.  The folds are the plain step's, so the values are identical.
+    {
+        const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+        bool ok = u0 < total && u1 - u0 == (uint64_t)RUN && u1 <= frame_pfx[trk + 1];
+        uint64_t f0 = 0, a0 = 0, n = 0;
+        if (ok) {
+            f0 = g - frame_pfx[trk];
+            n = n_len[trk];
+            a0 = src_off[trk] + f0 * (uint64_t)hop;
+            ok = (a0 & 3u) == 0 && f0 * (uint64_t)hop + (uint64_t)(RUN + G - 1) * (uint64_t)hop <= n;
+        }
+        const int trk0 = __builtin_amdgcn_readfirstlane(trk);
+        if (__builtin_amdgcn_ballot_w64(!(ok && trk == trk0)) == 0) {
+            const f4* q = reinterpret_cast<const f4*>(x);
+            const uint64_t blkw = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(a0 >> 2)) |
+                                   ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(a0 >> 34)) << 32));
+            const uint64_t bstride = (uint64_t)RUN * (uint64_t)hop / 4;  // blocks between lanes' runs
+            const uint64_t lbase = blkw + (uint64_t)(l >> 3) * bstride + (uint64_t)(l & 7);
+            const float gn = gain[trk];
+            const int nseg = RUN + G - 1, spseg = hop >> 5, steps = nseg * spseg;
+            f4 stg[8];
+            auto issue = [&](int t) {
+#pragma unroll
+                for (int k = 0; k < 8; k++) stg[k] = q[lbase + (uint64_t)(8 * k) * bstride + 8 * (uint64_t)t];
+            };
+            auto wave_sync = [] {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            };
+            float acc[G];
+#pragma unroll
+            for (int r = 0; r < G; r++) acc[r] = 0.0f;
+            issue(0);
+            int t = 0;
+            for (int sg = 0; sg <= nseg; sg++) {
+#pragma unroll
+                for (int r = 0; r < G; r++) {
+                    if (sg % G != r) continue;  // wave-uniform
+                    if (sg >= G) {              // frame sg - G (< RUN) of the run: whole, inside the track
+                        const uint64_t fj = f0 + (uint64_t)(sg - G);
+                        rms[frame_pfx[trk] + fj] = __builtin_sqrtf(acc[r] / (float)fs);
+                    }
+                    acc[r] = 0.0f;
+                }
+                if (sg == nseg) break;
+                for (int c = 0; c < spseg; c++, t++) {
+                    wave_sync();  // the previous step's tile reads are done
+#pragma unroll
+                    for (int k = 0; k < 8; k++) tile[wv][8 * k + (l >> 3)][l & 7] = stg[k];
+                    wave_sync();
+                    f4 cur[8];
+#pragma unroll
+                    for (int e = 0; e < 8; e++) cur[e] = tile[wv][l][e];
+                    if (t + 1 < steps) issue(t + 1);
+#pragma unroll
+                    for (int e = 0; e < 8; e++) {
+                        const float v[4] = {cur[e].x, cur[e].y, cur[e].z, cur[e].w};
+#pragma unroll
+                        for (int w = 0; w < 4; w++) {
+                            const float y = v[w] * gn;
+                            const float yy = y * y;
+#pragma unroll
+                            for (int r = 0; r < G; r++) acc[r] += yy;
+                        }
+                    }
+                }
+            }
+            return;
+        }
+    }
+    if (u0 >= total) return;
     while (g < u1) {  // one piece per track the run touches
         while (g >= frame_pfx[trk + 1]) trk++;
         const uint64_t f0 = g - frame_pfx[trk];
