@@ -954,7 +954,11 @@ __device__ __noinline__ double kc_clarity(const float* raw, const float* SS, con
 #ifndef KV_THREADS
 #define KV_THREADS 256
 #endif
-__global__ __launch_bounds__(KV_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_key_vote(const int* __restrict__ tracks, int n_items,
+#ifndef KV_SMALL_ITEMS
+#define KV_SMALL_ITEMS 96
+#endif
+template <int NT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_key_vote(const int* __restrict__ tracks, int n_items,
                                                   const uint64_t* __restrict__ frame_pfx, float* __restrict__ chroma_raw,
                                                   const float* __restrict__ energy, float* __restrict__ chroma_s,
                                                   float* __restrict__ weights, float* __restrict__ seg_scratch,
@@ -963,7 +967,7 @@ __global__ __launch_bounds__(KV_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
                                                   const float* __restrict__ edel, float* __restrict__ wdel) {
     __shared__ int hist[256];
     __shared__ int misc[4];
-    __shared__ int redi[KV_THREADS / 64];
+    __shared__ int redi[NT / 64];
     __shared__ float acc[48];
     __shared__ int use_w_s, used_s, near_s;
     __shared__ float totw_s;
@@ -977,7 +981,7 @@ __global__ __launch_bounds__(KV_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     __shared__ unsigned int kc_dmax, kc_emax;
     __shared__ float kc_pa[24], kc_ss[24], kc_v[24];
     __shared__ int kc_w;
-    __shared__ double kc_red[KV_THREADS / 64];
+    __shared__ double kc_red[NT / 64];
     __shared__ float kc_crs;  // the common factor's relative range (the median's), for absolute thresholds
     const bool cert = P.near_check && !P.cert_fixed && edel && wdel;
     const int it = blockIdx.x;
@@ -1622,8 +1626,15 @@ void launch_key_vote(const int* tracks, int n_items, const uint64_t* frame_pfx, 
                      const float* tmpl, const KeyParams& P, KeyOut* out, hipStream_t st, KeyDbg* dbg,
                      const float* edel, float* wdel) {
     if (n_items == 0) return;
-    hipLaunchKernelGGL(k_key_vote, dim3(n_items), dim3(KV_THREADS), 0, st, tracks, n_items, frame_pfx, chroma_raw, energy,
-                       chroma_s, weights, seg_scratch, seg_off, tmpl, P, out, dbg, edel, wdel);
+    // a few tracks (the exact reruns of near-decision tracks, one-track calls): the latency of one
+    // track's workgroup is the launch, and 1024 threads cut it (the segment scores in one round
+    // instead of three); full sub-batches keep 256 threads, which fit beside the key-stream STFT
+    if (n_items <= KV_SMALL_ITEMS)
+        hipLaunchKernelGGL(k_key_vote<1024>, dim3(n_items), dim3(1024), 0, st, tracks, n_items, frame_pfx, chroma_raw,
+                           energy, chroma_s, weights, seg_scratch, seg_off, tmpl, P, out, dbg, edel, wdel);
+    else
+        hipLaunchKernelGGL(k_key_vote<KV_THREADS>, dim3(n_items), dim3(KV_THREADS), 0, st, tracks, n_items, frame_pfx,
+                           chroma_raw, energy, chroma_s, weights, seg_scratch, seg_off, tmpl, P, out, dbg, edel, wdel);
 }
 
 }  // namespace sdsp
