@@ -217,6 +217,9 @@ __global__ __launch_bounds__(MASK_T) __attribute__((amdgpu_waves_per_eu(4, 4))) 
     // the hardware drops their stores without an exec-mask branch per element.
     float* const trk0 = mags + frame_pfx[trk] * (uint64_t)stride;
     const uint32_t lvo = (uint32_t)(live ? b : 0) * 4u;
+    // lanes past the last bin load through an offset past the row resource's range: the hardware
+    // returns 0 without an exec-mask branch per load
+    const uint32_t lvo_z = live ? (uint32_t)b * 4u : 0x80000000u;
     const uint32_t svo = keep ? (uint32_t)b * 4u : 0x80000000u;
     const uint32_t rowb = (uint32_t)stride * 4u;
     auto row_rsrc = [&](int64_t row, uint32_t bytes) {
@@ -247,8 +250,11 @@ __global__ __launch_bounds__(MASK_T) __attribute__((amdgpu_waves_per_eu(4, 4))) 
         const bool bad = ((ab << 1) != 0u) & (ab - 0x12800000u > 0x7B800000u - 0x12800000u);
         if (chk && __builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0))
             if (bad) hm = a / (float)(2 * M + 1);
-        const float x = max0_quiet(xr);
-        const float h = max0_quiet(hm);
+        // the block test (chk = false) also certifies every sample of the block and the ring finite
+        // and >= +0, and then a >= +0 and its correctly rounded quotient hm >= +0: both max(., 0)
+        // are the identity there
+        const float x = chk ? max0_quiet(xr) : xr;
+        const float h = chk ? max0_quiet(hm) : hm;
         const float r = max_bnn(x - h, 0.0f);
         const float hp = mask_pow<PW>(h, p);
         const float rp = mask_pow<PW>(r, p);
@@ -285,8 +291,7 @@ __global__ __launch_bounds__(MASK_T) __attribute__((amdgpu_waves_per_eu(4, 4))) 
         const auto rs = row_rsrc(base, 0x7FFFFFFFu);
         if (base >= 2 * M && base + R <= F) {
 #pragma unroll
-            for (int u = 0; u < R; u++)
-                xv[u] = live ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, lvo, (uint32_t)u * rowb, 2)) : 0.0f;
+            for (int u = 0; u < R; u++) xv[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, lvo_z, (uint32_t)u * rowb, 2));
         } else {
 #pragma unroll
             for (int u = 0; u < R; u++)
@@ -310,14 +315,18 @@ __global__ __launch_bounds__(MASK_T) __attribute__((amdgpu_waves_per_eu(4, 4))) 
             // covers the block's samples and the raw ring (the centres x of the block's first
             // elements are the previous block's).  A block and past of zeros is exact on either
             // path.  NaN and inf fail the tests.
-            float mx = xv[0];
+            // max(x) over the block and the ring as unsigned bit patterns: for values with a clear
+            // sign bit that is the float maximum, and a NaN, an infinity or a negative value (sign bit)
+            // makes it >= 0x7F800000, so the test below also certifies every value finite and >= +0
+            uint32_t mb = __float_as_uint(xv[0]);
 #pragma unroll
-            for (int u = 1; u < R; u++) mx = __builtin_fmaxf(mx, xv[u]);
+            for (int u = 1; u < R; u++) mb = max(mb, __float_as_uint(xv[u]));
 #pragma unroll
-            for (int j = 0; j < RX; j++) mx = __builtin_fmaxf(mx, X[j]);
+            for (int j = 0; j < RX; j++) mb = max(mb, __float_as_uint(X[j]));
+            const float mx = __uint_as_float(mb);
             const float pf = prev + xv[0];
-            const bool ok = prev + mx == 0.0f ||
-                            (pf >= 0x1p-21f && pf >= mx * 0x1p-31f && prev + (float)R * mx <= 0x1p60f);
+            const bool ok = mb < 0x7F800000u && (prev + mx == 0.0f || (pf >= 0x1p-21f && pf >= mx * 0x1p-31f &&
+                                                                        prev + (float)R * mx <= 0x1p60f));
             if (__builtin_expect(__builtin_amdgcn_ballot_w64(!ok) == 0, 1)) {
 #pragma unroll
                 for (int u = 0; u < R; u++) {
