@@ -287,9 +287,13 @@ __global__ __launch_bounds__(FT_FRAMES) __attribute__((amdgpu_waves_per_eu(KK > 
                 const float so_start = so;
                 // MEL: the chunk's mel plans come in one scalar load; a flush stores accA through a
                 // buffer resource whose record count drops the stores of lanes without a frame
-                auto walk = [&](auto mel_tag, auto reg_tag) {
+                // NOBAND: a chunk outside every sub-band (vbc = 0: most of the bins above the high
+                // band's edge), whose walk drops the sub-band folds instead of computing and
+                // discarding them (-0.7 % per launch, profiles/r06_kernel_ab_features_noband.txt)
+                auto walk = [&](auto mel_tag, auto reg_tag, auto noband_tag) {
                     constexpr bool MEL = decltype(mel_tag)::value;
                     constexpr bool REG = decltype(reg_tag)::value;
+                    constexpr bool NOBAND = decltype(noband_tag)::value;
                     MelChunk mc{};
                     const ConstMC mcp = (ConstMC)P.mel_chunks + c0 / CW;
                     if constexpr (MEL) {
@@ -320,7 +324,7 @@ __global__ __launch_bounds__(FT_FRAMES) __attribute__((amdgpu_waves_per_eu(KK > 
                         const float df = max_bnn(lc - Wm[j], 0.0f);
                         const float df2 = df * df;
                         sx[0] += df2;
-                        if (vbc) {
+                        if (!NOBAND && vbc) {
                             eb += ee;
                             hb += hh;
                             sb += df2;
@@ -352,11 +356,13 @@ __global__ __launch_bounds__(FT_FRAMES) __attribute__((amdgpu_waves_per_eu(KK > 
                     }
                 };
                 if (cf & FT_CHUNK_MELREG)
-                    walk(std::true_type{}, std::true_type{});
+                    walk(std::true_type{}, std::true_type{}, std::false_type{});
                 else if (cf & FT_CHUNK_MEL)
-                    walk(std::true_type{}, std::false_type{});
+                    walk(std::true_type{}, std::false_type{}, std::false_type{});
+                else if (vbc == 0)
+                    walk(std::false_type{}, std::false_type{}, std::true_type{});
                 else
-                    walk(std::false_type{}, std::false_type{});
+                    walk(std::false_type{}, std::false_type{}, std::false_type{});
                 quot_redo(c0, CW, so_start);
                 continue;
             }
