@@ -188,11 +188,18 @@ __global__ __launch_bounds__(MASK_T) void k_mask_r(float* __restrict__ mags, int
 // peak band [st_lo, st_hi] (extractor.rs:583-671: peaks in [pk_lo, pk_hi] and their neighbours)
 // and otherwise only folds the frame energy sum(x * x) over every bin (extractor.rs:1133).  The
 // masked value is stored only on that band; for every frame the workgroup's 64 bins (block g) fold
-// their squares in bin order into part[g][frame] (an LDS tile: lane = bin writes, then lane u folds
-// the row of frame base + u - M), and HPCP folds the 65 block sums in block order.  Only that fold's
-// association differs from the reference's one sequential sum over 4,097 bins (a GPU-only
-// re-association of the key energies); every masked value is bit-identical.
+// their squares into part[g][frame] (an LDS tile: lane = bin writes, then lanes u and u + 32 fold the
+// two 32-bin halves of the row of frame base + u - M in bin order and the halves are added), and
+// HPCP folds the 65 block sums in block order.  Only that fold's association differs from the
+// reference's one sequential sum over 4,097 bins (a GPU-only re-association of the key energies,
+// DESIGN.md §2); every masked value is bit-identical.
 // Lanes past the last bin stay in the wave and contribute +0 (exact: the sums are >= +0).
+// the block fold's chains: 1 = lane u folds the 64 squares of frame u alone; 2 (default) = lanes u
+// and u + 32 fold 32 each and add the halves (-1.8 % per launch, profiles/r06_kernel_ab_mask_fold.txt;
+// 4 = two interleaved chains of 16 per lane, -0.8 %)
+#ifndef SDSP_MASK_FOLD_CH
+#define SDSP_MASK_FOLD_CH 2
+#endif
 template <int M, int PW>
 __global__ __launch_bounds__(MASK_T) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_mask_rp(float* __restrict__ mags, int stride, int B,
                                                      const uint64_t* __restrict__ frame_pfx,
@@ -273,6 +280,7 @@ __global__ __launch_bounds__(MASK_T) __attribute__((amdgpu_waves_per_eu(4, 4))) 
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#if SDSP_MASK_FOLD_CH == 1
         const int64_t t = base + lane - M;
         if (lane < R && t >= 0 && t < F) {
             float sum = 0.0f;
@@ -280,6 +288,29 @@ __global__ __launch_bounds__(MASK_T) __attribute__((amdgpu_waves_per_eu(4, 4))) 
             for (int j = 0; j < MASK_T; j++) sum += tile[lane][j];
             pg[t] = sum;
         }
+#else
+        {
+            // two lanes per frame (u, u + 32), each folding half of the block's bins in bin order
+            // (SDSP_MASK_FOLD_CH / 2 interleaved chains each), the halves added at the end
+            constexpr int NCH = SDSP_MASK_FOLD_CH / 2, CL = MASK_T / 2 / NCH;
+            const int fu = lane & 31, hf = lane >> 5;
+            const int64_t t = base + fu - M;
+            float sc[NCH];
+#pragma unroll
+            for (int c = 0; c < NCH; c++) sc[c] = 0.0f;
+            if (fu < R) {
+#pragma unroll
+                for (int j = 0; j < CL; j++)
+#pragma unroll
+                    for (int c = 0; c < NCH; c++) sc[c] += tile[fu][hf * (MASK_T / 2) + c * CL + j];
+            }
+            float sum = sc[0];
+#pragma unroll
+            for (int c = 1; c < NCH; c++) sum += sc[c];
+            const float hi = __shfl_down(sum, 32);
+            if (hf == 0 && fu < R && t >= 0 && t < F) pg[t] = sum + hi;
+        }
+#endif
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -520,8 +551,10 @@ __global__ __launch_bounds__(HP_FRAMES) SDSP_HPCP_ATTR void k_hpcp(const float* 
 }
 
 // A rigorous bound on |e_blk - e_ref| / e_blk for one frame ("Certification"): e_blk
-// is this engine's fold of the 65 block sums Bt_b (each the sequential f32 fold of its 64 squares
-// t_k = RN(x_k^2) from 0, k_mask_rp), e_ref the reference's one sequential f32 fold of the same
+// is this engine's fold of the 65 block sums Bt_b (each an f32 fold of its 64 squares
+// t_k = RN(x_k^2) from 0, k_mask_rp: two sequential halves of 32, then their sum; the g63 bound
+// below holds for any association of 64 non-negative terms, since no term passes through more than
+// 63 roundings), e_ref the reference's one sequential f32 fold of the same
 // 4,097 squares (extractor.rs:1133).  With u = 2^-24, T = sum t_k (exact), B_b the exact block sums:
 //   |Bt_b - B_b| <= g63 B_b, so B_b <= Bt_b / (1 - g63) =: Bu_b;
 //   |e_blk - sum Bt_b| <= u (1 + g64) sum_b (Bt_0 + .. + Bt_b)   (one rounding per block fold step);
