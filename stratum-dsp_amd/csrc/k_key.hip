@@ -435,6 +435,17 @@ struct HpcpFrame {
                 bool gt[KCAP];
 #pragma unroll
                 for (int q = 0; q < KCAP; q++) gt[q] = m1 > pm[q];
+#ifndef SDSP_HPCP_SELECT_PM
+                // the magnitudes: slot q takes the median of {pm[q], m1, pm[q-1]} (pm[q-1] >= pm[q]:
+                // that is pm[q] if m1 <= pm[q], m1 between the two, pm[q-1] if m1 > pm[q-1]), one
+                // v_med3 instead of two selects; exact, every operand is a number (m1 > thr >= -1)
+#pragma unroll
+                for (int q = KCAP - 1; q >= 1; q--) {
+                    const int nbv = gt[q - 1] ? pb[q - 1] : c;
+                    pm[q] = __builtin_amdgcn_fmed3f(pm[q], m1, pm[q - 1]);
+                    pb[q] = gt[q] ? nbv : pb[q];
+                }
+#else
 #pragma unroll
                 for (int q = KCAP - 1; q >= 1; q--) {
                     const float nv = gt[q - 1] ? pm[q - 1] : m1;
@@ -442,6 +453,7 @@ struct HpcpFrame {
                     pm[q] = gt[q] ? nv : pm[q];
                     pb[q] = gt[q] ? nbv : pb[q];
                 }
+#endif
                 pm[0] = gt[0] ? m1 : pm[0];
                 pb[0] = gt[0] ? c : pb[0];
                 thr = pm[KCAP - 1];
