@@ -311,9 +311,9 @@ __device__ __forceinline__ void topk_insert(float (&pm)[KCAP], int (&pb)[KCAP], 
     for (int q = 0; q < KCAP; q++) gt[q] = v > pm[q];
 #pragma unroll
     for (int q = KCAP - 1; q >= 1; q--) {
-        const float nv = gt[q - 1] ? pm[q - 1] : v;
+        // magnitudes: the median of {pm[q], v, pm[q-1]} (the list is descending; v > thr is a number)
         const int nbv = gt[q - 1] ? pb[q - 1] : vb;
-        pm[q] = gt[q] ? nv : pm[q];
+        pm[q] = __builtin_amdgcn_fmed3f(pm[q], v, pm[q - 1]);
         pb[q] = gt[q] ? nbv : pb[q];
     }
     pm[0] = gt[0] ? v : pm[0];
