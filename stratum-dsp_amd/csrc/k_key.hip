@@ -1011,6 +1011,11 @@ __device__ __noinline__ double kc_clarity(const float* raw, const float* SS, con
 #ifndef KV_SMALL_ITEMS
 #define KV_SMALL_ITEMS 96
 #endif
+#ifdef SDSP_KV_PROF
+#define KV_T(i) do { if (threadIdx.x == 0) kv_t[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define KV_T(i) do { } while (0)
+#endif
 template <int NT>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_key_vote(const int* __restrict__ tracks, int n_items,
                                                   const uint64_t* __restrict__ frame_pfx, float* __restrict__ chroma_raw,
@@ -1038,6 +1043,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
     __shared__ double kc_red[NT / 64];
     __shared__ float kc_crs;  // the common factor's relative range (the median's), for absolute thresholds
     const bool cert = P.near_check && !P.cert_fixed && edel && wdel;
+#ifdef SDSP_KV_PROF
+    uint64_t kv_t[12] = {};
+#endif
+    KV_T(0);
     const int it = blockIdx.x;
     const int trk = tracks[it];
     const int64_t F_all = (int64_t)(frame_pfx[trk + 1] - frame_pfx[trk]);
@@ -1123,6 +1132,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
         }
     }
     __syncthreads();
+    KV_T(1);
     // optional edge trim (src/lib.rs:1215-1232): keep the middle frames
     int64_t t0 = 0, F = F_all;
     if (P.edge_trim && F_all >= 200) {
@@ -1143,7 +1153,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
     if (P.weighting) {
         const float med = sd_maxf(block_select_kth(en, (int)F, (int)(F / 2), hist, misc), 1e-12f);
         const float ln12 = sd_logf(12.0f);
-        int used_local = 0;
+        int used_local = 0, rng_local = 0;
+        uint32_t dmax_local = 0u, emax_local = 0u;
         for (int64_t f = threadIdx.x; f < F; f += blockDim.x) {
             const float* ch = cs + f * 12;
             float sum = 0.0f;
@@ -1171,9 +1182,18 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 // an energy whose quotient or weight could underflow on one side only, or no bound
                 if (!(d < 0.25) || (en[f] > 0.0f && !(e_norm >= 0x1p-100f) && we != 1.0f) ||
                     (ww > 0.0f && !(ww >= 0x1p-100f)) || !(ww < 0x1p100f))
-                    atomicOr(&near_s, KV_NEAR_RANGE);
-                atomicMax(&kc_dmax, __float_as_uint((float)d));
-                atomicMax(&kc_emax, __float_as_uint(kc_up(eta)));
+                    rng_local = 1;
+                dmax_local = max(dmax_local, __float_as_uint((float)d));
+                emax_local = max(emax_local, __float_as_uint(kc_up(eta)));
+            }
+        }
+        if (cert) {  // one LDS atomic per wave (the maxima of non-negative floats as bit patterns)
+            const uint32_t dm = wave_max_u32(dmax_local), em = wave_max_u32(emax_local);
+            const bool rg = __builtin_amdgcn_ballot_w64(rng_local != 0) != 0;
+            if ((threadIdx.x & 63) == 0) {
+                if (rg) atomicOr(&near_s, KV_NEAR_RANGE);
+                atomicMax(&kc_dmax, dm);
+                atomicMax(&kc_emax, em);
             }
         }
         const int used = block_sum_i(used_local, redi);
@@ -1198,6 +1218,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
         use_w_s = 0;
     }
     __syncthreads();
+    KV_T(2);
     const bool use_w = use_w_s;
     const int toff = P.tset == 1 ? 24 : 0;  // template rows of the selected set
     if (dbg) {  // debug_track_id: weighted pitch-class sums over the slice, in frame order (src/lib.rs:1473-1491)
@@ -1473,6 +1494,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
             S[(size_t)(q / 13) * KV_ROW + (i == 12 ? 51 : 52 + i)] = avg_sum(st, len, i);
         }
     __syncthreads();
+    KV_T(3);
     for (int sg = threadIdx.x; sg < nseg; sg += blockDim.x) {
         float* row = S + (size_t)sg * KV_ROW;
         float raw[24], sorted[24];
@@ -1516,7 +1538,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
         row[50] = cl * sw;
     }
     __syncthreads();
+    KV_T(4);
     if (kc2) kc_pair_pass();
+    KV_T(5);
     if (threadIdx.x < 24) {
         const int key = threadIdx.x;
         float a = 0.0f;
@@ -1546,6 +1570,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
         totw_s = tw;
     }
     __syncthreads();
+    KV_T(6);
     const int used = used_s;
     const float totw = totw_s;
     if (used == 0 || (mode == 1 && totw <= 1e-12f)) {
@@ -1600,6 +1625,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
         write_out(order[0], conf, clarity_of(sorted), used);
         put_dbg(sorted, order, order[0]);
     }
+    KV_T(7);
+#ifdef SDSP_KV_PROF
+    if (threadIdx.x == 0 && (blockIdx.x % 64) == 0)
+        printf("kvprof blk %d nseg %d smooth %.1f weights %.1f segs %.1f segkey %.1f pair %.1f acc %.1f final %.1f us\n",
+               (int)blockIdx.x, nseg, (kv_t[1] - kv_t[0]) * 0.01, (kv_t[2] - kv_t[1]) * 0.01, (kv_t[3] - kv_t[2]) * 0.01,
+               (kv_t[4] - kv_t[3]) * 0.01, (kv_t[5] - kv_t[4]) * 0.01, (kv_t[6] - kv_t[5]) * 0.01, (kv_t[7] - kv_t[6]) * 0.01);
+#endif
 }
 
 // ---- launchers ----
@@ -1678,12 +1710,13 @@ void launch_hpcp(const float* mags, const uint64_t* frame_pfx, const uint64_t* t
 void launch_key_vote(const int* tracks, int n_items, const uint64_t* frame_pfx, float* chroma_raw,
                      const float* energy, float* chroma_s, float* weights, float* seg_scratch, const uint64_t* seg_off,
                      const float* tmpl, const KeyParams& P, KeyOut* out, hipStream_t st, KeyDbg* dbg,
-                     const float* edel, float* wdel) {
+                     const float* edel, float* wdel, bool alone) {
     if (n_items == 0) return;
-    // a few tracks (the exact reruns of near-decision tracks, one-track calls): the latency of one
-    // track's workgroup is the launch, and 1024 threads cut it (the segment scores in one round
-    // instead of three); full sub-batches keep 256 threads, which fit beside the key-stream STFT
-    if (n_items <= KV_SMALL_ITEMS)
+    // a few tracks (the exact reruns of near-decision tracks, one-track calls) or a launch with
+    // nothing beside it (the call's last sub-batch, `alone`): the latency of one track's workgroup
+    // is the launch, and 1024 threads cut it (the segment scores in one round instead of three);
+    // other sub-batches keep 256 threads, which fit beside the key-stream STFT
+    if (n_items <= KV_SMALL_ITEMS || alone)
         hipLaunchKernelGGL(k_key_vote<1024>, dim3(n_items), dim3(1024), 0, st, tracks, n_items, frame_pfx, chroma_raw,
                            energy, chroma_s, weights, seg_scratch, seg_off, tmpl, P, out, dbg, edel, wdel);
     else

@@ -370,7 +370,7 @@ void launch_hpcp(const float* mags, const uint64_t* frame_pfx, const uint64_t* t
 void launch_key_vote(const int* tracks, int n_items, const uint64_t* frame_pfx, float* chroma_raw,
                      const float* energy, float* chroma_s, float* weights, float* seg_scratch, const uint64_t* seg_off,
                      const float* tmpl, const KeyParams& P, KeyOut* out, hipStream_t st, KeyDbg* dbg = nullptr,
-                     const float* edel = nullptr, float* wdel = nullptr);
+                     const float* edel = nullptr, float* wdel = nullptr, bool alone = false);
 void launch_synth(float* out, uint64_t n_tracks, uint64_t len, uint32_t sr, const float* bpm, const int* key,
                   uint64_t seed0, hipStream_t st);
 void launch_synth_normalize(float* out, uint64_t n_tracks, uint64_t len, unsigned int* peak_bits, hipStream_t st);

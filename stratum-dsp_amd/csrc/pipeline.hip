@@ -867,6 +867,8 @@ class Pipeline {
     // a rerun started from inside the main pass (rerun_near): its buffers carry the prefix "X."
     // and its key path runs on the main stream, in that stream's slack beside the key stream
     bool nested_ = false;
+    // the sub-batch being run is the call's last (its key vote runs alone at the tail)
+    bool last_sub_ = false;
     uint64_t reruns_ = 0;
     double rerun_ms_ = 0.0;
     void rerun_near(const float* d_samples, const std::vector<uint64_t>& in_off, const std::vector<uint64_t>& n_raw,
@@ -948,6 +950,7 @@ void Pipeline::run(const float* d_samples, const std::vector<uint64_t>& in_off, 
         acc = 0;
     };
     times_ = sdsp_stage_times{};
+    last_sub_ = false;
     auto t0 = std::chrono::steady_clock::now();
     if (cfg_.enable_normalization && cfg_.normalization != SDSP_NORM_PEAK && why.empty())
         loudness_prepass(d_samples, in_off, n_raw, res);
@@ -980,7 +983,9 @@ void Pipeline::run(const float* d_samples, const std::vector<uint64_t>& in_off, 
         acc += need[i];
         cum += need[i];
     }
+    last_sub_ = true;
     flush();
+    last_sub_ = false;
     finish_key(res);  // the last sub-batch's near tracks are rerun by run_locked
     times_.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     times_.key_reruns = reruns_;  // in-flight reruns (rerun_near), their time inside total_ms
@@ -1851,8 +1856,9 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         SDSP_HIP_CHECK(hipStreamWaitEvent(st3, kt.ev[11], 0));
         d_kdbg = dbg_on ? c_.dev<KeyDbg>(EP + "kdbg", (size_t)NK) : nullptr;
         float* d_wdel = d_edel ? c_.dev<float>("E.wdel", total8) : nullptr;
+        // the call's last sub-batch votes with nothing beside it on the chip (its tail)
         launch_key_vote(d_kid, NK, d_kpfx, d_chroma, d_energy, d_cs, d_w, d_sscr, d_kseg, d_tpl, kp, d_kout, st3, d_kdbg,
-                        d_edel, d_wdel);
+                        d_edel, d_wdel, last_sub_ || nested_ || key_only_);
         SDSP_HIP_CHECK(hipGetLastError());
         kt.mark(2, st3);
         if (!nested_) SDSP_HIP_CHECK(hipEventRecord(d_.vote_done, st3));
@@ -2357,7 +2363,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
             sb_off.push_back(bpfx[(size_t)i]);
             const uint64_t rows = (uint64_t)nb - 1;
             rpfx.push_back(rpfx.back() + rows);
-            sseg.push_back(sseg.back() + 64 * seg_rows(rows));
+            sseg.push_back(sseg.back() + (uint64_t)KV_ROW * seg_rows(rows));
         }
         const int NS = (int)sel.size();
         if (NS > 0) {

@@ -112,6 +112,20 @@ def test_chroma_option_sample_rates(case, sr):
     _run(case, xs, sr)
 
 
+def test_beat_sync_segment_rows():
+    """Beat-synchronous chroma with segments short enough that each track's beat rows make several
+    segments (key_segment_len_frames is counted in beat rows there): the vote's per-track segment
+    scratch is laid out in KV_ROW-float rows, so the tracks' rows must not overlap (round 6 fixed
+    this path's scratch offsets, which still counted 64 floats per row)."""
+    CASES["beat_sync_short_segments"] = dict(enable_key_beat_synchronous=1, key_segment_len_frames=120,
+                                             key_segment_hop_frames=20)
+    try:
+        xs = [synth.make_track(s, seconds=sec)[0] for s, sec in ((61, 100.0), (67, 75.0), (71, 130.0))]
+        got, refs = _run("beat_sync_short_segments", xs)
+    finally:
+        del CASES["beat_sync_short_segments"]
+
+
 def test_chroma_options_change_results():
     """The front-ends are live: most cases change some key result against the default config."""
     xs = tracks()
