@@ -1716,8 +1716,19 @@ void launch_key_vote(const int* tracks, int n_items, const uint64_t* frame_pfx, 
     // nothing beside it (the call's last sub-batch, `alone`): the latency of one track's workgroup
     // is the launch, and 1024 threads cut it (the segment scores in one round instead of three);
     // other sub-batches keep 256 threads, which fit beside the key-stream STFT
-    if (n_items <= KV_SMALL_ITEMS || alone)
+    // (a 1,024-thread workgroup fills its CU's 4 waves per SIMD: more tracks than CUs take two
+    // rounds, so a lone launch of more tracks than CUs runs 512 threads, two workgroups per CU)
+    int cus = 0;
+    if (alone && n_items > KV_SMALL_ITEMS) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 0;
+    }
+    if (n_items <= KV_SMALL_ITEMS || (alone && n_items <= cus))
         hipLaunchKernelGGL(k_key_vote<1024>, dim3(n_items), dim3(1024), 0, st, tracks, n_items, frame_pfx, chroma_raw,
+                           energy, chroma_s, weights, seg_scratch, seg_off, tmpl, P, out, dbg, edel, wdel);
+    else if (alone)
+        hipLaunchKernelGGL(k_key_vote<512>, dim3(n_items), dim3(512), 0, st, tracks, n_items, frame_pfx, chroma_raw,
                            energy, chroma_s, weights, seg_scratch, seg_off, tmpl, P, out, dbg, edel, wdel);
     else
         hipLaunchKernelGGL(k_key_vote<KV_THREADS>, dim3(n_items), dim3(KV_THREADS), 0, st, tracks, n_items, frame_pfx,

@@ -8,7 +8,7 @@ cd /tmp && export TMPDIR=/tmp
 for v in "$@"; do
   if [ "$v" = base ]; then unset SDSP_LIB_PATH; else export SDSP_LIB_PATH=$R/stratum-dsp_amd/lib_exp/lib_$v.so; fi
   O=$R/gpurun_out/ab_${tag}_$v
-  SDSP_SERIAL_STREAMS=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O -o s -- python3 $R/bench.py --tracks 256 --steps 1 --warmup 1 --no-cpu-baseline > $O.json 2> $O.err || { echo "$v failed"; tail -5 $O.err; exit 1; }
+  SDSP_SERIAL_STREAMS=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O -o s -- python3 $R/bench.py --tracks ${AB_TRACKS:-256} --steps 1 --warmup 1 --no-cpu-baseline > $O.json 2> $O.err || { echo "$v failed"; tail -5 $O.err; exit 1; }
   python3 - "$O/s_kernel_stats.csv" "$rx" "$v" <<'PY'
 import csv, re, sys
 for r in csv.DictReader(open(sys.argv[1])):
