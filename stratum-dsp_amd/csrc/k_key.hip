@@ -205,7 +205,7 @@ __global__ __launch_bounds__(MASK_T) __attribute__((amdgpu_waves_per_eu(4, 4))) 
                                                      const uint64_t* __restrict__ frame_pfx,
                                                      const int* __restrict__ tracks, int blocks_per_track,
                                                      float power, int st_lo, int st_hi, float* __restrict__ part,
-                                                     uint64_t total) {
+                                                     uint64_t total, int outside) {
     constexpr int R = 2 * M + 2, RX = M + 1;
     static_assert(M >= 1 && 2 * M + 1 <= 25 && R <= MASK_T, "fast window division validated for 3..25");
     __shared__ float tile[R][MASK_T + 1];
@@ -216,8 +216,11 @@ __global__ __launch_bounds__(MASK_T) __attribute__((amdgpu_waves_per_eu(4, 4))) 
     const int b = gblk * MASK_T + lane;
     const int64_t F = (int64_t)(frame_pfx[trk + 1] - frame_pfx[trk]);
     if (F <= 0) return;  // the whole workgroup
+    // outside: store the bins outside [st_lo, st_hi] instead (the exact rerun's completion of a
+    // spectrogram whose band already holds masked values); a block wholly inside stores nothing
+    if (outside && gblk * MASK_T >= st_lo && gblk * MASK_T + MASK_T - 1 <= st_hi) return;
     const bool live = b < B;
-    const bool keep = live && b >= st_lo && b <= st_hi;
+    const bool keep = live && (outside ? (b < st_lo || b > st_hi) : (b >= st_lo && b <= st_hi));
     // Rows are addressed through buffer resources whose base is the row (wave-uniform, advanced in
     // SGPRs) and lane offsets in VGPRs: no 64-bit address arithmetic per element.  A store
     // resource spans one row (B floats) and the lanes off HPCP's band carry an offset past it, so
@@ -1664,11 +1667,11 @@ void launch_mask(float* mags, int stride, int B, const uint64_t* frame_pfx, cons
 }
 bool mask_band_ok(int margin, float power) { return margin == 12 && sd_maxf(power, 1.0f) == 2.0f; }
 void launch_mask_band(float* mags, int stride, int B, const uint64_t* frame_pfx, const int* tracks, int n_items,
-                      float power, int st_lo, int st_hi, float* part, uint64_t total, hipStream_t st) {
+                      float power, int st_lo, int st_hi, float* part, uint64_t total, hipStream_t st, bool outside) {
     if (n_items == 0) return;
     const int bpt = (B + MASK_T - 1) / MASK_T;
     hipLaunchKernelGGL((k_mask_rp<12, 2>), dim3(n_items * bpt), dim3(MASK_T), 0, st, mags, stride, B, frame_pfx, tracks,
-                       bpt, power, st_lo, st_hi, part, total);
+                       bpt, power, st_lo, st_hi, part, total, outside ? 1 : 0);
 }
 void launch_hpcp_band(const float* mags, const uint64_t* frame_pfx, const uint64_t* tile_pfx, const int* tracks,
                       int n_items, uint64_t n_tiles, const HpcpParams& P, const HarmEntry* harm, const float* part,

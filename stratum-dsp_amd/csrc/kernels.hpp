@@ -360,7 +360,8 @@ void launch_beat_sync(const int* tracks, int n_items, const uint64_t* frame_pfx,
 // (k_key.hip k_mask_rp / k_hpcp_band; only for margin 12, power 2)
 bool mask_band_ok(int margin, float power);
 void launch_mask_band(float* mags, int stride, int B, const uint64_t* frame_pfx, const int* tracks, int n_items,
-                      float power, int st_lo, int st_hi, float* part, uint64_t total, hipStream_t st);
+                      float power, int st_lo, int st_hi, float* part, uint64_t total, hipStream_t st,
+                      bool outside = false);
 void launch_hpcp_band(const float* mags, const uint64_t* frame_pfx, const uint64_t* tile_pfx, const int* tracks,
                       int n_items, uint64_t n_tiles, const HpcpParams& P, const HarmEntry* harm, const float* part,
                       uint64_t total, float* chroma, float* energy, float* edel, hipStream_t st);

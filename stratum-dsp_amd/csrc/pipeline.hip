@@ -893,14 +893,34 @@ class Pipeline {
     // holding the main stream back.  Uploads read by the key stream and the key output live in
     // per-parity buffers (E0.*, E1.*); the key stream itself is in order, so its big buffers are
     // shared.
+    // The band path's state of a sub-batch for the exact rerun in place (rerun_tail): its key
+    // spectrogram (band masked in place, every other bin the STFT's), its chroma and vote buffers.
+    // Valid for the call's last sub-batch only (the next sub-batch's key stream reuses them).
+    struct KeyTail {
+        bool ok = false;
+        float* mags8 = nullptr;
+        uint64_t* d_kpfx = nullptr;
+        std::vector<uint64_t> kpfx, kseg;  // frame and segment-scratch prefixes over the key tracks
+        float* d_part = nullptr;
+        uint64_t total8 = 0;
+        int st_lo = 0, st_hi = -1, B8 = 0;
+        HpcpParams hp{};
+        const HarmEntry* d_ht = nullptr;
+        float *d_chroma = nullptr, *d_energy = nullptr, *d_cs = nullptr, *d_w = nullptr, *d_sscr = nullptr;
+        const float* d_tpl = nullptr;
+        KeyParams kp{};
+    };
     struct KeyPending {
         std::unique_ptr<Timers> kt;
         KeyOut* d_kout = nullptr;
         std::vector<size_t> at;  // result slot of each key track
+        KeyTail tail;
     };
     std::unique_ptr<KeyPending> key_pending_;
+    std::unique_ptr<KeyPending> tail_;  // the last sub-batch's pending join, kept for rerun_tail
     int sb_parity_ = 0;
-    std::vector<size_t> finish_key(std::vector<TrackRes>& res);
+    std::vector<size_t> finish_key(std::vector<TrackRes>& res, bool keep_tail = false);
+    void rerun_tail(const std::vector<size_t>& near, std::vector<TrackRes>& res);
     void tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPassOut& out);
     void legacy_select(const TempoPassIn& bin, const uint32_t* d_onsets, const uint64_t* d_on_off, const int* d_on_n,
                        const std::vector<int>& R, const std::vector<int>& idx, std::vector<TrackRes>& res,
@@ -986,7 +1006,9 @@ void Pipeline::run(const float* d_samples, const std::vector<uint64_t>& in_off, 
     last_sub_ = true;
     flush();
     last_sub_ = false;
-    finish_key(res);  // the last sub-batch's near tracks are rerun by run_locked
+    // the last sub-batch's near tracks: rerun in place when its band-path buffers are intact,
+    // otherwise by run_locked
+    rerun_tail(finish_key(res, true), res);
     times_.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     times_.key_reruns = reruns_;  // in-flight reruns (rerun_near), their time inside total_ms
     times_.rerun_ms = rerun_ms_;
@@ -1454,7 +1476,7 @@ void Pipeline::tempo_pass(const std::string& tag, const TempoPassIn& in, TempoPa
 namespace sdsp {
 
 // SDSP_HOST_TRACE=1: host wall time between the sub-batch's synchronisation points (stderr)
-std::vector<size_t> Pipeline::finish_key(std::vector<TrackRes>& res) {
+std::vector<size_t> Pipeline::finish_key(std::vector<TrackRes>& res, bool keep_tail) {
     std::vector<size_t> near;
     if (!key_pending_) return near;
     std::unique_ptr<KeyPending> kp = std::move(key_pending_);
@@ -1473,7 +1495,65 @@ std::vector<size_t> Pipeline::finish_key(std::vector<TrackRes>& res) {
     }
     times_.stft8192_ms += kp->kt->ms(0, 1);
     times_.key_ms += kp->kt->ms(1, 2);
+    if (keep_tail && kp->tail.ok) tail_ = std::move(kp);
     return near;
+}
+
+// The exact key rerun of the call's last sub-batch's near-decision tracks, in place:
+// the reference's sequential frame-energy fold needs every masked bin, and the band path stored only
+// HPCP's band.  The bins outside it still hold the STFT's magnitudes, so k_mask_rp completes the
+// masked spectrogram there (the same masked values the nested rerun's full-bin mask stores), k_hpcp
+// folds each frame's energy in bin order (and rewrites the same chroma), and the vote runs on the
+// exact energies: the nested rerun's results without its front end and 8192-point STFT.
+void Pipeline::rerun_tail(const std::vector<size_t>& near, std::vector<TrackRes>& res) {
+    std::unique_ptr<KeyPending> kp = std::move(tail_);
+    if (near.empty() || !kp || exact_energy_ || nested_) return;
+    const KeyTail& t = kp->tail;
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<int> sel;
+    for (size_t i : near)
+        for (size_t k = 0; k < kp->at.size(); k++)
+            if (kp->at[k] == i) sel.push_back((int)k);
+    if (sel.size() != near.size()) throw HipError("rerun_tail: a near track is not in the last sub-batch");
+    const int n = (int)sel.size();
+    std::vector<uint64_t> tp(1, 0), sp(1, 0);
+    for (int k : sel) {
+        const uint64_t F = t.kpfx[(size_t)k + 1] - t.kpfx[(size_t)k];
+        tp.push_back(tp.back() + (F + HP_FRAMES - 1) / HP_FRAMES);
+        sp.push_back(sp.back() + (t.kseg[(size_t)k + 1] - t.kseg[(size_t)k]));
+    }
+    hipStream_t st = d_.stream;
+    int* d_sel = c_.up("E.tail_sel", sel);
+    uint64_t* d_tp = c_.up("E.tail_tile", tp);
+    uint64_t* d_sp = c_.up("E.tail_seg", sp);
+    launch_mask_band(t.mags8, ks_, t.B8, t.d_kpfx, d_sel, n, cfg_.key_harmonic_mask_power, t.st_lo, t.st_hi, t.d_part,
+                     t.total8, st, true);
+    SDSP_HIP_CHECK(hipGetLastError());
+    launch_hpcp(t.mags8, t.d_kpfx, d_tp, d_sel, n, tp.back(), t.hp, t.d_ht, t.d_chroma, t.d_energy, st);
+    SDSP_HIP_CHECK(hipGetLastError());
+    KeyParams kx = t.kp;
+    kx.near_check = 0;  // the exact energies: nothing left to certify
+    // (the vote writes out[track], so the selected tracks' entries of the sub-batch's KeyOut array)
+    launch_key_vote(d_sel, n, t.d_kpfx, t.d_chroma, t.d_energy, t.d_cs, t.d_w, t.d_sscr, d_sp, t.d_tpl, kx, kp->d_kout,
+                    st, nullptr, nullptr, nullptr, true);
+    SDSP_HIP_CHECK(hipGetLastError());
+    const std::vector<KeyOut> ko = c_.down(kp->d_kout, kp->at.size());
+    for (int j = 0; j < n; j++) {
+        TrackRes& r = res[near[(size_t)j]];
+        const KeyOut& o = ko[(size_t)sel[(size_t)j]];
+        if (!o.ok) {
+            r.status = SDSP_ERR_PROCESSING;
+            r.err = "Processing error: key certification rerun failed (no key from the exact energies)";
+            continue;
+        }
+        r.key_mode = o.mode;
+        r.key_tonic = o.tonic;
+        r.key_conf = o.conf;
+        r.key_clarity = o.clarity;
+        r.key_rerun = true;
+    }
+    reruns_ += (uint64_t)n;
+    rerun_ms_ += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
 // The exact key rerun of near-decision tracks for a finished sub-batch, from inside
@@ -1695,6 +1775,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
     int* d_kid = nullptr;
     float* d_tpl = nullptr;
     KeyParams kp{};
+    KeyTail ktail;  // the band path's state for rerun_tail
     const int B8 = KFS / 2 + 1;
     const float fres8 = (float)sr_ / (float)KFS;
     if (NK > 0) {
@@ -1797,6 +1878,7 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
             std::vector<HarmEntry> ht =
                 harm_table(B8, sr_, KFS, cfg_.soft_mapping_sigma, hp.hmax, cfg_.key_hpcp_harmonic_decay);
             HarmEntry* d_ht = c_.up(EP + "harm", ht);
+            ktail.d_ht = d_ht;
             // the table upload is queued on the main stream: order the key stream after it
             kt.mark(10);
             SDSP_HIP_CHECK(hipStreamWaitEvent(st2, kt.ev[10], 0));
@@ -1849,6 +1931,25 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         float* d_w = c_.dev<float>("E.weights", total8);
         float* d_sscr = c_.dev<float>("E.segscr", std::max<uint64_t>(kseg.back(), 1));
         d_kout = c_.dev<KeyOut>(EP + "kout", (size_t)NK);
+        if (band && ktail.d_ht) {
+            ktail.ok = true;
+            ktail.mags8 = mags8;
+            ktail.d_kpfx = d_kpfx;
+            ktail.kpfx = kpfx;
+            ktail.kseg = kseg;
+            ktail.d_part = d_part;
+            ktail.total8 = total8;
+            ktail.st_lo = hp.pk_lo - 1;
+            ktail.st_hi = hp.pk_hi + 1;
+            ktail.B8 = B8;
+            ktail.hp = hp;
+            ktail.d_chroma = d_chroma;
+            ktail.d_energy = d_energy;
+            ktail.d_cs = d_cs;
+            ktail.d_w = d_w;
+            ktail.d_sscr = d_sscr;
+            ktail.d_tpl = d_tpl;
+        }
         // the template upload above is on the main stream too; the vote follows the chroma on st2
         kt.mark(8);
         kt.mark(11, st2);
@@ -2329,6 +2430,8 @@ void Pipeline::sub_batch(const float* d_samples, const std::vector<uint64_t>& in
         key_pending_->kt = std::move(ktp);
         key_pending_->d_kout = d_kout;
         for (int k = 0; k < NK; k++) key_pending_->at.push_back((size_t)idx[(size_t)R[(size_t)K[(size_t)k]]]);
+        ktail.kp = kp;
+        key_pending_->tail = std::move(ktail);
     } else if (NK > 0) {  // join the key stream
         SDSP_HIP_CHECK(hipStreamWaitEvent(st, kt.ev[2], 0));
         kout = c_.down(d_kout, (size_t)NK);
