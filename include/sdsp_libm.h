@@ -318,9 +318,11 @@ SD_HD float sd_ln1p_x_t2(float x, const sd_logtab2_t* tab) {
  * with k the mantissa's offset from c's (14 bits, or negative for i >= 212) and s = (1/c) 2^-23 or
  * 2^-24 from include/sdsp_logtab9.h; ln(1 + r) by its degree-4 Taylor polynomial (|r| < 2^-9); and
  * e ln 2 from a per-exponent pair {e LN2_HI (exact: LN2_HI has 21 trailing zero bits), RN(e LN2_LO)},
- * so the sum is three double additions: 10 double operations instead of 13.  Bit-identical to
- * sd_logf_ge1 on every finite f32 >= 1 (tools/check_logf_ge1.c, exhaustive; the same check finds 634
- * differences with a degree-3 polynomial, 22 with an 8-bit table).  x = +inf is the caller's select. */
+ * so the sum is three double additions: 10 double operations instead of 13.  Round 6: the
+ * polynomial's last product and the table term's addition are one FMA, ln c + r q(r) rounded once
+ * (9 double operations).  Bit-identical to sd_logf_ge1 on every finite f32 >= 1
+ * (tools/check_logf_ge1.c, exhaustive, for both forms; the same check finds 634 differences with a
+ * degree-3 polynomial, 22 with an 8-bit table).  x = +inf is the caller's select. */
 #include "sdsp_logtab9.h"
 #define SD_LOGTAB9_PIV 212
 typedef struct {
@@ -349,9 +351,8 @@ SD_HD float sd_ln1p_x_t9_finite(float x, const sd_logtab2_t* tab, const sd_ln2ta
     p = __builtin_fma(p, r, 1.0 / 3.0);
     p = __builtin_fma(p, r, -0.5);
     p = __builtin_fma(p, r, 1.0);
-    p = p * r;
     const sd_ln2tab_t E = et[e];
-    return (float)(E.hi + (E.lo + (t.lg + p)));
+    return (float)(E.hi + (E.lo + __builtin_fma(p, r, t.lg)));
 }
 
 /* f32::log10 */
@@ -496,6 +497,24 @@ SD_HD float sd_powf(float x, float y) {
     }
     if (!sd_isfinite_f(x)) return y > 0.0f ? SD_INF_F : 0.0f;
     return (float)sd_exp_d((double)y * sd_log_d((double)x));
+}
+
+/* x^0.5 as sd_powf(x, 0.5f) computes it, by the correctly rounded square root where that is provably
+ * the same value (round 6; HPCP's peak weights at the default magnitude power 0.5): sd_powf rounds a
+ * double exp(0.5 log x) once, which equals sqrt(x)'s correct rounding unless sqrt(x) lies within
+ * ~2^-25 ulp of a rounding midpoint (48 of the 2^31 non-negative inputs).  With s the correctly
+ * rounded sqrt, x - s^2 is exact in one FMA and |x - s^2| / (s ulp(s)) measures the distance to the
+ * midpoint, so s is taken when that ratio is below 1 - 2^-20 and x lies in [2^-100, 2^120) (no
+ * denormal intermediate); otherwise the caller evaluates sd_powf.  tools/check_powf_half.c checks
+ * every non-negative f32 (0 differences; 294 M inputs, all but a handful outside the range, take
+ * sd_powf).  s must be the correctly rounded sqrtf(x). */
+SD_HD int sd_sqrt_is_powf_half(float x, float s) {
+    const uint32_t bx = sd_bits_f(x);
+    if (!(bx >= 0x0d800000u && bx < 0x7b800000u)) return 0;
+    const float e = __builtin_fmaf(-s, s, x);
+    const float u = sd_from_bits_f((sd_bits_f(s) & 0x7f800000u) - 0x0b800000u); /* ulp(s) */
+    const float lim = (s * u) * 0x1.ffffe0p-1f;
+    return (e < 0.0f ? -e : e) < lim;
 }
 
 /* f32::rem_euclid */

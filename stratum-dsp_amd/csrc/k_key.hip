@@ -476,7 +476,14 @@ struct HpcpFrame {
         for (int k = 0; k < KCAP; k++) {
             if (k >= P.K || !(pm[k] > 0.0f)) continue;
             const int bin = pb[k];
-            const float w0 = sd_powf_ool(sd_maxf(pm[k], 0.0f), P.p);
+            const float xk = sd_maxf(pm[k], 0.0f);
+            float w0;
+            if (P.p == 0.5f) {  // the default power: the correctly rounded sqrt where it is sd_powf's value
+                const float s = __builtin_sqrtf(xk);
+                w0 = sd_sqrt_is_powf_half(xk, s) ? s : sd_powf_ool(xk, 0.5f);
+            } else {
+                w0 = sd_powf_ool(xk, P.p);
+            }
             if (w0 <= 0.0f) continue;
             for (int h = 1; h <= P.hmax; h++) {
                 const HarmEntry he = harm[bin * HP_HMAX + (h - 1)];

@@ -130,3 +130,22 @@ def test_logf_ge1_two_column_table_exhaustive(tmp_path):
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=600)
     assert out.returncode == 0, out.stdout + out.stderr
     assert out.stdout.count(" 0 differ") == 3, out.stdout
+
+
+def test_sqrt_is_powf_half_exhaustive(tmp_path):
+    """HPCP's peak weights at the default power 0.5 take the correctly rounded sqrt where
+    sd_sqrt_is_powf_half admits it (round 6); on every non-negative f32 the admitted sqrt equals
+    sd_powf(x, 0.5f) bit for bit (tools/check_powf_half.c: 2.1e9 inputs, ~15 s on 8 threads).
+    sqrtf alone would differ on 48 inputs, all within 2^-20 of a rounding midpoint."""
+    import shutil
+    import subprocess
+    from pathlib import Path
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    root = Path(__file__).resolve().parents[1]
+    exe = tmp_path / "check_powf_half"
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-march=x86-64-v3", "-fopenmp",
+                    str(root / "tools" / "check_powf_half.c"), "-o", str(exe), "-lm"], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert " 0 differ" in out.stdout and "would differ on 48" in out.stdout, out.stdout
