@@ -485,7 +485,36 @@ struct HpcpFrame {
                 w0 = sd_powf_ool(xk, P.p);
             }
             if (w0 <= 0.0f) continue;
+#ifdef SDSP_HPCP_DIAG_NOHARM
+            pc[bin % 12][i] += w0;  // diagnostic timing build: no harmonic table walk (wrong chroma)
+            continue;
+#endif
+#ifndef SDSP_HPCP_HARM_SEQ
+            // the peak's first HU table entries (128 contiguous bytes) are loaded together, ahead of
+            // their use, instead of one dependent load per harmonic; the accumulation order is the
+            // same (h ascending, the walk ends at the first state-0 entry)
+            constexpr int HU = 4;
+            HarmEntry hv[HU];
+#pragma unroll
+            for (int h = 0; h < HU; h++)
+                if (h < P.hmax) hv[h] = harm[bin * HP_HMAX + h];
+            bool stop = false;
+#pragma unroll
+            for (int h = 0; h < HU; h++) {
+                if (stop || h >= P.hmax) break;
+                const HarmEntry& he = hv[h];
+                if (he.state == 0) {
+                    stop = true;
+                    break;
+                }
+                if (he.state == 1) continue;
+                const float contrib = w0 * he.hw;
+                for (int o = 0; o < 3; o++) pc[he.tc[o]][i] += contrib * he.wt[o];
+            }
+            for (int h = HU + 1; !stop && h <= P.hmax; h++) {
+#else
             for (int h = 1; h <= P.hmax; h++) {
+#endif
                 const HarmEntry he = harm[bin * HP_HMAX + (h - 1)];
                 if (he.state == 0) break;
                 if (he.state == 1) continue;
