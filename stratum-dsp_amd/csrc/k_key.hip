@@ -637,6 +637,25 @@ __device__ float energy_delta(const float* __restrict__ pp, uint64_t total, int 
     return d;
 }
 
+// energy_delta's bound from its terms accumulated in f32 (round 6): every term is >= 0 and every f32
+// operation rounds to nearest, so each computed sum or product is at least (1 - 2^-24)^m of its exact
+// value for the m <= 300 roundings on its path (the constants' included), and the computed bound
+// times (1 + 2^-14) is an upper bound of the exact one (300 * 2^-24 = 1.8e-5 < 2^-14 = 6.1e-5, the
+// final division's rounding included).  Outside e in [2^-60, 2^100] (no overflow; no denormal loses
+// more than 2^-141 absolute against a bound >= 2^-78) the double evaluation runs instead.
+constexpr float KC_IU_F = (float)(1.0 / (1.0 - 63.0 * 0x1p-24 / (1.0 - 63.0 * 0x1p-24)));
+__device__ float energy_delta_f32(float e_blk, float pu, float eref, float eo, const float* __restrict__ pp,
+                                  uint64_t total, int n_blocks, int B) {
+    if (!(e_blk > 0.0f)) return 0.0f;
+    if (!(e_blk >= 0x1p-60f && e_blk <= 0x1p100f)) return energy_delta(pp, total, n_blocks, B, e_blk);
+    const float u = 0x1p-24f;
+    const float g63 = 63.0f * u / (1.0f - 63.0f * u), g64 = 64.0f * u / (1.0f - 64.0f * u);
+    const float D = eref + u * (1.0f + u) * (1.0f + g64) * eo + g63 * pu;
+    const float r = (D / e_blk) * (1.0f + 0x1p-14f);
+    if (!(r < 1.0f)) return 1.0f;  // no usable bound; the vote flags it
+    return r;
+}
+
 // k_hpcp_band: k_hpcp after k_mask_rp.  The frame energy folds the 65 block sums part[g][frame] in
 // block order; the bin walk covers only the band k_mask_rp stored, [pk_lo - 1, pk_hi + 1] (the
 // local-maximum test of candidate c reads bins c - 1 .. c + 1; starting the walk at pk_lo - 1 with
@@ -671,11 +690,31 @@ __global__ __launch_bounds__(HP_FRAMES) SDSP_HPCP_ATTR void k_hpcp_band(const fl
     hf.init();
     if (valid) {
         const float* pp = part + g0 + (uint64_t)f;
+#ifndef SDSP_HPCP_EDEL_DOUBLE
+        // the frame energy (pt: the block sums folded in block order) and, in the same pass, the
+        // certificate's bound terms in f32 (energy_delta_f32)
+        const float u = 0x1p-24f;
+        const float gN = (float)P.B * u / (1.0f - (float)P.B * u);
+        const float c64 = 64.0f * u * (1.0f + u) * (1.0f + gN);
+        const float clast = (float)(P.B - 64 * (n_blocks - 1)) * u * (1.0f + u) * (1.0f + gN);
+        float pt = 0.0f, pu = 0.0f, eref = 0.0f, eo = 0.0f;
+        for (int g = 0; g < n_blocks; g++) {
+            const float bt = pp[(uint64_t)g * total];
+            pt += bt;
+            const float bu = bt * KC_IU_F;
+            pu += bu;
+            eref += __builtin_fminf(bu, (g + 1 < n_blocks ? c64 : clast) * pu);
+            eo += pt;
+        }
+        hf.e = pt;
+        if (edel) edel[g0 + (uint64_t)f] = energy_delta_f32(pt, pu, eref, eo, pp, total, n_blocks, P.B);
+#else
         float e = 0.0f;
         for (int g = 0; g < n_blocks; g++) e += pp[(uint64_t)g * total];
         hf.e = e;
         // the certificate's per-frame energy bound (k_key_vote, KeyParams::near_check)
         if (edel) edel[g0 + (uint64_t)f] = energy_delta(pp, total, n_blocks, P.B, e);
+#endif
     }
     const int w_lo = P.pk_lo - 1 > 0 ? P.pk_lo - 1 : 0, w_hi = P.pk_hi + 1 < P.B - 1 ? P.pk_hi + 1 : P.B - 1;
     // lane (r4, q4) stages bins 4 q4 .. 4 q4 + 3 of rows wrow + r4 + 16 u (u < 4), one 16-byte load
