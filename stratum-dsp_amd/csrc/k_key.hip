@@ -467,6 +467,7 @@ struct HpcpFrame {
     }
     // harmonic summation of the top-K peaks into 12 pitch classes (pc[q][i]: this thread's
     // column of an LDS scratch), L2 normalisation, and the frame's chroma row and energy at g
+    template <int HU = 4>
     __device__ __forceinline__ void finish(float (*pc)[HP_FRAMES], int i, const HpcpParams& P,
                                            const HarmEntry* __restrict__ harm, float* __restrict__ chroma,
                                            float* __restrict__ energy, uint64_t g) {
@@ -493,7 +494,6 @@ struct HpcpFrame {
             // the peak's first HU table entries (128 contiguous bytes) are loaded together, ahead of
             // their use, instead of one dependent load per harmonic; the accumulation order is the
             // same (h ascending, the walk ends at the first state-0 entry)
-            constexpr int HU = 4;
             HarmEntry hv[HU];
 #pragma unroll
             for (int h = 0; h < HU; h++)
@@ -663,6 +663,9 @@ __device__ float energy_delta_f32(float e_blk, float pu, float eref, float eo, c
 // own frames, so the waves run without workgroup barriers: a wave whose frames insert more peaks
 // does not hold the others at a barrier per chunk (a wave's LDS operations execute in order; a
 // wave-level fence keeps the staging writes and the walk's reads in program order).
+#ifndef SDSP_HPCP_BAND_HU
+#define SDSP_HPCP_BAND_HU 4
+#endif
 template <int KCAP>
 __global__ __launch_bounds__(HP_FRAMES) SDSP_HPCP_ATTR void k_hpcp_band(const float* __restrict__ mags,
                                                          const uint64_t* __restrict__ frame_pfx,
@@ -764,7 +767,7 @@ __global__ __launch_bounds__(HP_FRAMES) SDSP_HPCP_ATTR void k_hpcp_band(const fl
         hf.template walk<false>(tile[i], c0, w_hi + 1 - c0 < HPB_CW ? w_hi + 1 - c0 : HPB_CW, P);
     }
     if (!valid) return;
-    hf.finish(pcs, i, P, harm, chroma, energy, g0 + (uint64_t)f);
+    hf.template finish<SDSP_HPCP_BAND_HU>(pcs, i, P, harm, chroma, energy, g0 + (uint64_t)f);
 }
 
 // ----------------------------------------------------------------------------------------
