@@ -108,3 +108,24 @@ def test_rigorous_certificate_covers_fixed_margins():
         assert all(g[k] == e[k] for k in g if k not in parity.KEY_ENERGY_FIELDS), i
         if rig[i]:
             assert parity.exact_fraction(got[i], ref, strict=True) == 1.0, i
+
+
+def test_tail_rerun_in_place_equals_nested(monkeypatch):
+    """The last sub-batch's near-decision tracks are rerun in place (Pipeline::rerun_tail: the
+    mask completed outside HPCP's band, the exact energy fold, the vote) instead of by a nested
+    pipeline from the samples.  With the late key join off (SDSP_NO_KEY_DEFER) the same tracks take
+    the nested rerun; every result field must be identical, and so must the rerun count."""
+    n, L = 48, 180 * 44100
+    buf = sdsp.DeviceBuffer(n * L)
+    sdsp.generate_synthetic(buf.ptr, n, L, 44100, seed0=3000)
+    offs, lens = np.arange(n) * L, np.full(n, L)
+    monkeypatch.delenv("SDSP_NO_KEY_DEFER", raising=False)
+    got = sdsp.analyze_batch_device(buf.ptr, offs, lens, 44100)
+    st = sdsp.stage_times()
+    near = sdsp.last_key_near(n).copy()
+    monkeypatch.setenv("SDSP_NO_KEY_DEFER", "1")
+    ref = sdsp.analyze_batch_device(buf.ptr, offs, lens, 44100)
+    st_ref = sdsp.stage_times()
+    assert (near != 0).sum() > 0 and st["key_reruns"] == st_ref["key_reruns"] == int((near != 0).sum())
+    for i in range(n):
+        assert parity.result_digest(got[i]) == parity.result_digest(ref[i]), i
