@@ -16,6 +16,8 @@ namespace sdsp {
 
 constexpr int NACF_MAX = 512;
 constexpr int ACF_U = 16;  // k_acf_tempogram: fold steps loaded per block
+constexpr int ACF_CH = 4096;   // k_acf_tempogram: frames per LDS chunk
+constexpr int ACF_HMAX = 1024; // k_acf_tempogram: the largest lag the LDS path serves (its halo)
 
 // ----------------------------------------------------------------------------------------
 // Block-cooperative complex FFT, Stockham radix-4 (+radix-2) exactly as sdsp_fft_spec.h.
@@ -221,6 +223,46 @@ __global__ __launch_bounds__(256) void k_acf_tempogram(const int* __restrict__ i
     const float* x = nov + (uint64_t)v * total + frame_pfx[trk];
     int K2 = 1;
     while (K2 < NB) K2 <<= 1;
+#ifndef SDSP_ACF_GLOBAL
+    // The novelty is staged through LDS in ACF_CH-frame chunks with the largest lag as halo, and
+    // every lag's thread continues its fold across the chunks (i ascending, the same products in
+    // the same order): each step reads LDS instead of two vector-memory loads per element, which
+    // held the kernel at the texture unit's address rate.  Lags beyond the halo keep the global path.
+    __shared__ float xs[ACF_CH + ACF_HMAX];
+    __shared__ int lagmax_s;
+    if (threadIdx.x == 0) lagmax_s = 0;
+    __syncthreads();
+    int lm = 0;
+    for (int j = threadIdx.x; j < NB; j += blockDim.x) lm = max(lm, lag_grid[j]);
+    atomicMax(&lagmax_s, lm);
+    __syncthreads();
+    const int lagmax = lagmax_s;
+    if (NB <= (int)blockDim.x && lagmax >= 0 && lagmax <= ACF_HMAX) {
+        const int j = threadIdx.x;
+        const int64_t lag = j < NB ? lag_grid[j] : 0;
+        const int64_t n = j < NB ? L - lag : 0;  // terms i = 0 .. n-1
+        float acc = 0.0f;
+        for (int64_t c0 = 0; c0 < L; c0 += ACF_CH) {
+            const int64_t m = L - c0 < ACF_CH + lagmax ? L - c0 : ACF_CH + lagmax;  // x[c0 .. c0+m) staged
+            __syncthreads();  // the previous chunk's reads are done
+            for (int k = threadIdx.x; k < m; k += blockDim.x) xs[k] = x[c0 + k];
+            __syncthreads();
+            const int64_t e = n < c0 + ACF_CH ? n : c0 + ACF_CH;  // this chunk's terms: i in [c0, e)
+            const int cnt = e > c0 ? (int)(e - c0) : 0;
+            const float* xl = xs + lag;
+#pragma unroll 8
+            for (int i = 0; i < cnt; i++) acc += xs[i] * xl[i];
+        }
+        if (j < NB) {
+            const int32_t cnt = n > 0 ? (int32_t)n : 0;
+            const float sv = cnt > 0 ? acc / (float)cnt : 0.0f;
+            vals[j] = sv;
+            keys[j] = key_desc(sv, (uint32_t)j);
+        } else if (j < K2) {
+            keys[j] = ~0ull;  // K2 <= blockDim.x here (NB <= blockDim.x)
+        }
+    } else
+#endif
     for (int j = threadIdx.x; j < K2; j += blockDim.x) {
         uint64_t key = ~0ull;
         if (j < NB) {
